@@ -1,0 +1,245 @@
+"""Benchmark of the v18 embedding-RAG imputation hot path on MI355X.
+
+One step = one batch of B synthetic samples (2B query haplotypes) through:
+  retrieval: LUT -> int8-MFMA scan of the HBM-resident panel (N haplotypes x
+             window sites) -> exact top-k merge -> neighbour K-mean (rag_mean)
+  forward:   embedding + emb_fusion + rag_fusion + 12-block encoder + heads
+             (BERTFoundationModel eval forward, bf16 compute, f32 accumulation)
+Metric (BASELINE.json): masked SNVs imputed/s (2 * sum(mask) per sample-window),
+with kNN queries/s reported beside it.  Workload = configs[2] of BASELINE.json:
+window 1024 sites, k = 32, 1M-haplotype panel resident in HBM, d384/L12/H12.
+
+Launch: python bench.py --gpus 1 --steps K --warmup W   (N>1: torch.distributed.run,
+one rank per GPU; each rank imputes its own B samples against its own HBM copy of
+the panel -> weak scaling, no data-path collective).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "rag-snvbert_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (no sparsity)
+F32_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=64, help="samples per step per GPU")
+    p.add_argument("--n-ref", type=int, default=1_000_000, help="panel haplotypes")
+    p.add_argument("--window", type=int, default=1024, help="sites per window")
+    p.add_argument("--k", type=int, default=32)
+    p.add_argument("--dims", type=int, default=384)
+    p.add_argument("--layers", type=int, default=12)
+    p.add_argument("--heads", type=int, default=12)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--level", type=int, default=4, help="curriculum mask level (4 -> 50%%, rare 70%%)")
+    p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on host cores (rank 0)")
+    p.add_argument("--cpu-panel", type=int, default=65536, help="panel sample for the CPU kNN timing")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def make_queries(args, af_np, seed, rank):
+    """B samples whose haplotypes copy panel rows (hash-generated like the device panel) with 2% flips."""
+    from src.dataset.synthetic import hash_uniform
+    rng = np.random.default_rng([seed, rank])
+    B, S = args.batch, args.window
+    src = rng.integers(0, args.n_ref, size=(B, 2))
+    cols = np.arange(S)
+    alle = (hash_uniform(seed, src[..., None], cols[None, None]) < af_np[None, None]).astype(np.uint8)
+    alle ^= (rng.random(alle.shape) < 0.02).astype(np.uint8)
+    return alle, src
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device(f"cuda:{local}")
+    from src import kernels as K, native as N
+    from src.dataset import synthetic
+    from src.dataset import utils as U
+    from src.dataset.vocab import WordVocab
+    from src.engine import engine_for
+    from src.model import build_model
+    from src.retrieval import PanelIndex
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    vocab = WordVocab(synthetic.POPS)
+    torch.manual_seed(0)
+    model = build_model(len(vocab), args.dims, args.layers, args.heads).to(dev).eval()
+    eng = engine_for(model)
+    eng.set_dtype(dtype)
+    P = eng.packed()
+
+    # ---- window, panel (HBM-resident, generated on device), queries ----
+    S, B, L = args.window, args.batch, 1030
+    seed = 1234
+    rng = np.random.default_rng(seed)
+    af_np = rng.beta(0.3, 3.0, S).astype(np.float32)
+    pos = np.sort(rng.choice(np.arange(1, 50 * S), S, replace=False))
+    af_dev = torch.from_numpy(af_np).to(dev)
+    ref_af = U.sequence_padding(af_np, "float").astype(np.float32)
+    index = PanelIndex.synthetic(args.n_ref, S, af_dev, torch.from_numpy(ref_af).to(dev), seed)
+    raw_mask = U.af_guided_mask(af_np, args.level, 0, 0)
+    mask = U.sequence_padding(raw_mask, "int")
+    alle, _ = make_queries(args, af_np, seed, rank)
+    pad = lambda a: torch.from_numpy(np.stack([U.sequence_padding(r, "float") for r in a]).astype(np.float32)).to(dev)
+    afp = np.clip(af_np[None] + 0.05 * rng.standard_normal((B, S)), 0, 1)
+    x = dict(hap_1=torch.from_numpy(vocab.tokenize(alle[:, 0], mask)).to(dev),
+             hap_2=torch.from_numpy(vocab.tokenize(alle[:, 1], mask)).to(dev),
+             af=pad(np.broadcast_to(af_np, (B, S))), af_p=pad(afp),
+             pos=pad(np.broadcast_to(U.position_normalize(pos), (B, S))),
+             ref=pad((1 - afp) ** 2), het=pad(2 * afp * (1 - afp)), hom=pad(afp ** 2))
+    site_mask = torch.from_numpy(raw_mask.astype(np.uint8)).to(dev)
+    tok = torch.cat([x["hap_1"], x["hap_2"]]).contiguous()
+    Ar = eng.af_embedding(torch.from_numpy(ref_af).to(dev)[None]).float()[0].contiguous()
+    masked_per_step = 2 * B * int(raw_mask.sum())
+    k = args.k
+
+    def step():
+        idx, _ = index.search(tok, P.W, site_mask, k)
+        x["rag_mean"] = K.rag_mean(idx, index.codes, S, P.W, P.pe, Ar, L, dtype)
+        return eng.forward(x)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib = N.lib()
+    cap = 4096
+    lib.snvrag_evlog_enable(cap)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    kinds = np.zeros(cap, np.int32)
+    ms = np.zeros(cap, np.float32)
+    work = np.zeros(cap, np.float64)
+    n = lib.snvrag_evlog_read(kinds.ctypes.data, ms.ctypes.data, work.ctypes.data, cap)
+    lib.snvrag_evlog_enable(0)
+    kinds, ms, work = kinds[:n], ms[:n], work[:n]
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    def agg(kind):
+        sel = kinds == kind
+        cnt = int(sel.sum())
+        if cnt == 0:
+            return None
+        return dict(launches_per_step=cnt / args.steps, avg_ms=float(ms[sel].mean()),
+                    work_per_launch=float(work[sel].mean()), total_ms_per_step=float(ms[sel].sum()) / args.steps,
+                    rate=float(work[sel].sum() / (ms[sel].sum() * 1e-3)))
+
+    gemm, attn, ln, scan = agg(1), agg(2), agg(3), agg(4)
+    ms_step = elapsed / args.steps * 1e3
+    value = masked_per_step * world * args.steps / elapsed
+    knn_qps = 2 * B * world * args.steps / elapsed
+    if rank != 0:
+        return
+    peak_f = BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_PEAK_TFLOPS
+    roofline = dict(bound="mfma", kernel="linear_kernel (all encoder/head GEMMs)",
+                    achieved=round(gemm["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",
+                    frac=round(gemm["rate"] / 1e12 / peak_f, 4), traffic=None,
+                    avg_launch_ms=round(gemm["avg_ms"], 4),
+                    algorithmic_per_launch=f"{gemm['work_per_launch']:.4g} FLOP (2*M*N*K averaged over launches)")
+    extra = {
+        "kernels": {
+            "attention": dict(achieved_tflops=round(attn["rate"] / 1e12, 2), frac=round(attn["rate"] / 1e12 / peak_f, 4),
+                              ms_per_step=round(attn["total_ms_per_step"], 3)),
+            "knn_scan": dict(bound="hbm", achieved_gbs=round(scan["rate"] / 1e9, 1), peak=HBM_PEAK_GBS,
+                             frac=round(scan["rate"] / 1e9 / HBM_PEAK_GBS, 4), avg_launch_ms=round(scan["avg_ms"], 4),
+                             bytes_per_launch=scan["work_per_launch"]),
+            "gemm": dict(ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
+            "layernorm": dict(ms_per_step=round(ln["total_ms_per_step"], 3),
+                              achieved_gbs=round(ln["rate"] / 1e9, 1)),
+        },
+        "knn_queries_per_s": round(knn_qps, 1),
+        "masked_snvs_per_step_per_gpu": masked_per_step,
+    }
+    cpu = None
+    if args.cpu_baseline:
+        cpu = cpu_baseline(args, model, vocab, af_np, ref_af, raw_mask, x, dev)
+    line = {
+        "metric": "masked SNVs imputed/sec (+ kNN queries/sec), window=1024 k=32",
+        "value": round(value, 1), "unit": "masked SNVs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded AF~Beta(0.3,3) panel + copied queries)",
+        "config": {"workload": "configs[2]: v18 embedding-RAG imputation, window=1024 sites (L=1030 tokens), "
+                               f"k={k}, {args.n_ref}-haplotype panel resident in HBM, d{args.dims}/L{args.layers}/H{args.heads}",
+                   "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (panel replicated)"},
+        "roofline": roofline, "cpu_baseline": cpu, **extra,
+    }
+    print(json.dumps(line))
+
+
+def cpu_baseline(args, model, vocab, af_np, ref_af, raw_mask, x, dev):
+    """Oracle ('port') timed on host cores: exact LUT-form kNN over a panel sample
+    (scaled linearly to the full panel) + fp32 numpy forward of ONE sample."""
+    from oracle import knn_np, model_np
+    from src.dataset.synthetic import hash_uniform
+    sd = {kk: v.detach().float().cpu().numpy() for kk, v in model.state_dict().items()}
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    S, k = args.window, args.k
+    ns = min(args.cpu_panel, args.n_ref)
+    r, c = np.meshgrid(np.arange(ns), np.arange(S), indexing="ij")
+    panel = (hash_uniform(1234, r, c) < af_np[None]).astype(np.uint8)
+    tok = np.concatenate([x["hap_1"][:1].cpu().numpy(), x["hap_2"][:1].cpu().numpy()])
+    W = sd["bert.embedding.tokenizer.weight"]
+    t0 = time.perf_counter()
+    dq, _ = knn_np.quantize_lut(knn_np.lut_delta(W, tok, None, raw_mask.astype(np.uint8)), 2)
+    idx, _ = knn_np.knn(panel, dq, k)
+    t_knn = (time.perf_counter() - t0) * (args.n_ref / ns)
+    ref_tok = vocab.tokenize(panel, np.zeros(1030, np.int64))
+    xo = {kk: x[kk][:1].cpu().numpy() for kk in ("hap_1", "hap_2", "af", "af_p", "pos", "ref", "het", "hom")}
+    xo["rag_mean_h1"] = model_np.rag_mean(ref_tok, idx[:1], ref_af, sd)
+    xo["rag_mean_h2"] = model_np.rag_mean(ref_tok, idx[1:], ref_af, sd)
+    t1 = time.perf_counter()
+    model_np.forward(xo, sd, args.layers, args.heads)
+    t_fwd = time.perf_counter() - t1
+    masked = 2 * int(raw_mask.sum())
+    return {"value": round(masked / (t_knn + t_fwd), 1), "unit": "masked SNVs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"1 sample (2 haplotypes): oracle kNN over {ns} panel haplotypes scaled x{args.n_ref / ns:.1f} "
+                      f"to {args.n_ref} ({t_knn:.2f}s) + numpy fp32 forward d{args.dims}/L{args.layers} ({t_fwd:.2f}s)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+/*
+ * snvrag.h — C ABI of libsnvrag.so, the MI355X (gfx950) hot path of the v18
+ * embedding-RAG SNV-imputation model (wangbaonan/RAG-SNVBERT).
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + sizes, row-major, leading dimensions in ELEMENTS;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - caller owns every buffer (outputs and workspaces); no hidden device state;
+ *   - return 0 on success, non-zero on error; snvrag_last_error() has the text
+ *     (thread-local).  The Python host layer maps non-zero to RuntimeError.
+ *   - dtypes: SNVRAG_F32 (exact-f32 parity path) or SNVRAG_BF16 (throughput
+ *     path; f32 accumulation, f32 LayerNorm/softmax statistics).
+ *
+ * Each group names the reference interface it replaces (paths relative to
+ * /root/reference/src).
+ */
+#ifndef SNVRAG_H
+#define SNVRAG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNVRAG_ABI_VERSION 1
+
+enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
+enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
+
+int snvrag_abi_version(void);
+const char* snvrag_last_error(void);
+/* fills name (>= 64 bytes) with the device name of `device`; returns the CU count */
+int snvrag_device_info(int device, char* name, int name_len);
+
+/* ------------------------------------------------------------------------
+ * Dense layers  (replaces torch.nn.Linear calls of model/attention/
+ * multi_head_attention.py:44-51, model/utils/feed_forward.py:18-21,
+ * model/fusion.py:96-117,346, model/foundation_model.py:72-80,
+ * model/embedding/af_embedding.py:131-137)
+ *   C[m,n] = act( sum_k A[m,k] W[n,k] + bias[n]
+ *                 + row1[(m % row_period)*row1_stride] * col1[n]
+ *                 + row2[(m % row_period)*row2_stride] * col2[n] )
+ *            + resid[m,n]
+ * The rank-1 terms fold the reference's torch.cat([x, af, af_p]) / cat([emb,
+ * pos_feat, af]) input columns into the epilogue.
+ * A and W share dtype_in; C/resid use dtype_out.  K must be a multiple of 8.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  const float* bias;
+  const float* row1; int64_t row1_stride; const float* col1;
+  const float* row2; int64_t row2_stride; const float* col2;
+  int64_t row_period;          /* 0 = no wrap */
+  int act; float slope;
+  const void* resid; int64_t ld_resid;
+} snvrag_epilogue_t;
+
+int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
+                  const void* A, int64_t lda, const void* W, int64_t ldw,
+                  void* C, int64_t ldc, const snvrag_epilogue_t* epi, void* stream);
+
+/* LayerNorm over the last dim, eps as given (torch default 1e-5):
+ *   y = LN(x + r) * gamma + beta                  (r optional: residual of sublayer.py:15-16)
+ *   post (optional): y = act(y); y = base + scale * y * w(m)   w = maf weight of af[m % period]
+ *   (EnhancedRareVariantFusion tail, model/fusion.py:155-162) or w = 1.            */
+typedef struct {
+  const void* base; int64_t ld_base;  /* dtype_out */
+  float scale;
+  const float* af; int64_t af_period; int maf_weight;
+  int act;                            /* applied to LN output before the base/scale step */
+} snvrag_ln_post_t;
+
+int snvrag_layernorm(int dtype_in, int dtype_out, int64_t M, int64_t N,
+                     const void* X, int64_t ldx, const void* R, int64_t ldr,
+                     const float* gamma, const float* beta, float eps,
+                     void* Y, int64_t ldy, const snvrag_ln_post_t* post, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Attention without mask (model/attention/attention.py:21-31 with
+ * multi_head_attention.py head split/merge).  qkv row = [q | k | v], each
+ * heads*dh wide, row stride ld_qkv; out row stride ld_out (heads*dh used).
+ * softmax(q k^T * scale) v per (sequence, head).  dh in {16,32,48,64}.
+ * ---------------------------------------------------------------------- */
+int snvrag_attention(int dtype, int64_t nseq, int64_t L, int heads, int dh,
+                     const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out,
+                     float scale, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Embedding  (model/embedding/bert.py:66-77, af_embedding.py:79-91,
+ * position.py:37-38)
+ * ---------------------------------------------------------------------- */
+/* feat[m, j] = sin(2*pi*af[m]*f[j]), feat[m, nb+j] = cos(..), j < nb   */
+int snvrag_af_features(int dtype_out, int64_t M, const float* af, const float* freqs, int nb,
+                       void* feat, void* stream);
+/* out[s,l,:] = W[tok[s,l]] + pe[l,:] + afemb[(s % af_period)*L + l, :]  (afemb may be NULL) */
+int snvrag_embed_tokens(int dtype_out, int64_t nseq, int64_t L, int64_t D, const int64_t* tok,
+                        const float* W, int64_t vocab, const float* pe, const void* afemb,
+                        int afemb_dtype, int64_t af_period, void* out, void* stream);
+
+/* PositionFeatModule (model/fusion.py:317-332), eval BatchNorm */
+typedef struct {
+  const float* c1_w; const float* c1_b;   /* [4,1,9], [4] */
+  const float* c2_w; const float* c2_b;   /* [4,4,9], [4] */
+  const float* c3_w; const float* c3_b;   /* [1,4,9], [1] */
+  const float* bn1_w; const float* bn1_b; const float* bn1_rm; const float* bn1_rv;
+  const float* bn2_w; const float* bn2_b; const float* bn2_rm; const float* bn2_rv;
+  float bn_eps;
+} snvrag_posfeat_w_t;
+int snvrag_posfeat(int64_t B, int64_t L, const float* pos, const snvrag_posfeat_w_t* w,
+                   float* out, void* stream);
+
+/* CrossAFInteraction (model/fusion.py:82-86): fused_af[m,:] = af + rs*(gate*enc) */
+typedef struct {
+  const float* g1_w; const float* g1_b;   /* [32,2], [32] */
+  const float* g2_w; const float* g2_b;   /* [D,32], [D]  */
+  const float* j_w; const float* j_b;     /* [D,2],  [D]  */
+  const float* ln_w; const float* ln_b;   /* [D] */
+  float res_scale;
+} snvrag_afgate_w_t;
+int snvrag_af_gate(int dtype_out, int64_t M, int64_t D, const float* af, const float* af_p,
+                   const snvrag_afgate_w_t* w, void* out, void* stream);
+
+/* out[m, 0:D] = q[m,:];  out[m, D:2D] = rag[m,:] * wgt[m % period, :]
+ * (torch.cat([orig_feat, pooled_ref]) with K=1 pooling weight 1, model/fusion.py:141-152) */
+int snvrag_rag_weighted_concat(int dtype, int64_t M, int64_t D, const void* q, const void* rag,
+                               const void* wgt, int64_t period, void* out, void* stream);
+
+/* heads (model/foundation_model.py:64-80, :156-176) */
+int snvrag_hap_head_out(int dtype_in, int64_t M, int64_t K, const void* H, int64_t ldh,
+                        const float* w /*[2,K]*/, const float* b /*[2]*/,
+                        float* logits /*[M,2] or NULL*/, float* probs /*[M,2]*/, void* stream);
+typedef struct {
+  const float* f_w; const float* f_b;       /* gf_fusion [16,7] */
+  const float* n_w; const float* n_b;       /* gf_norm [16] */
+  const float* w1; const float* b1;         /* layer.w_1 [16,16] */
+  const float* ln_w; const float* ln_b;     /* layer.norm [16] */
+  const float* w2; const float* b2;         /* layer.w_2 [16,16] */
+  const float* c_w; const float* c_b;       /* classifier [4,16] */
+} snvrag_gt_w_t;
+int snvrag_gt_head(int64_t M, const float* p1, const float* p2, const float* ref,
+                   const float* het, const float* hom, int64_t period,
+                   const snvrag_gt_w_t* w, float* out /*[M,4]*/, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Reference-panel kNN on the HBM-resident token index
+ * (replaces embedding_rag_dataset.py:334-402 JIT embedding index + cdist/topk
+ *  and embedding_rag_infer_dataset.py:71-224,279-285 FAISS IndexFlatL2)
+ *
+ * Index: codes u8 [n_ref, ld_codes], allele (0/1) of each panel haplotype at
+ * each window site (ld_codes >= n_sites_pad = round_up(n_sites, 64), zero pad).
+ * Distances are exact integers on a per-query power-of-two fixed-point LUT;
+ * results are ordered by (distance, index) — see DESIGN.md §3.
+ * ---------------------------------------------------------------------- */
+/* LUT: Delta_q[s] = ||u - W[tok1]||^2 - ||u - W[tok0]||^2, u = W[tok_q[s+1]] + Aq - Ar,
+ * 0 where site_mask[s]; quantised to `limbs` int8 limbs (1 or 2) in scan-fragment
+ * order.  Aq: [nq_period rows of L x D] (query q uses (q % aq_period)); Aq/Ar may be NULL.
+ * lut_out: knn_lut_bytes(nq, n_sites_pad, limbs); exp_out [nq] int32 scale exponents;
+ * const_out [nq] f32 (distance offset; dist^2 = const + D * 2^-exp) may be NULL.      */
+size_t snvrag_knn_lut_bytes(int64_t nq, int32_t n_sites_pad, int limbs);
+int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
+                   const float* Aq, int64_t aq_period, const float* Ar,
+                   const uint8_t* site_mask, int32_t n_sites, int32_t n_sites_pad,
+                   int tok0, int tok1, int mask_tok, int limbs,
+                   void* lut_out, int32_t* exp_out, float* const_out, void* stream);
+
+/* Scan: every block scans a contiguous range of the panel and keeps an exact
+ * per-query top-k (k <= 32) of its range; partial lists (ascending uint64 keys
+ * ((D + 2^30) << 32 | ref_index), UINT64_MAX padding) -> part_keys [n_parts, nq, k].
+ * ref_offset is added to ref indices (panel shards).  Returns n_parts via *n_parts_out. */
+int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq);
+int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_codes, int32_t n_sites_pad,
+                    const void* lut, int32_t nq, int limbs, int k, int64_t ref_offset,
+                    uint64_t* part_keys, int32_t n_parts, void* stream);
+/* Merge n_lists sorted lists per query into the global top-k (exact (D, idx) order). */
+size_t snvrag_topk_merge_ws_bytes(int32_t n_lists, int32_t nq, int k);
+int snvrag_topk_merge(const uint64_t* keys, int32_t n_lists, int32_t nq, int k,
+                      uint64_t* out_keys, void* ws, size_t ws_bytes, void* stream);
+/* keys -> int64 indices (-1 for padding) and f32 squared-L2 (const + D*2^-exp) */
+int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const int32_t* exps,
+                      const float* consts, int64_t* idx_out, float* dist_out, void* stream);
+
+/* Mean of the k retrieved neighbours' COMPLETE-token embeddings
+ * (embedding_rag_dataset.py:406-438 re-encode + bert.py:176-179 K-mean), eval:
+ * out[q,l,:] = mean_j W[tok_j(l)] + pe[l] + Ar[l]; tokens: <sos>, alleles, <eos>, <pad>. */
+int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                    const uint8_t* codes, int64_t ld_codes, int32_t n_sites,
+                    const float* W, const float* pe, const float* Ar,
+                    int tok0, int tok1, int sos, int eos, int pad, void* out, void* stream);
+
+/* Deterministic synthetic panel on device: code = (u(seed,r,s) < af[s]), u = splitmix64
+ * hash (src/dataset/synthetic.py hash_uniform), zero padding to ld. */
+int snvrag_panel_synth(uint8_t* codes, int64_t n_ref, int64_t ld, int32_t n_sites,
+                       const float* af, uint64_t seed, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Encoder stack (model/transformer.py:27-30 x n_layers, model/bert.py:213-217),
+ * eval: x <- LN2(x1 + FFN(x1)), x1 = LN1(x + MHA(x)).  x is [nseq*L, D] in place.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  const void* w_qkv; const float* b_qkv;   /* [3D, D] rows q;k;v (dtype), [3D] */
+  const void* w_o; const float* b_o;       /* [D, D], [D] */
+  const float* ln1_g; const float* ln1_b;  /* input_sublayer.norm */
+  const void* w1; const float* b1;         /* [4D, D], [4D] */
+  const float* lnf_g; const float* lnf_b;  /* feed_forward.norm [4D] */
+  const void* w2; const float* b2;         /* [D, 4D], [D] */
+  const float* ln2_g; const float* ln2_b;  /* output_sublayer.norm */
+} snvrag_layer_t;
+
+size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);
+int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,
+                           const snvrag_layer_t* layers, void* x, void* ws, size_t ws_bytes,
+                           void* stream);
+
+/* Event log for live per-kernel timing (bench.py): when enabled, GEMM / attention /
+ * LayerNorm / kNN-scan launches record a HIP event pair on their stream plus their
+ * algorithmic work (FLOPs, or bytes for LN / kNN scan).  kinds: 1 GEMM, 2 attention,
+ * 3 LayerNorm, 4 kNN scan.  enable(capacity<=0) frees the log. */
+int snvrag_evlog_enable(int capacity);
+int snvrag_evlog_pause(int paused);
+int snvrag_evlog_reset(void);
+int snvrag_evlog_read(int* kinds, float* ms, double* work, int max);
+
+/* self tests of MFMA operand/accumulator layouts used by the kernels (GPU only):
+ * returns 0 when the i8 / bf16 / f32 MFMA maps match the CPU product. */
+int snvrag_selftest_mfma(void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNVRAG_H */

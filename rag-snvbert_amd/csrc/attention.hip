@@ -1,0 +1,287 @@
+// Unmasked multi-head attention, flash-style (no L x L score matrix in HBM).
+//
+// Reference: model/attention/attention.py:21-31 (softmax(QK^T/sqrt(dh)) V, no
+// mask — padding tokens participate) with the head split/merge of
+// multi_head_attention.py:44-51.  L = 1030 for every v18 configuration.
+//
+// bf16 path (v_mfma_f32_16x16x32_bf16), one workgroup = 4 waves = 64 queries of
+// one (sequence, head); each wave owns 16 queries.  Scores are computed
+// TRANSPOSED, S^T = K Q^T, so each lane holds one query's column of scores and
+// the softmax row statistics need only 2 cross-lane shuffles; P^T then feeds
+// the O^T = V^T P^T MFMA as the B operand straight from the accumulators
+// (key order permuted consistently on the V^T side).  K is staged row-major
+// (XOR-swizzled for conflict-free 16-lane reads), V transposed, both double
+// buffered with register prefetch of the next 64-key tile.
+//
+// f32 path: exact-f32 VALU online softmax, one thread per query (parity mode).
+#include "common.h"
+
+namespace snvrag {
+
+constexpr int AQ = 64;     // queries per workgroup
+constexpr int AK = 64;     // keys per tile
+
+template <int DH>
+struct AttnCfg {
+  static constexpr int KS = (DH + 31) / 32;        // 32-wide MFMA k-steps over head dim
+  static constexpr int DP = KS * 32;               // padded head dim in the K tile
+  static constexpr int KROWB = DP * 2;             // bytes per K-tile row
+  static constexpr int CPR = DP / 8;               // 16-B chunks per K row
+  static constexpr int RPC = 256 / KROWB;          // rows per 256-B bank cycle
+  static constexpr int ET = DH / 16;               // 16-wide output d tiles
+  static constexpr int VT_LD = AK + 8;             // V^T row stride (bf16), padded
+  static constexpr int KBYTES = AK * KROWB;
+  static constexpr int VBYTES = DP * VT_LD * 2;
+  static constexpr int STAGE = KBYTES + VBYTES;
+};
+
+template <int DH>
+__device__ __forceinline__ int k_off(int key, int chunk) {
+  using C = AttnCfg<DH>;
+  return key * C::KROWB + ((chunk ^ ((key / C::RPC) % C::CPR)) << 4);
+}
+
+template <int DH>
+__global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, const bf16* __restrict__ qkv,
+                                                     long ld, bf16* __restrict__ out, long ldo,
+                                                     float scale_log2e, int nqb) {
+  using C = AttnCfg<DH>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE];
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const long base = (long)seq * L * ld;
+  const int D = H * DH;
+  const bf16* Qp = qkv + base + h * DH;
+  const bf16* Kp = qkv + base + D + h * DH;
+  const bf16* Vp = qkv + base + 2 * D + h * DH;
+
+  // Q fragment (B operand of S^T = K Q^T): lane -> query q0+li, d = 32*ks + 8*lg + j
+  const int q = qb * AQ + wave * 16 + li;
+  bf16x8 qf[C::KS];
+#pragma unroll
+  for (int ks = 0; ks < C::KS; ++ks) {
+    const int d0 = 32 * ks + 8 * lg;
+    if (q < L && d0 < DH)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + d0);
+    else
+      qf[ks] = bf16x8{};
+  }
+
+  // tile loader: thread -> (key, 16-B chunk) for K and V; rows beyond L / DH are zero
+  constexpr int CH = C::CPR;                               // chunks per key (padded)
+  constexpr int NLD = (AK * CH + 255) / 256;
+  u32x4 kr[NLD], vr[NLD];
+  auto load_tile = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int id = tid + 256 * i;
+      const int key = id / CH, c = id % CH;
+      const int kk = t0 + key, d0 = 8 * c;
+      if (id < AK * CH && kk < L && d0 < DH) {
+        kr[i] = *reinterpret_cast<const u32x4*>(Kp + (long)kk * ld + d0);
+        vr[i] = *reinterpret_cast<const u32x4*>(Vp + (long)kk * ld + d0);
+      } else {
+        kr[i] = u32x4{0u, 0u, 0u, 0u};
+        vr[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  auto store_tile = [&](char* st) {
+    bf16* vt = reinterpret_cast<bf16*>(st + C::KBYTES);
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int id = tid + 256 * i;
+      if (id < AK * CH) {
+        const int key = id / CH, c = id % CH;
+        *reinterpret_cast<u32x4*>(st + k_off<DH>(key, c)) = kr[i];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, vr[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vt[(8 * c + j) * C::VT_LD + key] = v[j];
+      }
+    }
+  };
+
+  f32x4 o[C::ET];
+#pragma unroll
+  for (int e = 0; e < C::ET; ++e) o[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int ntile = (L + AK - 1) / AK;
+  load_tile(0);
+  store_tile(smem);
+  __syncthreads();
+
+  for (int t = 0; t < ntile; ++t) {
+    char* st = smem + (t & 1) * C::STAGE;
+    const bool more = t + 1 < ntile;
+    if (more) load_tile((t + 1) * AK);
+
+    // ---- S^T tile: 4 x (16 keys x 16 queries) ----
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int key = 16 * kt + li;
+#pragma unroll
+      for (int ks = 0; ks < C::KS; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(st + k_off<DH>(key, 4 * ks + lg));
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[kt], 0, 0, 0);
+      }
+    }
+    // ---- online softmax over the 64 keys of this tile (per query = per lane column) ----
+    const int kbase = t * AK;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + 16 * kt + 4 * lg + r;
+        float v = s[kt][r] * scale_log2e;
+        v = key < L ? v : -INFINITY;
+        s[kt][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
+    bf16x8 pb[2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[kt][r] - m_new);
+        psum += p;
+        pb[kt >> 1][(kt & 1) * 4 + r] = (bf16)p;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int e = 0; e < C::ET; ++e) o[e] *= alpha;
+
+    // ---- O^T += V^T P^T : keys of MFMA c in the order the accumulators hold them ----
+    const bf16* vt = reinterpret_cast<const bf16*>(st + C::KBYTES);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int e = 0; e < C::ET; ++e) {
+        const bf16* row = vt + (16 * e + li) * C::VT_LD + 32 * c + 4 * lg;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(row);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(row + 16);
+        const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[c], o[e], 0, 0, 0);
+      }
+    }
+    if (more) store_tile(smem + ((t + 1) & 1) * C::STAGE);
+    __syncthreads();
+  }
+
+  if (q < L) {
+    const float inv = 1.0f / l_run;
+    bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * DH;
+#pragma unroll
+    for (int e = 0; e < C::ET; ++e) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[e][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * e + 4 * lg) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- f32 path --
+template <int DH>
+__global__ __launch_bounds__(64) void attn_fwd_f32(int nseq, int L, int H, const float* __restrict__ qkv,
+                                                   long ld, float* __restrict__ out, long ldo, float scale) {
+  __shared__ float ks[AK][DH];
+  __shared__ float vs[AK][DH];
+  const int qb = blockIdx.x, h = blockIdx.y, seq = blockIdx.z;
+  const int tid = threadIdx.x;
+  const int D = H * DH;
+  const long base = (long)seq * L * ld;
+  const int q = qb * 64 + tid;
+  float qv[DH], o[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    qv[d] = q < L ? qkv[base + (long)q * ld + h * DH + d] * scale : 0.f;
+    o[d] = 0.f;
+  }
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int t0 = 0; t0 < L; t0 += AK) {
+    __syncthreads();
+    for (int i = tid; i < AK * DH; i += 64) {
+      const int key = i / DH, d = i % DH, kk = t0 + key;
+      ks[key][d] = kk < L ? qkv[base + (long)kk * ld + D + h * DH + d] : 0.f;
+      vs[key][d] = kk < L ? qkv[base + (long)kk * ld + 2 * D + h * DH + d] : 0.f;
+    }
+    __syncthreads();
+    const int nk = min(AK, L - t0);
+    for (int j = 0; j < nk; ++j) {
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) sc = fmaf(qv[d], ks[j][d], sc);
+      const float m_new = fmaxf(m_run, sc);
+      const float a = expf(m_run - m_new), p = expf(sc - m_new);
+      l_run = l_run * a + p;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) o[d] = o[d] * a + p * vs[j][d];
+      m_run = m_new;
+    }
+  }
+  if (q < L) {
+    float* op = out + (long)seq * L * ldo + (long)q * ldo + h * DH;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) op[d] = o[d] / l_run;
+  }
+}
+
+template <int DH>
+static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, long ld, void* out,
+                       long ldo, float scale, hipStream_t s) {
+  evlog_begin(s);
+  if (dtype == SNVRAG_BF16) {
+    const int nqb = cdiv(L, AQ);
+    const long nb = (long)nqb * H * nseq;
+    SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
+    hipLaunchKernelGGL(attn_fwd_bf16<DH>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, H,
+                       (const bf16*)qkv, ld, (bf16*)out, ldo, scale * 1.4426950408889634f, nqb);
+  } else {
+    hipLaunchKernelGGL(attn_fwd_f32<DH>, dim3(cdiv(L, 64), H, (unsigned)nseq), dim3(64), 0, s,
+                       (int)nseq, (int)L, H, (const float*)qkv, ld, (float*)out, ldo, scale);
+  }
+  SNV_LAUNCH_CHECK();
+  evlog_end(s, EV_ATTN, 4.0 * nseq * H * (double)L * L * DH);
+  return 0;
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" int snvrag_attention(int dtype, int64_t nseq, int64_t L, int heads, int dh,
+                                const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out,
+                                float scale, void* stream) {
+  SNV_CHECK_ARG(qkv && out, "null pointer");
+  SNV_CHECK_ARG(nseq >= 0 && L > 0 && heads > 0, "bad shape");
+  SNV_CHECK_ARG(ld_qkv >= 3L * heads * dh && ld_out >= (long)heads * dh, "leading dims too small");
+  if (dtype == SNVRAG_BF16)
+    SNV_CHECK_ARG(ld_qkv % 8 == 0 && ld_out % 4 == 0 && (heads * dh) % 8 == 0, "bf16 alignment");
+  if (nseq == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  switch (dh) {
+    case 16: return launch_attn<16>(dtype, nseq, L, heads, qkv, ld_qkv, out, ld_out, scale, s);
+    case 32: return launch_attn<32>(dtype, nseq, L, heads, qkv, ld_qkv, out, ld_out, scale, s);
+    case 48: return launch_attn<48>(dtype, nseq, L, heads, qkv, ld_qkv, out, ld_out, scale, s);
+    case 64: return launch_attn<64>(dtype, nseq, L, heads, qkv, ld_qkv, out, ld_out, scale, s);
+    default: return fail(__func__, "head dim must be 16, 32, 48 or 64");
+  }
+}

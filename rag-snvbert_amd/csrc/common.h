@@ -1,0 +1,84 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of libsnvrag.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <string>
+
+#include "../../include/snvrag.h"
+
+namespace snvrag {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+void set_error(const std::string& msg);
+
+// ---- event log (bench.py live per-kernel timing; off by default) ----
+enum EvKind { EV_GEMM = 1, EV_ATTN = 2, EV_LN = 3, EV_KNN_SCAN = 4, EV_KNN_LUT = 5, EV_MERGE = 6, EV_OTHER = 7 };
+bool evlog_on();
+void evlog_begin(hipStream_t s);
+void evlog_end(hipStream_t s, int kind, double work);
+int fail(const char* where, const std::string& msg);
+
+#define SNV_CHECK_ARG(cond, msg)                                     \
+  do {                                                               \
+    if (!(cond)) return ::snvrag::fail(__func__, (msg));             \
+  } while (0)
+
+#define SNV_HIP(expr)                                                \
+  do {                                                               \
+    hipError_t e_ = (expr);                                          \
+    if (e_ != hipSuccess)                                            \
+      return ::snvrag::fail(__func__, hipGetErrorString(e_));        \
+  } while (0)
+
+// launch + error check (kernel launch errors surface via hipGetLastError)
+#define SNV_LAUNCH_CHECK()                                           \
+  do {                                                               \
+    hipError_t e_ = hipGetLastError();                               \
+    if (e_ != hipSuccess)                                            \
+      return ::snvrag::fail(__func__, hipGetErrorString(e_));        \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------ device --
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(int act, float x, float slope) {
+  switch (act) {
+    case SNVRAG_ACT_GELU: return gelu_erf(x);
+    case SNVRAG_ACT_LRELU: return x >= 0.f ? x : x * slope;
+    case SNVRAG_ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace snvrag

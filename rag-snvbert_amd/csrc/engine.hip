@@ -1,0 +1,97 @@
+// Encoder stack orchestration: all n_layers x 8 launches of the transformer
+// blocks issued from C++ (one C-ABI call per forward, capturable in a hipGraph).
+//
+// Per block (model/transformer.py:27-30, sublayer.py:15-16, feed_forward.py:18-21,
+// multi_head_attention.py:44-51), eval:
+//   qkv = x Wqkv^T + b                      (one GEMM, N = 3D: q;k;v rows packed)
+//   a   = attention(qkv)                    (flash, unmasked)
+//   x1  = LN1(x + a Wo^T + bo)              (residual fused in the GEMM epilogue)
+//   h   = LN_f(lrelu(x1 W1^T + b1))         (LN in place)
+//   x   = LN2(x1 + lrelu(h W2^T + b2))      (residual fused after the activation)
+// Sequences are processed in chunks so a chunk's activations (9 D per token)
+// stay resident in the 256 MiB Infinity Cache across the 12 layers.
+#include "common.h"
+
+#include <cmath>
+
+namespace snvrag {
+
+static int64_t chunk_seqs(int64_t nseq, int64_t L, int D, int esz) {
+  const char* e = getenv("SNVRAG_ENCODER_CHUNK");
+  if (e) {
+    const long v = atol(e);
+    if (v > 0) return std::min<int64_t>(v, nseq);
+  }
+  // target ~160 MB of per-chunk activations (x + qkv + attn + x1 + h = 10 D / token)
+  const double per_seq = (double)L * D * 10.0 * esz;
+  int64_t c = (int64_t)(160.0e6 / per_seq);
+  if (c < 1) c = 1;
+  return std::min<int64_t>(c, nseq);
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads) {
+  (void)heads;
+  const int esz = dtype == SNVRAG_BF16 ? 2 : 4;
+  const int64_t c = chunk_seqs(nseq, L, D, esz);
+  const size_t M = (size_t)c * L;
+  return M * (size_t)D * 9 * esz + 4096;
+}
+
+extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,
+                                      const snvrag_layer_t* layers, void* x, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  SNV_CHECK_ARG(layers && x && ws, "null pointer");
+  SNV_CHECK_ARG(D % heads == 0, "D % heads");
+  SNV_CHECK_ARG(ws_bytes >= snvrag_encoder_ws_bytes(dtype, nseq, L, D, heads), "encoder workspace too small");
+  const int esz = dtype == SNVRAG_BF16 ? 2 : 4;
+  const int64_t cs = chunk_seqs(nseq, L, D, esz);
+  const size_t Mc = (size_t)cs * L;
+  char* w = (char*)ws;
+  auto carve = [&](size_t elems) { char* p = w; w += ((elems * esz + 255) / 256) * 256; return (void*)p; };
+  void* qkv = carve(Mc * 3 * D);
+  void* att = carve(Mc * D);
+  void* x1 = carve(Mc * D);
+  void* h = carve(Mc * 4 * D);
+  const int dh = D / heads;
+  const float scale = 1.0f / sqrtf((float)dh);
+
+  for (int64_t s0 = 0; s0 < nseq; s0 += cs) {
+    const int64_t ns = std::min<int64_t>(cs, nseq - s0);
+    const int64_t M = ns * L;
+    char* xc = (char*)x + (size_t)s0 * L * D * esz;
+    for (int i = 0; i < n_layers; ++i) {
+      const snvrag_layer_t& ly = layers[i];
+      snvrag_epilogue_t e{};
+      int rc;
+      e.bias = ly.b_qkv;
+      rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
+      if (rc) return rc;
+      rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, scale, stream);
+      if (rc) return rc;
+      e = snvrag_epilogue_t{};
+      e.bias = ly.b_o; e.resid = xc; e.ld_resid = D;
+      rc = snvrag_linear(dtype, dtype, M, D, D, att, D, ly.w_o, D, x1, D, &e, stream);
+      if (rc) return rc;
+      rc = snvrag_layernorm(dtype, dtype, M, D, x1, D, nullptr, 0, ly.ln1_g, ly.ln1_b, 1e-5f, x1, D, nullptr, stream);
+      if (rc) return rc;
+      e = snvrag_epilogue_t{};
+      e.bias = ly.b1; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f;
+      rc = snvrag_linear(dtype, dtype, M, 4 * D, D, x1, D, ly.w1, D, h, 4 * D, &e, stream);
+      if (rc) return rc;
+      rc = snvrag_layernorm(dtype, dtype, M, 4 * D, h, 4 * D, nullptr, 0, ly.lnf_g, ly.lnf_b, 1e-5f, h, 4 * D,
+                            nullptr, stream);
+      if (rc) return rc;
+      e = snvrag_epilogue_t{};
+      e.bias = ly.b2; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.resid = x1; e.ld_resid = D;
+      rc = snvrag_linear(dtype, dtype, M, D, 4 * D, h, 4 * D, ly.w2, 4 * D, xc, D, &e, stream);
+      if (rc) return rc;
+      rc = snvrag_layernorm(dtype, dtype, M, D, xc, D, nullptr, 0, ly.ln2_g, ly.ln2_b, 1e-5f, xc, D, nullptr, stream);
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}

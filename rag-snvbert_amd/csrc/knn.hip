@@ -1,0 +1,556 @@
+// Reference-panel kNN on the HBM-resident token index (gfx950).
+//
+// Replaces the reference's per-window fp32 embedding index + torch.cdist/topk
+// (src/dataset/embedding_rag_dataset.py:334-402) and the FAISS IndexFlatL2 of
+// inference (embedding_rag_infer_dataset.py:176, :279-285).  Because the
+// embedding is position-wise, dist^2(q,r) = C_q + sum_s Delta_q[s] * a_r[s]
+// (a_r[s] in {0,1}: allele of panel haplotype r at window site s), so the index
+// is the panel's allele codes (1 B / site / haplotype) and the per-query work
+// is a length-n_sites LUT.  DESIGN.md §3 has the derivation and the canonical
+// (distance, index) order these kernels reproduce bit-exactly.
+//
+//   lut_kernel    : Delta in f32 -> per-query power-of-two fixed point -> int8
+//                   limbs laid out in MFMA A-fragment order.
+//   scan_kernel   : v_mfma_i32_16x16x64_i8 distance tiles (16 queries x 16
+//                   haplotypes x 64 sites), codes streamed straight from HBM to
+//                   VGPRs (no reuse to stage), exact per-range top-k kept in LDS
+//                   with a strict-threshold filter + wave bitonic compaction.
+//   merge_kernel  : hierarchical LDS bitonic merge of the per-range lists.
+#include "common.h"
+
+namespace snvrag {
+
+constexpr uint64_t KEY_MAX = ~0ull;
+constexpr int KEY_BIAS = 1 << 30;
+constexpr int SCAN_CAP = 64;      // candidate slots per query per wave
+constexpr int SCAN_TH = SCAN_CAP - 16;
+
+__device__ __forceinline__ uint64_t make_key(int d, uint32_t idx) {
+  return ((uint64_t)(uint32_t)(d + KEY_BIAS) << 32) | idx;
+}
+
+// ------------------------------------------------------------------- LUT ---
+// One workgroup per query.  Positions l = 0..L-1 contribute to the constant
+// C_q; unmasked sites s (l = s + 1) contribute Delta_q[s].
+__global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* __restrict__ tok_q,
+                                                  const float* __restrict__ W, const float* __restrict__ Aq,
+                                                  long aq_period, const float* __restrict__ Ar,
+                                                  const uint8_t* __restrict__ site_mask, int n_sites,
+                                                  int n_sites_pad, int nq, int tok0, int tok1, int mask_tok,
+                                                  int limbs, int8_t* __restrict__ lut, int* __restrict__ exps,
+                                                  float* __restrict__ consts) {
+  extern __shared__ float sdelta[];              // [n_sites_pad] + [4] scratch
+  float* red = sdelta + n_sites_pad;
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long arow = Aq ? ((aq_period > 0 ? q % aq_period : q) * (long)L) : 0;
+  float cacc = 0.f;
+  for (int l = wave; l < L; l += 4) {
+    const int t = (int)tok_q[(long)q * L + l];
+    const bool is_site = l >= 1 && l <= n_sites;
+    const bool varying = is_site && !site_mask[l - 1];
+    int rt;                                        // panel token at l when not varying
+    if (l == 0) rt = 2; else if (is_site) rt = mask_tok; else if (l == n_sites + 1) rt = 3; else rt = 0;
+    float t0 = 0.f, t1 = 0.f, tc = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float u = W[(long)t * D + d];
+      if (Aq) u += Aq[(arow + l) * D + d];
+      if (Ar) u -= Ar[(long)l * D + d];
+      if (varying) {
+        const float a = u - W[(long)tok0 * D + d], b = u - W[(long)tok1 * D + d];
+        t0 = fmaf(a, a, t0);
+        t1 = fmaf(b, b, t1);
+      } else {
+        const float c = u - W[(long)rt * D + d];
+        tc = fmaf(c, c, tc);
+      }
+    }
+    t0 = wave_sum(t0); t1 = wave_sum(t1); tc = wave_sum(tc);
+    if (lane == 0) {
+      if (is_site) sdelta[l - 1] = varying ? (t1 - t0) : 0.f;
+      cacc += varying ? t0 : tc;
+    }
+  }
+  for (int s = n_sites + tid; s < n_sites_pad; s += 256) sdelta[s] = 0.f;
+  if (lane == 0) red[wave] = cacc;
+  __syncthreads();
+  // block max |Delta|
+  float mx = 0.f;
+  for (int s = tid; s < n_sites; s += 256) mx = fmaxf(mx, fabsf(sdelta[s]));
+  mx = wave_max(mx);
+  __shared__ float wmax[4];
+  __shared__ int sexp;
+  if (lane == 0) wmax[wave] = mx;
+  __syncthreads();
+  const int qmax = (1 << (7 * limbs)) - 1;
+  if (tid == 0) {
+    const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    int e = 0;
+    if (m > 0.f) {
+      e = (int)floor(log2((double)qmax / (double)m));
+      if ((double)m * exp2((double)e) > (double)qmax) e -= 1;
+    }
+    sexp = e;
+    exps[q] = e;
+    if (consts) consts[q] = red[0] + red[1] + red[2] + red[3];
+  }
+  __syncthreads();
+  const float sc = exp2f((float)sexp);
+  // quantise + scatter into fragment order: [qt][limb][ks][lane(64)][16]
+  const int qt = q >> 4, qr = q & 15;
+  const int KS = n_sites_pad / 64;
+  for (int s = tid; s < n_sites_pad; s += 256) {
+    float v = rintf(sdelta[s] * sc);
+    v = fminf(fmaxf(v, (float)-qmax), (float)qmax);
+    const int dq = (int)v;
+    const int ks = s >> 6, within = s & 63, g = within >> 4, j = within & 15;
+    const int ln = g * 16 + qr;
+    if (limbs == 2) {
+      const int hi = dq >> 7, lo = dq & 127;
+      lut[((((long)qt * 2 + 0) * KS + ks) * 64 + ln) * 16 + j] = (int8_t)hi;
+      lut[((((long)qt * 2 + 1) * KS + ks) * 64 + ln) * 16 + j] = (int8_t)lo;
+    } else {
+      lut[(((long)qt * KS + ks) * 64 + ln) * 16 + j] = (int8_t)dq;
+    }
+  }
+}
+
+// padding rows of the last query tile must be zero
+__global__ void lut_zero_pad_kernel(int8_t* lut, int nq, int KS, int limbs) {
+  const int qt = nq >> 4;
+  const long per_tile = (long)limbs * KS * 64 * 16;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < per_tile; i += (long)gridDim.x * blockDim.x) {
+    const int ln = (int)((i / 16) % 64);
+    if ((ln & 15) >= (nq & 15)) lut[qt * per_tile + i] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ scan ---
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ascending bitonic sort of one key per lane across the wave
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t key, int lane) {
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t other = shfl_xor64(key, stride);
+      const bool up = (lane & size) == 0;
+      const bool low = (lane & stride) == 0;
+      const uint64_t mn = key < other ? key : other, mxv = key < other ? other : key;
+      key = (low == up) ? mn : mxv;
+    }
+  }
+  return key;
+}
+
+// compact the candidate list of query row `row` (wave-uniform) to its top-k.
+__device__ __forceinline__ void compact_row(uint64_t* buf, int row, int cnt, int k, int lane,
+                                            int& new_cnt, int& new_th) {
+  uint64_t key = lane < cnt ? buf[row * SCAN_CAP + lane] : KEY_MAX;
+  key = wave_sort64(key, lane);
+  if (lane < k) buf[row * SCAN_CAP + lane] = key;
+  new_cnt = cnt < k ? cnt : k;
+  const uint64_t kth = shfl64(key, k - 1);
+  new_th = (cnt >= k) ? (int)(kth >> 32) - KEY_BIAS : INT_MAX;
+}
+
+template <int KSMAX, int LIMBS>
+__global__ __launch_bounds__(256) void scan_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
+                                                   int KS, const int8_t* __restrict__ lut, int nq, int k,
+                                                   long range, long ref_offset, uint64_t* __restrict__ parts) {
+  __shared__ __attribute__((aligned(16))) uint64_t sbuf[4][16 * SCAN_CAP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int nqt = (nq + 15) >> 4;
+  const int qt = blockIdx.y * 4 + wave;
+  if (qt >= nqt) return;                     // no block-level barriers below
+  uint64_t* buf = sbuf[wave];
+  const int part = blockIdx.x;
+  const long r_begin = part * range;
+  const long r_end = min(n_ref, r_begin + range);
+
+  // A fragments (LUT limbs) for this query tile: registers for the whole scan
+  i32x4 a[LIMBS][KSMAX];
+#pragma unroll
+  for (int lb = 0; lb < LIMBS; ++lb)
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+      if (ks < KS)
+        a[lb][ks] = *reinterpret_cast<const i32x4*>(lut + ((((long)qt * LIMBS + lb) * KS + ks) * 64 + lane) * 16);
+      else
+        a[lb][ks] = i32x4{0, 0, 0, 0};
+
+  int th[4], cnt[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { th[i] = INT_MAX; cnt[i] = 0; }
+
+  for (long r0 = r_begin; r0 < r_end; r0 += 16) {
+    const long r = r0 + li;
+    const bool rv = r < r_end;
+    const uint8_t* row = codes + (rv ? r : r_begin) * ld + 16 * lg;
+    i32x4 b[KSMAX];
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+      if (ks < KS) b[ks] = *reinterpret_cast<const i32x4*>(row + 64 * ks);
+    i32x4 acc[LIMBS];
+#pragma unroll
+    for (int lb = 0; lb < LIMBS; ++lb) acc[lb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+      if (ks < KS)
+#pragma unroll
+        for (int lb = 0; lb < LIMBS; ++lb)
+          acc[lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[lb][ks], b[ks], acc[lb], 0, 0, 0);
+
+    // filter: lane holds D[q = 4*lg + i][ref = r]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = LIMBS == 2 ? acc[0][i] * 128 + acc[1][i] : acc[0][i];
+      const bool pass = rv && d < th[i];
+      const uint64_t m = __ballot(pass);
+      if (m) {
+        const uint32_t gb = (uint32_t)(m >> (16 * lg)) & 0xFFFFu;
+        if (pass) {
+          const int pre = __popc(gb & ((1u << li) - 1u));
+          buf[(4 * lg + i) * SCAN_CAP + cnt[i] + pre] = make_key(d, (uint32_t)(r + ref_offset));
+        }
+        cnt[i] += __popc(gb);
+      }
+    }
+    // compaction of rows close to capacity (wave-uniform loop)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint64_t need = __ballot(cnt[i] > SCAN_TH);
+      while (need) {
+        const int src = __builtin_ctzll(need);
+        const int g = src >> 4;
+        need &= ~(0xFFFFull << (16 * g));
+        int nc, nt;
+        compact_row(buf, 4 * g + i, __shfl(cnt[i], src, 64), k, lane, nc, nt);
+        if (lg == g) { cnt[i] = nc; th[i] = nt; }
+      }
+    }
+  }
+  // final compaction of every row; emit the per-range top-k
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * g + i;
+      const int c = __shfl(cnt[i], 16 * g, 64);
+      int nc, nt;
+      compact_row(buf, row, c, k, lane, nc, nt);
+      const int q = qt * 16 + row;
+      if (q < nq && lane < k)
+        parts[((long)part * nq + q) * k + lane] = lane < nc ? buf[row * SCAN_CAP + lane] : KEY_MAX;
+    }
+  }
+}
+
+// ----------------------------------------------------------------- merge ---
+// block (256 threads) per (query, group of G lists): bitonic sort of <= 1024 keys in LDS
+__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int n_lists, int nq,
+                                                    int k, int G, uint64_t* __restrict__ out) {
+  __shared__ uint64_t s[1024];
+  const int q = blockIdx.y, grp = blockIdx.x, tid = threadIdx.x;
+  const int l0 = grp * G, nl = min(G, n_lists - l0);
+  const int n = nl * k;
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = tid; i < P; i += 256) {
+    uint64_t v = KEY_MAX;
+    if (i < n) {
+      const int li = i / k, j = i % k;
+      v = in[((long)(l0 + li) * nq + q) * k + j];
+    }
+    s[i] = v;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P / 2; i += 256) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t a = s[lo], b = s[hi];
+        if ((a > b) == up) { s[lo] = b; s[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < k; j += 256) out[((long)grp * nq + q) * k + j] = s[j];
+}
+
+__global__ void decode_kernel(const uint64_t* __restrict__ keys, int nq, int k, const int* __restrict__ exps,
+                              const float* __restrict__ consts, int64_t* __restrict__ idx, float* __restrict__ dist) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)nq * k) return;
+  const int q = (int)(i / k);
+  const uint64_t key = keys[i];
+  if (key == KEY_MAX) {
+    idx[i] = -1;
+    if (dist) dist[i] = INFINITY;
+    return;
+  }
+  idx[i] = (int64_t)(key & 0xFFFFFFFFull);
+  if (dist) {
+    const int d = (int)(key >> 32) - KEY_BIAS;
+    dist[i] = (consts ? consts[q] : 0.f) + ldexpf((float)d, -exps[q]);
+  }
+}
+
+// ------------------------------------------------------------- rag mean ---
+template <typename T>
+__global__ __launch_bounds__(256) void rag_mean_kernel(int L, int D, int k, const int64_t* __restrict__ idx,
+                                                       const uint8_t* __restrict__ codes, long ld, int n_sites,
+                                                       const float* __restrict__ W, const float* __restrict__ pe,
+                                                       const float* __restrict__ Ar, int tok0, int tok1, int sos,
+                                                       int eos, int pad, T* __restrict__ out) {
+  __shared__ float frac[64];
+  __shared__ int nvalid_s;
+  const int q = blockIdx.y, l0 = blockIdx.x * 64, tid = threadIdx.x;
+  if (tid == 0) {
+    int nv = 0;
+    for (int j = 0; j < k; ++j) nv += idx[(long)q * k + j] >= 0;
+    nvalid_s = nv;
+  }
+  __syncthreads();
+  const int nv = nvalid_s;
+  if (tid < 64) {
+    const int l = l0 + tid;
+    float f = 0.f;
+    if (l >= 1 && l <= n_sites && nv > 0) {
+      int c = 0;
+      for (int j = 0; j < k; ++j) {
+        const int64_t r = idx[(long)q * k + j];
+        if (r >= 0) c += codes[r * ld + (l - 1)];
+      }
+      f = (float)c / (float)nv;
+    }
+    frac[tid] = f;
+  }
+  __syncthreads();
+  constexpr int V = 16 / sizeof(T);
+  const int cpr = D / V;
+  for (int id = tid; id < 64 * cpr; id += 256) {
+    const int rl = id / cpr, c = (id % cpr) * V;
+    const int l = l0 + rl;
+    if (l >= L) break;
+    int t;
+    const bool site = l >= 1 && l <= n_sites;
+    if (l == 0) t = sos; else if (site) t = tok0; else if (l == n_sites + 1) t = eos; else t = pad;
+    const float f = frac[rl];
+    float v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float w = W[(long)t * D + c + j];
+      if (site) w = nv > 0 ? w + f * (W[(long)tok1 * D + c + j] - w) : 0.f;
+      float x = w + pe[(long)l * D + c + j];
+      if (Ar) x += Ar[(long)l * D + c + j];
+      v[j] = x;
+    }
+    T o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) o[j] = from_f32<T>(v[j]);
+    *reinterpret_cast<u32x4*>(out + ((long)q * L + l) * D + c) = *reinterpret_cast<u32x4*>(o);
+  }
+}
+
+// ---------------------------------------------------------- panel synth ---
+__device__ __forceinline__ double hash_u01(uint64_t seed, uint64_t r, uint64_t c) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + r * 0xD1B54A32D192ED03ull + c * 0x8CB92BA72F3D8DD7ull;
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x = x ^ (x >> 31);
+  return (double)(x >> 40) / (double)(1 << 24);
+}
+
+__global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long ld, int n_sites,
+                                   const float* __restrict__ af, uint64_t seed) {
+  const long chunks_per_row = ld / 16;
+  const long total = n_ref * chunks_per_row;
+  for (long id = (long)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (long)gridDim.x * blockDim.x) {
+    const long r = id / chunks_per_row;
+    const int c0 = (int)(id % chunks_per_row) * 16;
+    uint8_t v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int s = c0 + j;
+      v[j] = (s < n_sites && hash_u01(seed, (uint64_t)r, (uint64_t)s) < (double)af[s]) ? 1 : 0;
+    }
+    *reinterpret_cast<u32x4*>(codes + r * ld + c0) = *reinterpret_cast<u32x4*>(v);
+  }
+}
+
+static int scan_parts(long n_ref) {
+  // ~2048 refs per range, at least 16, at most 4096 parts
+  long p = (n_ref + 2047) / 2048;
+  if (p < 1) p = 1;
+  if (p > 4096) p = 4096;
+  return (int)p;
+}
+
+template <int KSM, int LB>
+static void launch_scan(dim3 g, hipStream_t s, const uint8_t* codes, long n_ref, long ld, int KS,
+                        const int8_t* lut, int nq, int k, long range, long off, uint64_t* parts) {
+  hipLaunchKernelGGL((scan_kernel<KSM, LB>), g, dim3(256), 0, s, codes, n_ref, ld, KS, lut, nq, k, range, off, parts);
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" size_t snvrag_knn_lut_bytes(int64_t nq, int32_t n_sites_pad, int limbs) {
+  return (size_t)((nq + 15) / 16) * limbs * (n_sites_pad / 64) * 64 * 16;
+}
+
+extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
+                              const float* Aq, int64_t aq_period, const float* Ar, const uint8_t* site_mask,
+                              int32_t n_sites, int32_t n_sites_pad, int tok0, int tok1, int mask_tok, int limbs,
+                              void* lut_out, int32_t* exp_out, float* const_out, void* stream) {
+  SNV_CHECK_ARG(tok_q && W && site_mask && lut_out && exp_out, "null pointer");
+  SNV_CHECK_ARG(limbs == 1 || limbs == 2, "limbs must be 1 or 2");
+  SNV_CHECK_ARG(n_sites_pad % 64 == 0 && n_sites_pad >= n_sites && n_sites + 2 <= L, "site padding");
+  SNV_CHECK_ARG(n_sites_pad <= 17 * 64, "window longer than 1088 sites");
+  if (nq == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const size_t sh = (size_t)(n_sites_pad + 4) * sizeof(float);
+  hipLaunchKernelGGL(lut_kernel, dim3((unsigned)nq), dim3(256), sh, s, (int)L, (int)D, tok_q, W, Aq,
+                     (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, (int)nq, tok0, tok1, mask_tok,
+                     limbs, (int8_t*)lut_out, exp_out, const_out);
+  SNV_LAUNCH_CHECK();
+  if (nq % 16)
+    hipLaunchKernelGGL(lut_zero_pad_kernel, dim3(64), dim3(256), 0, s, (int8_t*)lut_out, (int)nq,
+                       n_sites_pad / 64, limbs);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq) { (void)nq; return scan_parts(n_ref); }
+
+extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_codes, int32_t n_sites_pad,
+                               const void* lut, int32_t nq, int limbs, int k, int64_t ref_offset,
+                               uint64_t* part_keys, int32_t n_parts, void* stream) {
+  SNV_CHECK_ARG(codes && lut && part_keys, "null pointer");
+  SNV_CHECK_ARG(k >= 1 && k <= 32, "k must be in [1, 32]");
+  SNV_CHECK_ARG(limbs == 1 || limbs == 2, "limbs");
+  SNV_CHECK_ARG(n_sites_pad % 64 == 0 && n_sites_pad <= 17 * 64 && ld_codes >= n_sites_pad, "site padding");
+  SNV_CHECK_ARG(ld_codes % 16 == 0 && ((uintptr_t)codes % 16) == 0, "codes must be 16-byte aligned rows");
+  SNV_CHECK_ARG(n_parts >= 1, "n_parts");
+  SNV_CHECK_ARG(n_ref + ref_offset < (1LL << 32), "panel index must fit 32 bits");
+  if (nq == 0) return 0;
+  long range = (n_ref + n_parts - 1) / n_parts;
+  range = ((range + 15) / 16) * 16;
+  if (range == 0) range = 16;
+  const int KS = n_sites_pad / 64;
+  dim3 g((unsigned)n_parts, (unsigned)(((nq + 15) / 16 + 3) / 4));
+  hipStream_t s = as_stream(stream);
+  const int8_t* L8 = (const int8_t*)lut;
+  evlog_begin(s);
+#define SCAN(KSM)                                                                                   \
+  do {                                                                                              \
+    if (limbs == 2) launch_scan<KSM, 2>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys); \
+    else launch_scan<KSM, 1>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys);           \
+  } while (0)
+  if (KS <= 4) SCAN(4);
+  else if (KS <= 8) SCAN(8);
+  else if (KS <= 16) SCAN(16);
+  else SCAN(17);
+#undef SCAN
+  SNV_LAUNCH_CHECK();
+  // algorithmic bytes: every code byte of the window once + LUT + partial lists
+  evlog_end(s, EV_KNN_SCAN, (double)n_ref * n_sites_pad + (double)nq * n_sites_pad * limbs +
+                            (double)n_parts * nq * k * 8.0);
+  return 0;
+}
+
+static int merge_group(int k) {
+  int kp = 1;
+  while (kp < k) kp <<= 1;
+  return 1024 / kp;
+}
+
+extern "C" size_t snvrag_topk_merge_ws_bytes(int32_t n_lists, int32_t nq, int k) {
+  const int G = merge_group(k);
+  const long l1 = (n_lists + G - 1) / G;
+  return (size_t)2 * (size_t)l1 * nq * k * sizeof(uint64_t) + 256;
+}
+
+extern "C" int snvrag_topk_merge(const uint64_t* keys, int32_t n_lists, int32_t nq, int k, uint64_t* out_keys,
+                                 void* ws, size_t ws_bytes, void* stream) {
+  SNV_CHECK_ARG(keys && out_keys, "null pointer");
+  SNV_CHECK_ARG(k >= 1 && k <= 1024, "k");
+  if (nq == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const int G = merge_group(k);
+  const uint64_t* cur = keys;
+  int n = n_lists;
+  uint64_t* bufs[2] = {nullptr, nullptr};
+  if (n > G) {
+    SNV_CHECK_ARG(ws && ws_bytes >= snvrag_topk_merge_ws_bytes(n_lists, nq, k), "merge workspace too small");
+    const size_t half = (size_t)((n_lists + G - 1) / G) * nq * k;
+    bufs[0] = (uint64_t*)ws;
+    bufs[1] = bufs[0] + half;
+  }
+  int flip = 0;
+  while (true) {
+    const int groups = (n + G - 1) / G;
+    uint64_t* dst = groups == 1 ? out_keys : bufs[flip];
+    hipLaunchKernelGGL(merge_kernel, dim3(groups, nq), dim3(256), 0, s, cur, n, nq, k, G, dst);
+    SNV_LAUNCH_CHECK();
+    if (groups == 1) break;
+    cur = dst;
+    n = groups;
+    flip ^= 1;
+  }
+  return 0;
+}
+
+extern "C" int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const int32_t* exps, const float* consts,
+                                 int64_t* idx_out, float* dist_out, void* stream) {
+  SNV_CHECK_ARG(keys && idx_out && (!dist_out || exps), "null pointer");
+  const long n = (long)nq * k;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(decode_kernel, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream), keys, nq, k, exps,
+                     consts, idx_out, dist_out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                               const uint8_t* codes, int64_t ld_codes, int32_t n_sites, const float* W,
+                               const float* pe, const float* Ar, int tok0, int tok1, int sos, int eos, int pad,
+                               void* out, void* stream) {
+  SNV_CHECK_ARG(idx && codes && W && pe && out, "null pointer");
+  SNV_CHECK_ARG(D % 8 == 0 && n_sites + 2 <= L, "shape");
+  if (nq == 0) return 0;
+  dim3 g((unsigned)cdiv(L, 64), (unsigned)nq);
+  hipStream_t s = as_stream(stream);
+  if (dtype_out == SNVRAG_BF16)
+    hipLaunchKernelGGL(rag_mean_kernel<bf16>, g, dim3(256), 0, s, (int)L, (int)D, k, idx, codes, (long)ld_codes,
+                       n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (bf16*)out);
+  else
+    hipLaunchKernelGGL(rag_mean_kernel<float>, g, dim3(256), 0, s, (int)L, (int)D, k, idx, codes, (long)ld_codes,
+                       n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (float*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_panel_synth(uint8_t* codes, int64_t n_ref, int64_t ld, int32_t n_sites, const float* af,
+                                  uint64_t seed, void* stream) {
+  SNV_CHECK_ARG(codes && af && ld % 16 == 0 && ld >= n_sites, "bad args");
+  if (n_ref == 0) return 0;
+  const long work = n_ref * (ld / 16);
+  const int grid = (int)std::min<long>(cdiv(work, 256), 65536);
+  hipLaunchKernelGGL(panel_synth_kernel, dim3(grid), dim3(256), 0, as_stream(stream), codes, (long)n_ref, (long)ld,
+                     n_sites, af, seed);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}

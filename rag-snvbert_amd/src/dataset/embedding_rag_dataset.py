@@ -1,0 +1,222 @@
+"""EmbeddingRAGDataset — v18 training/validation dataset with panel retrieval
+(reference: src/dataset/embedding_rag_dataset.py).
+
+Drop-in surface:
+  * ``process_batch_retrieval(batch, embedding_layer, device, k_retrieve=1) -> batch``
+    adds ``rag_emb_h1`` / ``rag_emb_h2`` on ``device``.  The reference fills a dense
+    [B, k, L, D] tensor and the model immediately takes its mean over k
+    (model/bert.py:176-179); here the K-mean is produced directly by the
+    ``rag_mean`` kernel as [B, 1, L, D] — the model consumes it identically
+    (bert.py:180-182) — and ``rag_idx_h1/h2`` [B, k] carry the neighbour indices.
+    ``dense=True`` restores the [B, k, L, D] layout for callers that need it.
+  * ``regenerate_masks(seed)``, ``clear_jit_cache()``, ``add_level()``,
+    ``window_masks``, ``ref_tokens_complete``, ``ref_af_windows``, ``jit_cache_win_idx``.
+
+Index: per window, the panel's allele codes are uploaded once to HBM
+(``PanelIndex``); unlike the reference's fp32 embedding cache (:334-377) the
+index does not depend on the mask or the weights, so a mask refresh or a weight
+update never forces a rebuild — ``jit_cache_win_idx`` is kept for API parity.
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict, defaultdict
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .dataset import PanelData, TrainDataset, Window
+from .utils import mask_probs, sequence_padding
+from .vocab import WordVocab
+
+MAX_SEQ_LEN = 1030
+
+
+class EmbeddingRAGDataset(TrainDataset):
+    def __init__(self, vocab, vcf, pos, panel, freq, window, type_to_idx, pop_to_idx, pos_to_idx,
+                 ref_gt: Optional[np.ndarray] = None, ref_pos: Optional[np.ndarray] = None,
+                 embedding_layer=None, build_ref_data: bool = True, n_gpu: int = 1,
+                 maf_mask_percentage: int = 10, use_dynamic_mask: bool = False, name: str = "default",
+                 index_cache_bytes: int = 64 << 30):
+        super().__init__(vocab, vcf, pos, panel, freq, window, type_to_idx, pop_to_idx, pos_to_idx)
+        self.maf_mask_percentage, self.use_dynamic_mask = maf_mask_percentage, use_dynamic_mask
+        self.current_epoch, self.name = 0, name
+        self.ref_tokens_complete: List[np.ndarray] = []
+        self.ref_alleles: List[np.ndarray] = []
+        self.raw_window_masks: List[np.ndarray] = []
+        self.window_masks: List[np.ndarray] = []
+        self.mask_version = 0
+        self.ref_af_windows: List[np.ndarray] = []
+        self.window_valid_indices: Dict[int, np.ndarray] = {}
+        self.window_actual_lens: List[int] = []
+        self.jit_cache_win_idx = -1
+        self.embedding_layer = embedding_layer
+        self.embed_dim = embedding_layer.embed_size if embedding_layer is not None else None
+        self._index_cache: "OrderedDict[int, object]" = OrderedDict()
+        self._index_cache_bytes = index_cache_bytes
+        if build_ref_data and ref_gt is not None:
+            self._load_ref_data_to_memory(ref_gt, ref_pos)
+
+    # ---------------------------------------------------------------- panel --
+    def _load_ref_data_to_memory(self, ref_gt: np.ndarray, ref_pos: np.ndarray) -> None:
+        """embedding_rag_dataset.py:79-208: per-window site match, AF, AF-guided mask, complete tokens."""
+        ref_pos = np.asarray(ref_pos)
+        for w in range(self.window_count):
+            sl = self._window_slice(w)
+            train_pos = self.pos[sl]
+            found = np.clip(np.searchsorted(ref_pos, train_pos), 0, len(ref_pos) - 1)
+            is_match = ref_pos[found] == train_pos
+            valid = np.where(is_match)[0]
+            ref_idx = found[is_match]
+            if len(ref_idx) < len(train_pos):
+                if len(valid) == 0:
+                    raise ValueError(f"window {w}: no panel sites (the reference skips it, which misaligns "
+                                     "window ids; refusing)")
+                train_pos = train_pos[valid]
+                self.window_valid_indices[w] = valid
+            n = len(train_pos)
+            self.window_actual_lens.append(n)
+            cols = np.array([self.pos_to_idx.get(p, -1) for p in train_pos])
+            af = np.where(cols >= 0, self.freq[3][5][np.maximum(cols, 0)], 0.0).astype(np.float32)
+            ref_af = sequence_padding(af, "float").astype(np.float32)
+            self.ref_af_windows.append(ref_af)
+            raw = self.generate_mask(n, probs=mask_probs(af, self._level))
+            self.raw_window_masks.append(raw)
+            self.window_masks.append(sequence_padding(raw, "int"))
+            alleles = np.asarray(ref_gt[ref_idx]).reshape(len(ref_idx), -1).T   # [n_haps, n]
+            self.ref_alleles.append(alleles.astype(np.int64))
+            self.ref_tokens_complete.append(self.tokenize(alleles, np.zeros(MAX_SEQ_LEN, np.int64)))
+
+    def clear_jit_cache(self) -> None:
+        self.jit_cache_win_idx = -1
+        self._index_cache.clear()
+
+    def regenerate_masks(self, seed: int) -> None:
+        """embedding_rag_dataset.py:228-283 (np.random.seed(seed*10000 + w))."""
+        self.mask_version += 1
+        for w in range(self.window_count):
+            n = self.window_actual_lens[w]
+            probs = mask_probs(self.ref_af_windows[w][1:1 + n], self._level)
+            np.random.seed(seed * 10000 + w)
+            raw = self.generate_mask(n, probs=probs)
+            self.raw_window_masks[w] = raw
+            self.window_masks[w] = sequence_padding(raw, "int")
+
+    def _apply_mask_to_tokens_gpu(self, tokens: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        out = tokens.clone()
+        out[:, mask == 1] = self.vocab.mask_index
+        return out
+
+    # ----------------------------------------------------------------- items --
+    def __getitem__(self, item: int) -> dict:
+        """embedding_rag_dataset.py:486-555: seeded AF-guided mask per (epoch|2024, window)."""
+        w = item % self.window_count
+        # panel-filtered windows: featurise only the matched sites (the reference indexes its
+        # padded arrays with the unpadded site filter here, :498-507, and raises KeyError on 'label')
+        out = self.base_item(item, self.window_valid_indices.get(w))
+        n = self.window_actual_lens[w]
+        af = self.ref_af_windows[w][1:1 + n]
+        seed = self.current_epoch if self.name == "train" else 2024
+        old = np.random.get_state()
+        np.random.seed(seed * 10000 + w)
+        raw = self.generate_mask(n, probs=mask_probs(af, self._level))
+        np.random.set_state(old)
+        mask = sequence_padding(raw, "int")
+        out["mask"] = mask
+        out["hap_1"] = self.tokenize(out["hap1_nomask"], mask)
+        out["hap_2"] = self.tokenize(out["hap2_nomask"], mask)
+        return self.to_tensors(out)
+
+    # ------------------------------------------------------------- retrieval --
+    def panel_index(self, w: int, device) -> "object":
+        from ..retrieval import PanelIndex
+        idx = self._index_cache.get(w)
+        if idx is None or idx.codes.device != torch.device(device):
+            idx = PanelIndex.from_alleles(self.ref_alleles[w], self.ref_af_windows[w], device)
+            self._index_cache[w] = idx
+            while sum(i.nbytes for i in self._index_cache.values()) > self._index_cache_bytes and \
+                    len(self._index_cache) > 1:
+                self._index_cache.popitem(last=False)
+        else:
+            self._index_cache.move_to_end(w)
+        self.jit_cache_win_idx = w
+        return idx
+
+    def process_batch_retrieval(self, batch: dict, embedding_layer, device, k_retrieve: int = 1,
+                                dense: bool = False, limbs: int = 2) -> dict:
+        return retrieve(self, batch, embedding_layer, device, k_retrieve, self.window_masks, dense, limbs)
+
+    @classmethod
+    def from_arrays(cls, vocab, vcf, pos, pop_list, freq, window_bounds, pop_to_idx, pos_to_idx,
+                    ref_gt, ref_pos, embedding_layer=None, name="default", type_to_idx=None) -> "EmbeddingRAGDataset":
+        win = Window(np.asarray(window_bounds)[:, 0], np.asarray(window_bounds)[:, 1])
+        return cls(vocab, vcf, pos, PanelData(pop_list), freq, win, type_to_idx or {}, pop_to_idx, pos_to_idx,
+                   ref_gt=ref_gt, ref_pos=ref_pos, embedding_layer=embedding_layer, name=name)
+
+
+def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.ndarray],
+             dense: bool = False, limbs: int = 2) -> dict:
+    """Shared retrieval body of the train/val and infer datasets (see module docstring)."""
+    from ..engine import engine_for
+    from .. import kernels as K
+    eng = engine_for(embedding_layer)
+    P = eng.packed()
+    dev = torch.device(device)
+    h1 = batch["hap_1"].to(dev, non_blocking=True).long()
+    h2 = batch["hap_2"].to(dev, non_blocking=True).long()
+    af = batch["af"].to(dev, non_blocking=True).float()
+    B, L = h1.shape
+    D = P.W.shape[1]
+    groups = defaultdict(list)
+    for i, w in enumerate(batch["window_idx"]):
+        groups[int(w)].append(i)
+    rag_mean = torch.empty(2 * B, L, D, device=dev, dtype=eng.dtype)
+    rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
+    for w, rows in groups.items():
+        index = ds.panel_index(w, dev)
+        rows_t = torch.tensor(rows, device=dev, dtype=torch.long)
+        tok = torch.cat([h1[rows_t], h2[rows_t]], 0).contiguous()
+        n = index.n_sites
+        site_mask = torch.as_tensor(np.asarray(masks[w][1:1 + n], np.uint8), device=dev)
+        ref_af = index.ref_af
+        # A_q - A_r vanishes when the query AF rows equal the panel's window AF (always for
+        # windows built from one freq table); otherwise pass both AF embeddings (exact LUT form).
+        afw = af[rows_t]
+        same = bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw)))
+        Ar_emb = eng.af_embedding(ref_af.unsqueeze(0)).float()[0].contiguous() if P.af is not None else None
+        Aq = Ar = None
+        if not same and P.af is not None:
+            Aq = eng.af_embedding(afw).float().contiguous()
+            Ar = Ar_emb
+        idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
+        means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
+        nb = len(rows)
+        rag_mean[rows_t] = means[:nb]
+        rag_mean[rows_t + B] = means[nb:]
+        rag_idx[rows_t] = idx[:nb]
+        rag_idx[rows_t + B] = idx[nb:]
+    batch["rag_idx_h1"], batch["rag_idx_h2"] = rag_idx[:B], rag_idx[B:]
+    if dense:
+        raise NotImplementedError("dense [B,k,L,D] neighbour embeddings: use rag_idx_* with "
+                                  "BERTEmbedding on the retrieved complete tokens")
+    batch["rag_emb_h1"] = rag_mean[:B].unsqueeze(1)
+    batch["rag_emb_h2"] = rag_mean[B:].unsqueeze(1)
+    batch["rag_mean"] = rag_mean
+    return batch
+
+
+def embedding_rag_collate_fn(batch_list, dataset=None, embedding_layer=None, k_retrieve=1):
+    """CPU-only collate (embedding_rag_dataset.py:609-645)."""
+    out = defaultdict(list)
+    for s in batch_list:
+        for key in s:
+            out[key].append(s[key])
+    for key in out:
+        if key in ("window_idx", "hap1_nomask", "hap2_nomask"):
+            continue
+        try:
+            out[key] = torch.stack(out[key])
+        except (RuntimeError, TypeError):
+            pass
+    return dict(out)

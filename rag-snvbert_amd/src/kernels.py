@@ -1,0 +1,240 @@
+"""Typed torch-tensor wrappers over the C ABI (one function per ``snvrag_*`` entry).
+
+All tensors must be contiguous device tensors; outputs are allocated here unless
+passed in.  Every call runs on the current HIP stream.  No CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import native as N
+from .native import check, ptr, stream_ptr
+
+_dt = N.dtype_code
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return t
+
+
+# ------------------------------------------------------------------ linear --
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+           act: int = N.ACT_NONE, slope: float = 0.0,
+           row1: Optional[Tuple[torch.Tensor, int, torch.Tensor]] = None,
+           row2: Optional[Tuple[torch.Tensor, int, torch.Tensor]] = None,
+           row_period: int = 0, resid: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """out[m, n] = act(x[m] . w[n] + bias[n] + row1[m]*col1[n] + row2[m]*col2[n]) + resid[m, n]."""
+    N.require_gpu(x, w)
+    K = x.shape[-1]
+    M = x.numel() // K
+    Nn = w.shape[0]
+    assert w.shape[1] == K and w.dtype == x.dtype, (tuple(w.shape), K, w.dtype, x.dtype)
+    od = out_dtype or (out.dtype if out is not None else x.dtype)
+    if out is None:
+        out = torch.empty(*x.shape[:-1], Nn, device=x.device, dtype=od)
+    e = N.Epilogue()
+    e.bias = ptr(bias)
+    if row1 is not None:
+        e.row1, e.row1_stride, e.col1 = ptr(row1[0]), row1[1], ptr(row1[2])
+    if row2 is not None:
+        e.row2, e.row2_stride, e.col2 = ptr(row2[0]), row2[1], ptr(row2[2])
+    e.row_period, e.act, e.slope = row_period, act, slope
+    if resid is not None:
+        assert resid.dtype == od and resid.shape[-1] == Nn
+        e.resid, e.ld_resid = ptr(_c(resid)), Nn
+    check(N.lib().snvrag_linear(_dt(x.dtype), _dt(od), M, Nn, K, ptr(_c(x)), K, ptr(_c(w)), K,
+                                ptr(out), Nn, C.byref(e), stream_ptr()), "linear")
+    return out
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, *, resid: Optional[torch.Tensor] = None,
+              eps: float = 1e-5, out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
+              post_base: Optional[torch.Tensor] = None, post_scale: float = 1.0,
+              post_af: Optional[torch.Tensor] = None, af_period: int = 0, maf_weight: bool = False,
+              act: int = N.ACT_NONE) -> torch.Tensor:
+    N.require_gpu(x)
+    Nn = x.shape[-1]
+    M = x.numel() // Nn
+    od = out_dtype or (out.dtype if out is not None else x.dtype)
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=od)
+    p = None
+    if post_base is not None or post_af is not None or act != N.ACT_NONE:
+        p = N.LnPost()
+        p.base, p.ld_base, p.scale = ptr(post_base), Nn, post_scale
+        p.af, p.af_period, p.maf_weight, p.act = ptr(post_af), af_period, int(maf_weight), act
+    check(N.lib().snvrag_layernorm(_dt(x.dtype), _dt(od), M, Nn, ptr(_c(x)), Nn,
+                                   ptr(resid), Nn, ptr(g), ptr(b), eps, ptr(out), Nn,
+                                   C.byref(p) if p is not None else None, stream_ptr()), "layernorm")
+    return out
+
+
+def attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    N.require_gpu(qkv)
+    D = heads * dh
+    if out is None:
+        out = torch.empty(nseq * L, D, device=qkv.device, dtype=qkv.dtype)
+    check(N.lib().snvrag_attention(_dt(qkv.dtype), nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1],
+                                   ptr(out), D, 1.0 / float(dh) ** 0.5, stream_ptr()), "attention")
+    return out
+
+
+# ---------------------------------------------------------------- embedding --
+def af_features(af: torch.Tensor, freqs: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    N.require_gpu(af)
+    nb = freqs.numel()
+    out = torch.empty(*af.shape, 2 * nb, device=af.device, dtype=dtype)
+    check(N.lib().snvrag_af_features(_dt(dtype), af.numel(), ptr(_c(af)), ptr(_c(freqs)), nb, ptr(out),
+                                     stream_ptr()), "af_features")
+    return out
+
+
+def embed_tokens(tok: torch.Tensor, W: torch.Tensor, pe: torch.Tensor, afemb: Optional[torch.Tensor],
+                 af_period: int, dtype: torch.dtype, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    N.require_gpu(tok)
+    assert tok.dtype == torch.int64
+    nseq, L = tok.shape
+    D = W.shape[1]
+    if out is None:
+        out = torch.empty(nseq, L, D, device=tok.device, dtype=dtype)
+    check(N.lib().snvrag_embed_tokens(_dt(dtype), nseq, L, D, ptr(_c(tok)), ptr(_c(W)), W.shape[0],
+                                      ptr(_c(pe)), ptr(afemb), _dt(afemb.dtype) if afemb is not None else 0,
+                                      af_period, ptr(out), stream_ptr()), "embed_tokens")
+    return out
+
+
+def posfeat(pos: torch.Tensor, w: "N.PosfeatW") -> torch.Tensor:
+    N.require_gpu(pos)
+    B, L = pos.shape
+    out = torch.empty(B, L, device=pos.device, dtype=torch.float32)
+    check(N.lib().snvrag_posfeat(B, L, ptr(_c(pos)), C.byref(w), ptr(out), stream_ptr()), "posfeat")
+    return out
+
+
+def af_gate(af: torch.Tensor, af_p: torch.Tensor, w: "N.AfGateW", D: int, dtype: torch.dtype) -> torch.Tensor:
+    N.require_gpu(af)
+    out = torch.empty(*af.shape, D, device=af.device, dtype=dtype)
+    check(N.lib().snvrag_af_gate(_dt(dtype), af.numel(), D, ptr(_c(af)), ptr(_c(af_p)), C.byref(w), ptr(out),
+                                 stream_ptr()), "af_gate")
+    return out
+
+
+def rag_concat(q: torch.Tensor, rag: torch.Tensor, wgt: torch.Tensor, period: int) -> torch.Tensor:
+    D = q.shape[-1]
+    M = q.numel() // D
+    out = torch.empty(*q.shape[:-1], 2 * D, device=q.device, dtype=q.dtype)
+    check(N.lib().snvrag_rag_weighted_concat(_dt(q.dtype), M, D, ptr(_c(q)), ptr(_c(rag)), ptr(_c(wgt)),
+                                             period, ptr(out), stream_ptr()), "rag_concat")
+    return out
+
+
+def hap_head_out(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_logits: bool = True):
+    K = h.shape[-1]
+    M = h.numel() // K
+    probs = torch.empty(*h.shape[:-1], 2, device=h.device, dtype=torch.float32)
+    logits = torch.empty_like(probs) if want_logits else None
+    check(N.lib().snvrag_hap_head_out(_dt(h.dtype), M, K, ptr(_c(h)), K, ptr(_c(w)), ptr(_c(b)),
+                                      ptr(logits), ptr(probs), stream_ptr()), "hap_head_out")
+    return logits, probs
+
+
+def gt_head(p1, p2, ref, het, hom, period: int, w: "N.GtW") -> torch.Tensor:
+    M = p1.numel() // 2
+    out = torch.empty(*p1.shape[:-1], 4, device=p1.device, dtype=torch.float32)
+    check(N.lib().snvrag_gt_head(M, ptr(_c(p1)), ptr(_c(p2)), ptr(_c(ref)), ptr(_c(het)), ptr(_c(hom)), period,
+                                 C.byref(w), ptr(out), stream_ptr()), "gt_head")
+    return out
+
+
+# ---------------------------------------------------------------------- kNN --
+def knn_lut(tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, n_sites: int, n_sites_pad: int,
+            limbs: int = 2, Aq: Optional[torch.Tensor] = None, aq_period: int = 0,
+            Ar: Optional[torch.Tensor] = None, tok0: int = 5, tok1: int = 6, mask_tok: int = 4):
+    """Returns (lut bytes tensor, exps int32 [nq], consts f32 [nq])."""
+    N.require_gpu(tok_q)
+    nq, L = tok_q.shape
+    D = W.shape[1]
+    nbytes = N.lib().snvrag_knn_lut_bytes(nq, n_sites_pad, limbs)
+    lut = torch.empty(nbytes, device=tok_q.device, dtype=torch.int8)
+    exps = torch.empty(nq, device=tok_q.device, dtype=torch.int32)
+    consts = torch.empty(nq, device=tok_q.device, dtype=torch.float32)
+    check(N.lib().snvrag_knn_lut(nq, L, D, ptr(_c(tok_q)), ptr(_c(W)), ptr(Aq), aq_period, ptr(Ar),
+                                 ptr(_c(site_mask)), n_sites, n_sites_pad, tok0, tok1, mask_tok, limbs,
+                                 ptr(lut), ptr(exps), ptr(consts), stream_ptr()), "knn_lut")
+    return lut, exps, consts
+
+
+def knn_scan(codes: torch.Tensor, n_sites_pad: int, lut: torch.Tensor, nq: int, limbs: int, k: int,
+             ref_offset: int = 0, n_parts: Optional[int] = None) -> torch.Tensor:
+    n_ref, ld = codes.shape
+    if n_parts is None:
+        n_parts = N.lib().snvrag_knn_scan_parts(n_ref, nq)
+    parts = torch.empty(n_parts, nq, k, device=codes.device, dtype=torch.int64)
+    check(N.lib().snvrag_knn_scan(ptr(_c(codes)), n_ref, ld, n_sites_pad, ptr(lut), nq, limbs, k, ref_offset,
+                                  ptr(parts), n_parts, stream_ptr()), "knn_scan")
+    return parts
+
+
+def topk_merge(keys: torch.Tensor, k: int) -> torch.Tensor:
+    """keys int64 view of uint64 [n_lists, nq, k] -> [nq, k]."""
+    n_lists, nq, kk = keys.shape
+    assert kk == k
+    out = torch.empty(nq, k, device=keys.device, dtype=torch.int64)
+    wsb = N.lib().snvrag_topk_merge_ws_bytes(n_lists, nq, k)
+    ws = torch.empty(wsb, device=keys.device, dtype=torch.uint8)
+    check(N.lib().snvrag_topk_merge(ptr(_c(keys)), n_lists, nq, k, ptr(out), ptr(ws), wsb, stream_ptr()),
+          "topk_merge")
+    return out
+
+
+def knn_decode(keys: torch.Tensor, exps: Optional[torch.Tensor] = None, consts: Optional[torch.Tensor] = None):
+    nq, k = keys.shape
+    idx = torch.empty(nq, k, device=keys.device, dtype=torch.int64)
+    dist = torch.empty(nq, k, device=keys.device, dtype=torch.float32) if exps is not None else None
+    check(N.lib().snvrag_knn_decode(ptr(_c(keys)), nq, k, ptr(exps), ptr(consts), ptr(idx), ptr(dist),
+                                    stream_ptr()), "knn_decode")
+    return idx, dist
+
+
+def rag_mean(idx: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor, pe: torch.Tensor,
+             Ar: Optional[torch.Tensor], L: int, dtype: torch.dtype, tok0=5, tok1=6, sos=2, eos=3, pad=0):
+    nq, k = idx.shape
+    D = W.shape[1]
+    out = torch.empty(nq, L, D, device=idx.device, dtype=dtype)
+    check(N.lib().snvrag_rag_mean(_dt(dtype), nq, L, D, k, ptr(_c(idx)), ptr(_c(codes)), codes.shape[1], n_sites,
+                                  ptr(_c(W)), ptr(_c(pe)), ptr(Ar), tok0, tok1, sos, eos, pad, ptr(out),
+                                  stream_ptr()), "rag_mean")
+    return out
+
+
+def panel_synth(n_ref: int, n_sites: int, af: torch.Tensor, seed: int, ld: Optional[int] = None) -> torch.Tensor:
+    N.require_gpu(af)
+    ld = ld or ((n_sites + 63) // 64) * 64
+    codes = torch.empty(n_ref, ld, device=af.device, dtype=torch.uint8)
+    check(N.lib().snvrag_panel_synth(ptr(codes), n_ref, ld, n_sites, ptr(_c(af)), seed, stream_ptr()),
+          "panel_synth")
+    return codes
+
+
+def encoder_forward(x: torch.Tensor, layers: Sequence["N.LayerW"], heads: int, ws: torch.Tensor) -> torch.Tensor:
+    nseq, L, D = x.shape
+    arr = (N.LayerW * len(layers))(*layers)
+    check(N.lib().snvrag_encoder_forward(_dt(x.dtype), nseq, L, D, heads, len(layers), arr, ptr(_c(x)),
+                                         ptr(ws), ws.numel(), stream_ptr()), "encoder_forward")
+    return x
+
+
+def encoder_ws_bytes(dtype: torch.dtype, nseq: int, L: int, D: int, heads: int) -> int:
+    return int(N.lib().snvrag_encoder_ws_bytes(_dt(dtype), nseq, L, D, heads))
+
+
+def selftest_mfma() -> int:
+    return int(N.lib().snvrag_selftest_mfma(stream_ptr()))

@@ -1,0 +1,33 @@
+"""Panel sharding across ranks: each rank holds a contiguous
+range of panel haplotypes, computes its exact local top-k with GLOBAL indices
+(ref_offset), the partial lists are all-gathered over RCCL (xGMI) and merged
+with the same (distance, index) order — identical to the single-GPU result
+because every key carries its global index.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def merge_keys_gathered(gathered: torch.Tensor, k: int,
+                        merge_fn: Optional[Callable[[torch.Tensor, int], torch.Tensor]] = None) -> torch.Tensor:
+    """gathered: [world, nq, k] key lists -> [nq, k].  merge_fn defaults to the HIP merge kernel."""
+    if merge_fn is None:
+        from .. import kernels as K
+        merge_fn = K.topk_merge
+    return merge_fn(gathered.contiguous(), k)
+
+
+def sharded_search(local_keys: torch.Tensor, k: int, group=None,
+                   merge_fn: Optional[Callable[[torch.Tensor, int], torch.Tensor]] = None) -> torch.Tensor:
+    """All-gather every rank's [nq, k] local top-k keys and merge them (one collective per batch)."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local_keys
+    out = torch.empty((world,) + tuple(local_keys.shape), dtype=local_keys.dtype, device=local_keys.device)
+    dist.all_gather_into_tensor(out, local_keys.contiguous(), group=group)
+    return merge_keys_gathered(out, k, merge_fn)

@@ -1,0 +1,228 @@
+"""GPU parity of the individual HIP kernels (called through the C ABI).
+
+Integer/index work is checked bit-exactly against the ORACLE; floating-point
+kernels against a plain torch fp32 (float64 where stated) reference of the same op.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import knn_np  # noqa: E402
+
+
+def K():
+    from src import kernels
+    return kernels
+
+
+def N():
+    from src import native
+    return native
+
+
+DEV = "cuda"
+
+
+def test_mfma_layout_selftest():
+    assert K().selftest_mfma() == 0
+
+
+# ---------------------------------------------------------------------- GEMM --
+def _ref_linear(x, w, b, act, slope, r1=None, c1=None, r2=None, c2=None, resid=None):
+    y = x.double() @ w.double().T
+    if b is not None:
+        y = y + b.double()
+    if r1 is not None:
+        y = y + r1.double()[:, None] * c1.double()[None]
+    if r2 is not None:
+        y = y + r2.double()[:, None] * c2.double()[None]
+    if act == 1:
+        y = torch.nn.functional.gelu(y)
+    elif act == 2:
+        y = torch.nn.functional.leaky_relu(y, slope)
+    elif act == 3:
+        y = torch.sigmoid(y)
+    if resid is not None:
+        y = y + resid.double()
+    return y
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,Nn,Kk", [(1000, 384, 384), (257, 1152, 64), (130, 1536, 384), (64, 384, 1536), (3, 8, 8)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_linear(dt, M, Nn, Kk, act):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + Nn + act)
+    x = torch.randn(M, Kk, generator=g).to(DEV, dt)
+    w = (torch.randn(Nn, Kk, generator=g) / math.sqrt(Kk)).to(DEV, dt)
+    b = torch.randn(Nn, generator=g).to(DEV)
+    period = max(1, M // 3)
+    r1 = torch.randn(period, generator=g).to(DEV)
+    c1 = torch.randn(Nn, generator=g).to(DEV)
+    r2 = torch.randn(period * 2, generator=g).to(DEV)
+    c2 = torch.randn(Nn, generator=g).to(DEV)
+    resid = torch.randn(M, Nn, generator=g).to(DEV, dt)
+    out = K().linear(x, w, b, act=act, slope=0.1, row1=(r1, 1, c1), row2=(r2, 2, c2), row_period=period,
+                     resid=resid)
+    rows = torch.arange(M, device=DEV) % period
+    ref = _ref_linear(x.float(), w.float(), b, act, 0.1, r1[rows], c1, r2[rows * 2], c2, resid.float())
+    tol = 2e-5 if dt == torch.float32 else 2e-2
+    torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol * 4)
+
+
+def test_linear_bf16_to_f32_and_plain():
+    x = torch.randn(300, 256, device=DEV).to(torch.bfloat16)
+    w = torch.randn(72, 256, device=DEV).to(torch.bfloat16)
+    out = K().linear(x, w, out_dtype=torch.float32)
+    torch.testing.assert_close(out.double(), x.double() @ w.double().T, rtol=1e-5, atol=1e-4)
+
+
+# ------------------------------------------------------------------ layernorm --
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [16, 384, 1536])
+def test_layernorm_with_residual_and_post(dt, n):
+    M = 777
+    x = torch.randn(M, n, device=DEV).to(dt)
+    r = torch.randn(M, n, device=DEV).to(dt)
+    gm, bt = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    ref = torch.nn.functional.layer_norm((x.float() + r.float()), (n,), gm, bt, 1e-5)
+    out = K().layernorm(x, gm, bt, resid=r)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+    # rag-fusion tail: base + scale * LN(x) * clamp(log1p(1/(maf+1e-6)), 3)
+    af = torch.rand(M // 3 + 1, device=DEV)
+    base = torch.randn(M, n, device=DEV).to(dt)
+    out2 = K().layernorm(x, gm, bt, post_base=base, post_scale=0.37, post_af=af, af_period=af.numel(),
+                         maf_weight=True, act=1)
+    a = af[torch.arange(M, device=DEV) % af.numel()]
+    maf = torch.minimum(a, 1 - a)
+    mw = torch.log1p(1.0 / (maf + 1e-6)).clamp(max=3.0)
+    y = torch.nn.functional.gelu(torch.nn.functional.layer_norm(x.float(), (n,), gm, bt, 1e-5))
+    torch.testing.assert_close(out2.float(), base.float() + 0.37 * y * mw[:, None], rtol=tol, atol=tol * 2)
+
+
+# ------------------------------------------------------------------ attention --
+def _ref_attn(qkv, nseq, L, H, dh):
+    q, k, v = qkv.double().view(nseq, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    o = torch.softmax(s, -1) @ v
+    return o.permute(0, 2, 1, 3).reshape(nseq * L, H * dh)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nseq,L,H,dh", [(2, 1030, 12, 32), (3, 70, 4, 16), (1, 130, 8, 48), (2, 257, 6, 64)])
+def test_attention(dt, nseq, L, H, dh):
+    qkv = (torch.randn(nseq * L, 3 * H * dh, device=DEV) * 1.5).to(dt)
+    out = K().attention(qkv, nseq, L, H, dh)
+    ref = _ref_attn(qkv.float(), nseq, L, H, dh)
+    tol = 2e-5 if dt == torch.float32 else 2e-2
+    torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol)
+
+
+# ------------------------------------------------------------------------ kNN --
+def decode_lut(lut: torch.Tensor, nq: int, n_sites_pad: int, limbs: int) -> np.ndarray:
+    """Inverse of the fragment layout [qt][limb][ks][lane][16] -> int32 dq[q, s]."""
+    KS = n_sites_pad // 64
+    nqt = (nq + 15) // 16
+    b = lut.cpu().numpy().view(np.int8).reshape(nqt, limbs, KS, 4, 16, 16)   # [qt][limb][ks][g][li][j]
+    b = b.transpose(0, 4, 1, 2, 3, 5).reshape(nqt * 16, limbs, n_sites_pad).astype(np.int32)
+    dq = b[:, 0] * 128 + b[:, 1] if limbs == 2 else b[:, 0]
+    return dq[:nq]
+
+
+def _rand_case(n_ref, n_sites, nq, seed, tie_heavy=False):
+    rng = np.random.default_rng(seed)
+    W = rng.standard_normal((12, 64)).astype(np.float32)
+    af = rng.beta(0.3, 3.0, n_sites)
+    panel = (rng.random((n_ref, n_sites)) < af).astype(np.uint8)
+    if tie_heavy:
+        panel[: n_ref // 2] = panel[0]
+    q_alle = panel[rng.integers(0, n_ref, nq)] ^ (rng.random((nq, n_sites)) < 0.05)
+    site_mask = (rng.random(n_sites) < 0.4).astype(np.uint8)
+    L = 1030
+    tok = np.zeros((nq, L), np.int64)
+    tok[:, 0] = 2
+    tok[:, 1:1 + n_sites] = np.where(site_mask[None] == 1, 4, 5 + q_alle)
+    tok[:, 1 + n_sites] = 3
+    if not tie_heavy:   # a few query positions masked where the panel is not (misaligned masks)
+        tok[:, 1:1 + n_sites][:, rng.random(n_sites) < 0.05] = 4
+    return W, panel, site_mask, tok
+
+
+@pytest.mark.parametrize("n_ref,n_sites,nq,k,limbs,tie", [
+    (5000, 300, 20, 8, 2, False), (4099, 1020, 48, 32, 2, True), (3000, 512, 64, 32, 1, True),
+    (777, 1028, 70, 4, 2, False), (10, 200, 5, 32, 2, False), (33, 64, 17, 1, 1, True)])
+def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
+    from src.retrieval import PanelIndex
+    W, panel, site_mask, tok = _rand_case(n_ref, n_sites, nq, n_ref + nq, tie)
+    idx_t = PanelIndex.from_alleles(panel, np.zeros(1030, np.float32), DEV)
+    Wt = torch.from_numpy(W).to(DEV)
+    smask = torch.from_numpy(site_mask).to(DEV)
+    idx, dist, keys, lut, exps = idx_t.search(torch.from_numpy(tok).to(DEV), Wt, smask, k, limbs=limbs,
+                                              return_keys=True)
+    # LUT vs oracle quantisation of the fp64 Delta (<= 1 quantum, identical exponents)
+    delta = knn_np.lut_delta(W, tok, None, site_mask)
+    dq_o, e_o = knn_np.quantize_lut(delta, limbs)
+    dq_g = decode_lut(lut, nq, idx_t.n_sites_pad, limbs)
+    np.testing.assert_array_equal(exps.cpu().numpy(), e_o)
+    assert np.abs(dq_g[:, :n_sites] - dq_o).max() <= 1
+    assert (dq_g[:, n_sites:] == 0).all()
+    # scan + merge bit-exact against the oracle on the SAME integer LUT
+    oi, od = knn_np.knn(panel, dq_g[:, :n_sites], k)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    kk = keys.cpu().numpy().view(np.uint64)
+    valid = oi >= 0
+    np.testing.assert_array_equal(kk[valid], knn_np.pack_key(od, oi)[valid])
+
+
+def test_knn_shard_offsets_and_merge():
+    """Panel split in 3 contiguous shards with global offsets + merge == unsplit search."""
+    from src.retrieval import PanelIndex
+    W, panel, site_mask, tok = _rand_case(3001, 400, 24, 5, True)
+    Wt, smask, tq = torch.from_numpy(W).to(DEV), torch.from_numpy(site_mask).to(DEV), torch.from_numpy(tok).to(DEV)
+    full = PanelIndex.from_alleles(panel, np.zeros(1030, np.float32), DEV)
+    _, _, keys_full, lut, _ = full.search(tq, Wt, smask, 16, return_keys=True)
+    bounds = [0, 1000, 2100, 3001]
+    parts = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sh = PanelIndex.from_alleles(panel[a:b], np.zeros(1030, np.float32), DEV, ref_offset=a)
+        parts.append(sh.scan_keys(lut, 24, 2, 16))
+    merged = K().topk_merge(torch.stack(parts), 16)
+    torch.testing.assert_close(merged, keys_full, rtol=0, atol=0)
+
+
+def test_panel_synth_matches_hash_restatement():
+    from src.dataset.synthetic import hash_uniform
+    af = torch.rand(300, device=DEV) * 0.5
+    codes = K().panel_synth(257, 300, af, seed=11)
+    r, c = np.meshgrid(np.arange(257), np.arange(300), indexing="ij")
+    exp = (hash_uniform(11, r, c) < af.cpu().numpy().astype(np.float64)[None]).astype(np.uint8)
+    np.testing.assert_array_equal(codes[:, :300].cpu().numpy(), exp)
+    assert (codes[:, 300:] == 0).all()
+
+
+def test_rag_mean_vs_oracle():
+    from oracle import model_np
+    rng = np.random.default_rng(9)
+    D, L, n_sites, n_ref, k = 64, 1030, 500, 200, 8
+    W = rng.standard_normal((12, D)).astype(np.float32)
+    pe = rng.standard_normal((L, D)).astype(np.float32)
+    Ar = rng.standard_normal((L, D)).astype(np.float32)
+    panel = rng.integers(0, 2, (n_ref, n_sites)).astype(np.uint8)
+    idx = rng.integers(0, n_ref, (6, k))
+    idx[5, 3:] = -1                                    # missing neighbours are skipped
+    from src.retrieval import PanelIndex
+    pi = PanelIndex.from_alleles(panel, np.zeros(L, np.float32), DEV)
+    out = K().rag_mean(torch.from_numpy(idx).to(DEV), pi.codes, n_sites, torch.from_numpy(W).to(DEV),
+                       torch.from_numpy(pe).to(DEV), torch.from_numpy(Ar).to(DEV), L, torch.float32)
+    toks = np.zeros((n_ref, L), np.int64)
+    toks[:, 0], toks[:, 1:1 + n_sites], toks[:, 1 + n_sites] = 2, 5 + panel, 3
+    ref = np.zeros((6, L, D), np.float32)
+    for q in range(6):
+        v = idx[q][idx[q] >= 0]
+        ref[q] = (W[toks[v]] + pe[None] + Ar[None]).mean(0)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
