@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 1
+#define SNVRAG_ABI_VERSION 2
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -54,11 +54,28 @@ typedef struct {
   int64_t row_period;          /* 0 = no wrap */
   int act; float slope;
   const void* resid; int64_t ld_resid;
+  /* LayerNorm over the whole output row, fused (needs N in {64,128,256,384}):
+   *   y = ln_act(LN(v) * ln_g + ln_b);  optional y = post_base + post_scale * y * maf(post_af[m])  */
+  const float* ln_g; const float* ln_b; float ln_eps; int ln_act;
+  const void* post_base; int64_t ld_post; float post_scale;
+  const float* post_af; int64_t post_af_period; int post_maf;
+  /* per-(column tile, row) float2 (sum, sumsq) of the output: [N/tile][M] (tile = 384 when N % 384 == 0) */
+  float* stats_out;
 } snvrag_epilogue_t;
+
+/* LayerNorm applied to the A operand while staging it (stats from a previous stats_out):
+ * A'[m,k] = (A[m,k] - mean_m) * rstd_m * g[k] + b[k], mean/var from sum over n_parts partials / dim */
+typedef struct {
+  const float* stats; int n_parts; int64_t dim; const float* g; const float* b; float eps;
+} snvrag_anorm_t;
 
 int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                   const void* A, int64_t lda, const void* W, int64_t ldw,
                   void* C, int64_t ldc, const snvrag_epilogue_t* epi, void* stream);
+int snvrag_linear_ex(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
+                     const void* A, int64_t lda, const void* W, int64_t ldw,
+                     void* C, int64_t ldc, const snvrag_epilogue_t* epi,
+                     const snvrag_anorm_t* anorm, void* stream);
 
 /* LayerNorm over the last dim, eps as given (torch default 1e-5):
  *   y = LN(x + r) * gamma + beta                  (r optional: residual of sublayer.py:15-16)

@@ -38,7 +38,7 @@ extern "C" size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, in
   const int esz = dtype == SNVRAG_BF16 ? 2 : 4;
   const int64_t c = chunk_seqs(nseq, L, D, esz);
   const size_t M = (size_t)c * L;
-  return M * (size_t)D * 9 * esz + 4096;
+  return M * (size_t)D * 9 * esz + M * 64 * 8 + 8192;
 }
 
 extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,
@@ -56,9 +56,15 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
   void* att = carve(Mc * D);
   void* x1 = carve(Mc * D);
   void* h = carve(Mc * 4 * D);
+  // FFN LayerNorm statistics: [N-tiles of the 4D GEMM][Mc] float2
+  const int n_stat_parts = (4 * D) % 384 == 0 ? (4 * D) / 384 : (4 * D) % 256 == 0 ? (4 * D) / 256
+                           : (4 * D) % 128 == 0 ? (4 * D) / 128 : (4 * D) / 64;
+  w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
+  void* stats = w; w += ((Mc * n_stat_parts * 8 + 255) / 256) * 256;
   const int dh = D / heads;
   const float scale = 1.0f / sqrtf((float)dh);
 
+  const bool fused = (D == 64 || D == 128 || D == 256 || D == 384) && !getenv("SNVRAG_UNFUSED_LN");
   for (int64_t s0 = 0; s0 < nseq; s0 += cs) {
     const int64_t ns = std::min<int64_t>(cs, nseq - s0);
     const int64_t M = ns * L;
@@ -72,6 +78,26 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       if (rc) return rc;
       rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, scale, stream);
       if (rc) return rc;
+      if (fused) {
+        // x1 = LN1(x + attn Wo^T + bo)                       (one launch)
+        e = snvrag_epilogue_t{};
+        e.bias = ly.b_o; e.resid = xc; e.ld_resid = D; e.ln_g = ly.ln1_g; e.ln_b = ly.ln1_b; e.ln_eps = 1e-5f;
+        rc = snvrag_linear(dtype, dtype, M, D, D, att, D, ly.w_o, D, x1, D, &e, stream);
+        if (rc) return rc;
+        // h = lrelu(x1 W1^T + b1), row stats of h for the FFN LayerNorm (one launch)
+        e = snvrag_epilogue_t{};
+        e.bias = ly.b1; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.stats_out = (float*)stats;
+        rc = snvrag_linear(dtype, dtype, M, 4 * D, D, x1, D, ly.w1, D, h, 4 * D, &e, stream);
+        if (rc) return rc;
+        // x = LN2(x1 + lrelu(LN_f(h) W2^T + b2)); LN_f applied to A while staging (one launch)
+        snvrag_anorm_t an{(const float*)stats, n_stat_parts, 4 * D, ly.lnf_g, ly.lnf_b, 1e-5f};
+        e = snvrag_epilogue_t{};
+        e.bias = ly.b2; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.resid = x1; e.ld_resid = D;
+        e.ln_g = ly.ln2_g; e.ln_b = ly.ln2_b; e.ln_eps = 1e-5f;
+        rc = snvrag_linear_ex(dtype, dtype, M, D, 4 * D, h, 4 * D, ly.w2, 4 * D, xc, D, &e, &an, stream);
+        if (rc) return rc;
+        continue;
+      }
       e = snvrag_epilogue_t{};
       e.bias = ly.b_o; e.resid = xc; e.ld_resid = D;
       rc = snvrag_linear(dtype, dtype, M, D, D, att, D, ly.w_o, D, x1, D, &e, stream);

@@ -206,6 +206,9 @@ static int launch_linear(long M, long N, long K, const void* A, long lda, const 
   return 0;
 }
 
+int rows_linear(int din, int dout, long M, long N, long K, const void* A, long lda, const void* W, long ldw,
+                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm, hipStream_t s);
+
 }  // namespace snvrag
 
 using namespace snvrag;
@@ -213,6 +216,13 @@ using namespace snvrag;
 extern "C" int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                              const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
                              int64_t ldc, const snvrag_epilogue_t* epi, void* stream) {
+  return snvrag_linear_ex(dtype_in, dtype_out, M, N, K, A, lda, W, ldw, C, ldc, epi, nullptr, stream);
+}
+
+extern "C" int snvrag_linear_ex(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
+                                const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
+                                int64_t ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm,
+                                void* stream) {
   SNV_CHECK_ARG(M >= 0 && N > 0 && K > 0, "bad shape");
   SNV_CHECK_ARG(A && W && C, "null pointer");
   SNV_CHECK_ARG(dtype_in == SNVRAG_F32 || dtype_in == SNVRAG_BF16, "dtype_in");
@@ -224,6 +234,17 @@ extern "C" int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, 
   SNV_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0 && ((uintptr_t)C % 16) == 0,
                 "A/W/C must be 16-byte aligned");
   if (M == 0) return 0;
+  const int ept = dtype_in == SNVRAG_BF16 ? 64 : 32;
+  const bool fused = anorm || (epi && (epi->ln_g || epi->stats_out));
+  const bool rows_ok = N % 64 == 0 && K % ept == 0 && !getenv("SNVRAG_GEMM_TILE128");
+  if (fused || rows_ok) {               // row-panel GEMM (checks its own shape constraints)
+    hipStream_t s = as_stream(stream);
+    evlog_begin(s);
+    const int rc = rows_linear(dtype_in, dtype_out, M, N, K, A, lda, W, ldw, C, ldc, epi, anorm, s);
+    if (rc) return rc;
+    evlog_end(s, EV_GEMM, 2.0 * M * N * K);
+    return 0;
+  }
   EpiDev e{};
   if (epi) {
     e.bias = epi->bias; e.row1 = epi->row1; e.row1_stride = epi->row1_stride; e.col1 = epi->col1;

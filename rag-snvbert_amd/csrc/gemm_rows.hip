@@ -1,0 +1,388 @@
+// Row-panel GEMM with LayerNorm-fused epilogues (gfx950 MFMA).
+//
+// C[128 x BN] tiles, BN = 64*NW (NW = 6 -> 384 = the model width D, so one tile
+// holds whole output rows), 512 threads = 8 waves in a 2 (M) x 4 (N) grid, each
+// wave 64 x 16*NW = 4 x NW MFMA 16x16 tiles.  Operands are staged with
+// global_load_lds (16 B / lane, 1 KiB = 8 rows per wave instruction) into two
+// LDS stages; the st_16x32-style XOR swizzle of the fragment reads is applied on
+// the SOURCE address (the LDS image of a glds is lane-linear) — guide §5 rule 21.
+//
+// Epilogue options (all fused, no extra HBM pass):
+//   bias, two rank-1 row*col terms (the reference's cat([x, af, af_p]) columns),
+//   activation, residual add, then
+//   * LN over the full output row (requires N == BN): sublayer.py:15-16 post-LN,
+//     EmbeddingFusionModule / rag fusion / hap head norms, + act + (base + s*y*maf(af))
+//   * or row statistics (sum, sumsq) of this tile's columns -> stats[tile_n][M]
+//     (FeedForward's LayerNorm(4D), consumed by the next GEMM's A operand)
+// A-operand option: LayerNorm applied on the fly from such statistics
+// (feed_forward.py:20: w_2(norm(x)) without materialising norm(x)).
+#include "common.h"
+
+namespace snvrag {
+
+constexpr int R_BM = 128, R_ROWB = 128;
+
+struct EpiX {
+  const float* bias;
+  const float* row1; long row1_stride; const float* col1;
+  const float* row2; long row2_stride; const float* col2;
+  long row_period;
+  int act; float slope;
+  const void* resid; long ld_resid;
+  const float* ln_g; const float* ln_b; float ln_eps; int ln_act;
+  const void* post_base; long ld_post; float post_scale; const float* post_af; long post_af_period; int post_maf;
+  float* stats_out;
+};
+
+struct ANorm {
+  const float* stats; int n_parts; int dim; const float* g; const float* b; float eps;
+};
+
+__device__ __forceinline__ int rswz(int row, int chunk) { return row * R_ROWB + ((chunk ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ float maf_w(float af) {
+  const float maf = fminf(af, 1.0f - af);
+  return fminf(log1pf(1.0f / (maf + 1e-6f)), 3.0f);
+}
+
+template <typename TI, typename TO, int NW, bool ANORM>
+__global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, const TI* __restrict__ A, long lda,
+                                                        const TI* __restrict__ W, long ldw, TO* __restrict__ C,
+                                                        long ldc, EpiX epi, ANorm an, int n_tiles_n) {
+  constexpr int BN = 64 * NW;
+  constexpr int EPC = 16 / sizeof(TI);             // elements per 16-B chunk
+  constexpr int EPT = R_ROWB / sizeof(TI);         // K elements per K-tile
+  constexpr int STAGE = (R_BM + BN) * R_ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* rowstat = reinterpret_cast<float2*>(smem + 2 * STAGE);   // ANORM: (mean, rstd) per tile row
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tm = wg / n_tiles_n, tn = wg % n_tiles_n;
+  const int m0 = tm * R_BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int wmi = wave >> 2, wni = wave & 3;
+  const int wm = 64 * wmi, wn = 16 * NW * wni;
+  const int mrows = min(R_BM, M - m0), nrows = min(BN, N - n0);
+  const TI* Ab = A + (long)m0 * lda;
+  const TI* Wb = W + (long)n0 * ldw;
+  const int nk = K / EPT;
+
+  if constexpr (ANORM) {
+    if (tid < R_BM) {
+      float s = 0.f, ss = 0.f;
+      const int m = min(m0 + tid, M - 1);
+      for (int p = 0; p < an.n_parts; ++p) {
+        const float2 st = reinterpret_cast<const float2*>(an.stats)[(long)p * M + m];
+        s += st.x; ss += st.y;
+      }
+      const float mean = s / an.dim;
+      const float var = fmaxf(ss / an.dim - mean * mean, 0.f);
+      rowstat[tid] = make_float2(mean, 1.0f / sqrtf(var + an.eps));
+    }
+    __syncthreads();
+  }
+
+  // ---- staging ----
+  auto issue_w = [&](int stage, int k0) {
+    char* Wt = smem + stage * STAGE + R_BM * R_ROWB;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int r0 = wave * 8 * NW + j * 8;
+      const int r = r0 + (lane >> 3), c = (lane & 7) ^ (r & 7);
+      const int rs = r < nrows ? r : nrows - 1;
+      glds16(Wb + (long)rs * ldw + k0 + c * EPC, Wt + r0 * R_ROWB);
+    }
+  };
+  auto issue_a = [&](int stage, int k0) {
+    char* At = smem + stage * STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r0 = wave * 16 + j * 8;
+      const int r = r0 + (lane >> 3), c = (lane & 7) ^ (r & 7);
+      const int rs = r < mrows ? r : mrows - 1;
+      glds16(Ab + (long)rs * lda + k0 + c * EPC, At + r0 * R_ROWB);
+    }
+  };
+  // ANORM: A chunks through registers (2 per thread), normalised before the LDS write
+  u32x4 ar[2];
+  auto load_a_regs = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 512 * i, r = id >> 3, c = id & 7;
+      ar[i] = r < mrows ? *reinterpret_cast<const u32x4*>(Ab + (long)r * lda + k0 + c * EPC) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_a_norm = [&](int stage, int k0) {
+    char* At = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 512 * i, r = id >> 3, c = id & 7;
+      const float2 st = rowstat[r];
+      const int kb = k0 + c * EPC;
+      TI* e = reinterpret_cast<TI*>(&ar[i]);
+      TI o[EPC];
+#pragma unroll
+      for (int j = 0; j < EPC; ++j)
+        o[j] = from_f32<TI>((to_f32(e[j]) - st.x) * st.y * an.g[kb + j] + an.b[kb + j]);
+      *reinterpret_cast<u32x4*>(At + rswz(r, c)) = *reinterpret_cast<u32x4*>(o);
+    }
+  };
+
+  f32x4 acc[4][NW];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue
+  if constexpr (ANORM) {
+    load_a_regs(0);
+    store_a_norm(0, 0);
+  } else {
+    issue_a(0, 0);
+  }
+  issue_w(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      if constexpr (ANORM) load_a_regs((kt + 1) * EPT);
+      else issue_a(cur ^ 1, (kt + 1) * EPT);
+      issue_w(cur ^ 1, (kt + 1) * EPT);
+    }
+    const char* At = smem + cur * STAGE;
+    const char* Wt = At + R_BM * R_ROWB;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      u32x4 a[4], b[NW];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(At + rswz(wm + 16 * t + li, 4 * kc + lg));
+#pragma unroll
+      for (int t = 0; t < NW; ++t) b[t] = *reinterpret_cast<const u32x4*>(Wt + rswz(wn + 16 * t + li, 4 * kc + lg));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) {
+          if constexpr (sizeof(TI) == 2) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, a[mt]), __builtin_bit_cast(bf16x8, b[nt]), acc[mt][nt], 0, 0, 0);
+          } else {
+            const f32x4 av = __builtin_bit_cast(f32x4, a[mt]), bv = __builtin_bit_cast(f32x4, b[nt]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc[mt][nt], 0, 0, 0);
+          }
+        }
+    }
+    if constexpr (ANORM) {
+      if (more) store_a_norm(cur ^ 1, (kt + 1) * EPT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue --
+  // values in acc: row m = m0 + wm + 16 mt + 4 lg + i, col n = n0 + wn + 16 nt + li
+  float* red = reinterpret_cast<float*>(smem);           // [128][4] partial row sums (stage memory reuse)
+  float* red2 = red + R_BM * 4;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm + 16 * mt + 4 * lg + i;
+      const long mr = epi.row_period > 0 ? (m % epi.row_period) : m;
+      const bool mv = m < M;
+      const float r1 = (epi.row1 && mv) ? epi.row1[mr * epi.row1_stride] : 0.f;
+      const float r2 = (epi.row2 && mv) ? epi.row2[mr * epi.row2_stride] : 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) {
+        const int n = n0 + wn + 16 * nt + li;
+        float x = acc[mt][nt][i];
+        if (n < N) {
+          if (epi.bias) x += epi.bias[n];
+          if (epi.row1) x += r1 * epi.col1[n];
+          if (epi.row2) x += r2 * epi.col2[n];
+          x = apply_act(epi.act, x, epi.slope);
+          if (epi.resid && mv) x += to_f32(reinterpret_cast<const TO*>(epi.resid)[(long)m * epi.ld_resid + n]);
+        } else {
+          x = 0.f;
+        }
+        acc[mt][nt][i] = x;
+      }
+    }
+  }
+  const bool do_ln = epi.ln_g != nullptr;
+  if (do_ln || epi.stats_out) {
+    // pass 1: row sums (and sums of squares for stats) over this wave's columns
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float s = 0.f, ss = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) { const float x = acc[mt][nt][i]; s += x; ss += x * x; }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); ss += __shfl_xor(ss, o, 64); }
+        if (li == 0) {
+          const int rl = wm + 16 * mt + 4 * lg + i;
+          red[rl * 4 + wni] = s;
+          red2[rl * 4 + wni] = ss;
+        }
+      }
+    __syncthreads();
+    if (epi.stats_out && !do_ln) {
+      if (tid < R_BM && m0 + tid < M) {
+        const float s = red[tid * 4] + red[tid * 4 + 1] + red[tid * 4 + 2] + red[tid * 4 + 3];
+        const float ss = red2[tid * 4] + red2[tid * 4 + 1] + red2[tid * 4 + 2] + red2[tid * 4 + 3];
+        reinterpret_cast<float2*>(epi.stats_out)[(long)tn * M + m0 + tid] = make_float2(s, ss);
+      }
+    }
+  }
+  if (do_ln) {
+    // two-pass LayerNorm over the BN (= N) columns of each row
+    float mean[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = wm + 16 * mt + 4 * lg + i;
+        mean[mt][i] = (red[rl * 4] + red[rl * 4 + 1] + red[rl * 4 + 2] + red[rl * 4 + 3]) / (float)N;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float q = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) { const float d = acc[mt][nt][i] - mean[mt][i]; q += d * d; }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+        if (li == 0) red[(wm + 16 * mt + 4 * lg + i) * 4 + wni] = q;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = wm + 16 * mt + 4 * lg + i;
+        const int m = m0 + rl;
+        const float var = (red[rl * 4] + red[rl * 4 + 1] + red[rl * 4 + 2] + red[rl * 4 + 3]) / (float)N;
+        const float rstd = 1.0f / sqrtf(var + epi.ln_eps);
+        float w = 1.0f;
+        if (epi.post_maf && m < M) {
+          const long ar = epi.post_af_period > 0 ? m % epi.post_af_period : m;
+          w = maf_w(epi.post_af[ar]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) {
+          const int n = n0 + wn + 16 * nt + li;
+          float y = (acc[mt][nt][i] - mean[mt][i]) * rstd * epi.ln_g[n] + epi.ln_b[n];
+          y = apply_act(epi.ln_act, y, 0.f);
+          if (epi.post_base && m < M)
+            y = to_f32(reinterpret_cast<const TO*>(epi.post_base)[(long)m * epi.ld_post + n]) + epi.post_scale * (y * w);
+          acc[mt][nt][i] = y;
+        }
+      }
+  }
+  // store
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm + 16 * mt + 4 * lg + i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) {
+        const int n = n0 + wn + 16 * nt + li;
+        if (n < N) C[(long)m * ldc + n] = from_f32<TO>(acc[mt][nt][i]);
+      }
+    }
+}
+
+template <typename TI, typename TO, int NW>
+static int launch_rows(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
+                       const EpiX& e, const ANorm* an, hipStream_t s) {
+  constexpr int BN = 64 * NW;
+  const int tn = cdiv(N, BN), tm = cdiv(M, R_BM);
+  const long nb = (long)tn * tm;
+  SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
+  const size_t lds = 2 * (size_t)(R_BM + BN) * R_ROWB + R_BM * sizeof(float2);
+  ANorm a = an ? *an : ANorm{};
+  if (an) {
+    auto kern = rows_gemm_kernel<TI, TO, NW, true>;
+    SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
+                       (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
+  } else {
+    auto kern = rows_gemm_kernel<TI, TO, NW, false>;
+    SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
+                       (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
+  }
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename TI, typename TO>
+static int dispatch_nw(int nw, long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C,
+                       long ldc, const EpiX& e, const ANorm* an, hipStream_t s) {
+  switch (nw) {
+    case 1: return launch_rows<TI, TO, 1>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
+    case 2: return launch_rows<TI, TO, 2>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
+    case 4: return launch_rows<TI, TO, 4>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
+    default: return launch_rows<TI, TO, 6>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
+  }
+}
+
+// tile width for an N: prefer 384 (6), then 256, 128, 64; 0 = unsupported
+int rows_pick_nw(long N, bool need_full_row) {
+  const int cands[4] = {6, 4, 2, 1};
+  for (int c : cands) {
+    const long bn = 64L * c;
+    if (need_full_row ? (N == bn) : (N % bn == 0)) return c;
+  }
+  return 0;
+}
+
+int rows_linear(int din, int dout, long M, long N, long K, const void* A, long lda, const void* W, long ldw,
+                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm, hipStream_t s) {
+  const bool full = epi && epi->ln_g;
+  const int nw = rows_pick_nw(N, full);
+  SNV_CHECK_ARG(nw > 0, full ? "LayerNorm epilogue needs N in {64,128,256,384}" : "N must be a multiple of 64");
+  const int ept = din == SNVRAG_BF16 ? 64 : 32;
+  SNV_CHECK_ARG(K % ept == 0, "row-panel GEMM needs K % 64 (bf16) / 32 (f32) == 0");
+  EpiX e{};
+  if (epi) {
+    e.bias = epi->bias; e.row1 = epi->row1; e.row1_stride = epi->row1_stride; e.col1 = epi->col1;
+    e.row2 = epi->row2; e.row2_stride = epi->row2_stride; e.col2 = epi->col2; e.row_period = epi->row_period;
+    e.act = epi->act; e.slope = epi->slope; e.resid = epi->resid; e.ld_resid = epi->ld_resid;
+    e.ln_g = epi->ln_g; e.ln_b = epi->ln_b; e.ln_eps = epi->ln_eps; e.ln_act = epi->ln_act;
+    e.post_base = epi->post_base; e.ld_post = epi->ld_post; e.post_scale = epi->post_scale;
+    e.post_af = epi->post_af; e.post_af_period = epi->post_af_period; e.post_maf = epi->post_maf;
+    e.stats_out = epi->stats_out;
+  }
+  ANorm an{};
+  if (anorm) {
+    an.stats = anorm->stats; an.n_parts = anorm->n_parts; an.dim = (int)anorm->dim; an.g = anorm->g;
+    an.b = anorm->b; an.eps = anorm->eps;
+  }
+  const ANorm* ap = anorm ? &an : nullptr;
+  if (din == SNVRAG_BF16 && dout == SNVRAG_BF16) return dispatch_nw<bf16, bf16>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
+  if (din == SNVRAG_BF16) return dispatch_nw<bf16, float>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
+  if (dout == SNVRAG_F32) return dispatch_nw<float, float>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
+  return dispatch_nw<float, bf16>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
+}
+
+}  // namespace snvrag

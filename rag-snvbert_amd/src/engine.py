@@ -185,8 +185,7 @@ class Engine:
         af = af.float().contiguous()
         T = self.dtype
         feat = K.af_features(af, a["freqs"], T)
-        h = K.linear(feat, a["w0"], a["b0"])
-        h = K.layernorm(h, a["g"], a["bb"], act=N.ACT_GELU, out=h)
+        h = K.linear(feat, a["w0"], a["b0"], ln=(a["g"], a["bb"]), ln_act=N.ACT_GELU)
         return K.linear(h, a["w3"], a["b3"])
 
     def embed(self, seq: torch.Tensor, af: Optional[torch.Tensor] = None, pos: bool = False,
@@ -237,8 +236,7 @@ class Engine:
         pf = K.posfeat(pos, P.pf)                                     # [B, L]
         ef = P.ef
         fused = K.linear(hm, ef["w"], ef["b"], row1=(pf, 1, ef["c_pos"]), row2=(af, 1, ef["c_af"]),
-                         row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm)
-        K.layernorm(fused, ef["g"], ef["bb"], out=fused)
+                         row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm, ln=(ef["g"], ef["bb"]))
         if rag is not None:
             rf = P.rf
             fa = K.af_gate(af, af_p, P.ag, D, T)                      # [B, L, D]
@@ -246,9 +244,8 @@ class Engine:
             aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
             cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
             h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
-            h = K.linear(h, rf["f3"], rf["f3b"])
-            xx = K.layernorm(h, rf["g"], rf["bb"], post_base=fused[:2 * B], post_scale=rf["rs"],
-                             post_af=af, af_period=BL, maf_weight=True)
+            xx = K.linear(h, rf["f3"], rf["f3b"], ln=(rf["g"], rf["bb"]), post_base=fused[:2 * B],
+                          post_scale=rf["rs"], post_af=af, post_af_period=BL, post_maf=True)
         else:
             xx = fused[:2 * B].clone()
         ws_bytes = K.encoder_ws_bytes(T, 2 * B, L, D, P.heads)
@@ -266,8 +263,7 @@ class Engine:
         hh = P.hh
         h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
                      row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
-        h = K.linear(h, hh["w2"], hh["b2"])
-        K.layernorm(h, hh["g"], hh["bb"], out=h)
+        h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
         h = K.linear(h, hh["n0"], hh["n0b"], act=N.ACT_GELU)
         logits, probs = K.hap_head_out(h, hh["n2"], hh["n2b"], want_logits=want_logits)
         dev = probs.device

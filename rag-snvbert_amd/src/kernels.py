@@ -29,8 +29,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            row1: Optional[Tuple[torch.Tensor, int, torch.Tensor]] = None,
            row2: Optional[Tuple[torch.Tensor, int, torch.Tensor]] = None,
            row_period: int = 0, resid: Optional[torch.Tensor] = None,
+           ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, ln_act: int = N.ACT_NONE, ln_eps: float = 1e-5,
+           post_base: Optional[torch.Tensor] = None, post_scale: float = 1.0,
+           post_af: Optional[torch.Tensor] = None, post_af_period: int = 0, post_maf: bool = False,
+           stats_out: Optional[torch.Tensor] = None,
+           anorm: Optional[Tuple[torch.Tensor, int, int, torch.Tensor, torch.Tensor]] = None,
            out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    """out[m, n] = act(x[m] . w[n] + bias[n] + row1[m]*col1[n] + row2[m]*col2[n]) + resid[m, n]."""
+    """out[m, n] = act(x[m] . w[n] + bias[n] + row1[m]*col1[n] + row2[m]*col2[n]) + resid[m, n],
+    optionally followed by a fused LayerNorm over the row (``ln=(g, b)``, + ``ln_act`` and the
+    ``post_base + post_scale * y * maf(post_af)`` tail), or writing row statistics
+    (``stats_out`` float32 [n_tiles, M, 2]); ``anorm=(stats, n_parts, dim, g, b)`` applies a
+    LayerNorm to ``x`` while it is staged."""
     N.require_gpu(x, w)
     K = x.shape[-1]
     M = x.numel() // K
@@ -49,9 +58,30 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if resid is not None:
         assert resid.dtype == od and resid.shape[-1] == Nn
         e.resid, e.ld_resid = ptr(_c(resid)), Nn
-    check(N.lib().snvrag_linear(_dt(x.dtype), _dt(od), M, Nn, K, ptr(_c(x)), K, ptr(_c(w)), K,
-                                ptr(out), Nn, C.byref(e), stream_ptr()), "linear")
+    if ln is not None:
+        e.ln_g, e.ln_b, e.ln_eps, e.ln_act = ptr(ln[0]), ptr(ln[1]), ln_eps, ln_act
+    if post_base is not None:
+        assert post_base.dtype == od
+        e.post_base, e.ld_post, e.post_scale = ptr(_c(post_base)), Nn, post_scale
+    if post_af is not None:
+        e.post_af, e.post_af_period, e.post_maf = ptr(_c(post_af)), post_af_period, int(post_maf)
+    e.stats_out = ptr(stats_out)
+    an = None
+    if anorm is not None:
+        st, parts, dim, g, b = anorm
+        an = N.ANormS(ptr(st), parts, dim, ptr(g), ptr(b), 1e-5)
+    check(N.lib().snvrag_linear_ex(_dt(x.dtype), _dt(od), M, Nn, K, ptr(_c(x)), K, ptr(_c(w)), K,
+                                   ptr(out), Nn, C.byref(e), C.byref(an) if an is not None else None,
+                                   stream_ptr()), "linear")
     return out
+
+
+def stat_tiles(n: int) -> int:
+    """Column tiles of the row-panel GEMM for an N (the stats_out leading dim)."""
+    for bn in (384, 256, 128, 64):
+        if n % bn == 0:
+            return n // bn
+    raise ValueError("N must be a multiple of 64")
 
 
 def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, *, resid: Optional[torch.Tensor] = None,

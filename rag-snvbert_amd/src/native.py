@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -30,7 +30,15 @@ vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 class Epilogue(C.Structure):
     _fields_ = [("bias", vp), ("row1", vp), ("row1_stride", i64), ("col1", vp),
                 ("row2", vp), ("row2_stride", i64), ("col2", vp), ("row_period", i64),
-                ("act", C.c_int), ("slope", f32), ("resid", vp), ("ld_resid", i64)]
+                ("act", C.c_int), ("slope", f32), ("resid", vp), ("ld_resid", i64),
+                ("ln_g", vp), ("ln_b", vp), ("ln_eps", f32), ("ln_act", C.c_int),
+                ("post_base", vp), ("ld_post", i64), ("post_scale", f32),
+                ("post_af", vp), ("post_af_period", i64), ("post_maf", C.c_int),
+                ("stats_out", vp)]
+
+
+class ANormS(C.Structure):
+    _fields_ = [("stats", vp), ("n_parts", C.c_int), ("dim", i64), ("g", vp), ("b", vp), ("eps", f32)]
 
 
 class LnPost(C.Structure):
@@ -64,6 +72,8 @@ _SIGS = {
     "snvrag_last_error": ([], C.c_char_p),
     "snvrag_device_info": ([C.c_int, C.c_char_p, C.c_int], C.c_int),
     "snvrag_linear": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), vp], C.c_int),
+    "snvrag_linear_ex": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue),
+                          C.POINTER(ANormS), vp], C.c_int),
     "snvrag_layernorm": ([C.c_int, C.c_int, i64, i64, vp, i64, vp, i64, vp, vp, f32, vp, i64,
                           C.POINTER(LnPost), vp], C.c_int),
     "snvrag_attention": ([C.c_int, i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, f32, vp], C.c_int),

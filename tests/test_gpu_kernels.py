@@ -226,3 +226,70 @@ def test_rag_mean_vs_oracle():
         v = idx[q][idx[q] >= 0]
         ref[q] = (W[toks[v]] + pe[None] + Ar[None]).mean(0)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------- fused row-panel GEMM epilogues --
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [384, 128, 64])
+def test_linear_fused_layernorm_and_tail(dt, n):
+    g = torch.Generator(device="cpu").manual_seed(n)
+    M, Kk = 1000, 384
+    x = torch.randn(M, Kk, generator=g).to(DEV, dt)
+    w = (torch.randn(n, Kk, generator=g) / math.sqrt(Kk)).to(DEV, dt)
+    b, gm, bt = (torch.randn(n, generator=g).to(DEV) for _ in range(3))
+    resid = torch.randn(M, n, generator=g).to(DEV, dt)
+    base = torch.randn(M, n, generator=g).to(DEV, dt)
+    af = torch.rand(M // 2, generator=g).to(DEV)
+    out = K().linear(x, w, b, act=2, slope=0.1, resid=resid, ln=(gm, bt), ln_act=1, post_base=base,
+                     post_scale=0.3, post_af=af, post_af_period=M // 2, post_maf=True)
+    v = _ref_linear(x.float(), w.float(), b, 2, 0.1, resid=resid.float())
+    y = torch.nn.functional.gelu(torch.nn.functional.layer_norm(v, (n,), gm.double(), bt.double(), 1e-5))
+    a = af[torch.arange(M, device=DEV) % (M // 2)].double()
+    mw = torch.log1p(1.0 / (torch.minimum(a, 1 - a) + 1e-6)).clamp(max=3.0)
+    ref = base.double() + 0.3 * y * mw[:, None]
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_linear_stats_then_anorm_matches_ffn(dt):
+    """h = lrelu(x W1 + b1) with row stats -> out = lrelu(LN(h) W2 + b2): FeedForward of feed_forward.py."""
+    g = torch.Generator(device="cpu").manual_seed(1)
+    M, D = 777, 384
+    x = torch.randn(M, D, generator=g).to(DEV, dt)
+    w1 = (torch.randn(4 * D, D, generator=g) / math.sqrt(D)).to(DEV, dt)
+    w2 = (torch.randn(D, 4 * D, generator=g) / math.sqrt(4 * D)).to(DEV, dt)
+    b1, b2 = torch.randn(4 * D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    gf, bf = torch.randn(4 * D, generator=g).to(DEV), torch.randn(4 * D, generator=g).to(DEV)
+    parts = K().stat_tiles(4 * D)
+    stats = torch.empty(parts, M, 2, device=DEV)
+    h = K().linear(x, w1, b1, act=2, slope=0.1, stats_out=stats)
+    hr = h.double()
+    torch.testing.assert_close(stats.sum(0)[:, 0].double(), hr.sum(1), rtol=1e-4, atol=1e-2)
+    out = K().linear(h, w2, b2, act=2, slope=0.1, anorm=(stats, parts, 4 * D, gf, bf))
+    hn = torch.nn.functional.layer_norm(hr, (4 * D,), gf.double(), bf.double(), 1e-5)
+    ref = torch.nn.functional.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
+    tol = 1e-4 if dt == torch.float32 else 5e-2
+    torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_encoder_fused_equals_unfused(dt, monkeypatch):
+    """Encoder stack with LN fused into GEMM epilogues/prologues == the 8-launch unfused stack."""
+    import os
+    from src.model import build_model
+    from src.engine import engine_for
+    torch.manual_seed(0)
+    m = build_model(12, 384, 2, 12).to(DEV).eval()
+    eng = engine_for(m)
+    eng.set_dtype(dt)
+    P = eng.packed()
+    x0 = torch.randn(3, 1030, 384, device=DEV).to(dt)
+    ws = torch.empty(K().encoder_ws_bytes(dt, 3, 1030, 384, 12), device=DEV, dtype=torch.uint8)
+    a = x0.clone()
+    K().encoder_forward(a, P.layers, 12, ws)
+    monkeypatch.setenv("SNVRAG_UNFUSED_LN", "1")
+    b = x0.clone()
+    K().encoder_forward(b, P.layers, 12, ws)
+    tol = 2e-4 if dt == torch.float32 else 6e-2
+    torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
