@@ -188,8 +188,8 @@ def main():
                              frac=round(scan["rate"] / 1e9 / HBM_PEAK_GBS, 4), avg_launch_ms=round(scan["avg_ms"], 4),
                              bytes_per_launch=scan["work_per_launch"]),
             "gemm": dict(ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
-            "layernorm": dict(ms_per_step=round(ln["total_ms_per_step"], 3),
-                              achieved_gbs=round(ln["rate"] / 1e9, 1)),
+            "layernorm": (dict(ms_per_step=round(ln["total_ms_per_step"], 3), achieved_gbs=round(ln["rate"] / 1e9, 1))
+                          if ln else "fused into GEMM epilogues/prologues"),
         },
         "knn_queries_per_s": round(knn_qps, 1),
         "masked_snvs_per_step_per_gpu": masked_per_step,

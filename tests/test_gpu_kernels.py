@@ -265,7 +265,9 @@ def test_linear_stats_then_anorm_matches_ffn(dt):
     stats = torch.empty(parts, M, 2, device=DEV)
     h = K().linear(x, w1, b1, act=2, slope=0.1, stats_out=stats)
     hr = h.double()
-    torch.testing.assert_close(stats.sum(0)[:, 0].double(), hr.sum(1), rtol=1e-4, atol=1e-2)
+    # stats are taken from the f32 accumulators, before the output is rounded to dt
+    st_tol = 1e-4 if dt == torch.float32 else 2e-3
+    torch.testing.assert_close(stats.sum(0)[:, 0].double(), hr.sum(1), rtol=st_tol, atol=st_tol * 100)
     out = K().linear(h, w2, b2, act=2, slope=0.1, anorm=(stats, parts, 4 * D, gf, bf))
     hn = torch.nn.functional.layer_norm(hr, (4 * D,), gf.double(), bf.double(), 1e-5)
     ref = torch.nn.functional.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
