@@ -22,9 +22,11 @@ static int64_t chunk_seqs(int64_t nseq, int64_t L, int D, int esz) {
     const long v = atol(e);
     if (v > 0) return std::min<int64_t>(v, nseq);
   }
-  // target ~160 MB of per-chunk activations (x + qkv + attn + x1 + h = 10 D / token)
+  // The row-panel GEMMs tile M by 128 rows with whole output rows per tile, so a chunk
+  // must hold >= ~4 tiles per CU (1024 tiles = 131k rows) to fill 256 CUs; cap the
+  // per-chunk workspace (10 D / token) at ~4 GB of the 288 GB HBM.
   const double per_seq = (double)L * D * 10.0 * esz;
-  int64_t c = (int64_t)(160.0e6 / per_seq);
+  int64_t c = (int64_t)(4.0e9 / per_seq);
   if (c < 1) c = 1;
   return std::min<int64_t>(c, nseq);
 }

@@ -296,19 +296,40 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
         }
       }
   }
-  // store
+  // store: bf16 tiles go through LDS (the stages are free) for row-contiguous 16-B stores
+  if constexpr (sizeof(TO) == 2) {
+    constexpr int SLD = BN + 8;                                 // padded row (elements)
+    TO* st = reinterpret_cast<TO*>(smem);
+    __syncthreads();                                            // LN scratch reads done
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm + 16 * mt + 4 * lg + i;
-      if (m >= M) continue;
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int nt = 0; nt < NW; ++nt) {
-        const int n = n0 + wn + 16 * nt + li;
-        if (n < N) C[(long)m * ldc + n] = from_f32<TO>(acc[mt][nt][i]);
-      }
+        for (int nt = 0; nt < NW; ++nt)
+          st[(wm + 16 * mt + 4 * lg + i) * SLD + wn + 16 * nt + li] = from_f32<TO>(acc[mt][nt][i]);
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+    for (int id = tid; id < R_BM * CPR; id += 512) {
+      const int rl = id / CPR, c = (id % CPR) * 8;
+      const int m = m0 + rl, n = n0 + c;
+      if (m < M && n < N)
+        *reinterpret_cast<u32x4*>(C + (long)m * ldc + n) = *reinterpret_cast<const u32x4*>(st + rl * SLD + c);
     }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm + 16 * mt + 4 * lg + i;
+        if (m >= M) continue;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) {
+          const int n = n0 + wn + 16 * nt + li;
+          if (n < N) C[(long)m * ldc + n] = from_f32<TO>(acc[mt][nt][i]);
+        }
+      }
+  }
 }
 
 template <typename TI, typename TO, int NW>
@@ -322,12 +343,14 @@ static int launch_rows(long M, long N, long K, const void* A, long lda, const vo
   ANorm a = an ? *an : ANorm{};
   if (an) {
     auto kern = rows_gemm_kernel<TI, TO, NW, true>;
-    SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    static bool attr = false;
+    if (!attr) { SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); attr = true; }
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
                        (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
   } else {
     auto kern = rows_gemm_kernel<TI, TO, NW, false>;
-    SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    static bool attr = false;
+    if (!attr) { SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); attr = true; }
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
                        (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
   }

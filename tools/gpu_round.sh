@@ -23,6 +23,8 @@ for s in $STEPS; do
     model)   step pytest_model 900 python -m pytest tests/test_gpu_model.py -q -rf --timeout 300 ;;
     gpu)     step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf --timeout 300 ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench)   step bench 900 python bench.py --steps ${BSTEPS:-5} --warmup 2 ;;
+    bench)   step bench 900 python bench.py --steps ${BSTEPS:-5} --warmup 2 ${BENCH_ARGS:-} ;;
+    benchab) step bench_old 900 env SNVRAG_GEMM_TILE128=1 SNVRAG_UNFUSED_LN=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0
+             step bench_tile128_fusedoff 900 env SNVRAG_UNFUSED_LN=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0 ;;
   esac
 done
