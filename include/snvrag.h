@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 2
+#define SNVRAG_ABI_VERSION 3
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -63,11 +63,13 @@ typedef struct {
   float* stats_out;
 } snvrag_epilogue_t;
 
-/* LayerNorm applied to the A operand while staging it (stats from a previous stats_out):
- * A'[m,k] = (A[m,k] - mean_m) * rstd_m * g[k] + b[k], mean/var from sum over n_parts partials / dim */
+/* LayerNorm of the A operand folded into the epilogue (stats from a previous stats_out):
+ * LN(A) W^T = rstd_m * (A W'^T) - rstd_m * mean_m * c1[n] + beta W^T, with the caller passing
+ * W' = W diag(gamma), c1 = W gamma, and beta W^T added into the bias.  mean/var of row m
+ * from the n_parts (sum, sumsq) partials over `dim` columns. */
 typedef struct {
-  const float* stats; int n_parts; int64_t dim; const float* g; const float* b; float eps;
-} snvrag_anorm_t;
+  const float* stats; int n_parts; int64_t dim; float eps; const float* c1;
+} snvrag_rownorm_t;
 
 int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                   const void* A, int64_t lda, const void* W, int64_t ldw,
@@ -75,7 +77,7 @@ int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
 int snvrag_linear_ex(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                      const void* A, int64_t lda, const void* W, int64_t ldw,
                      void* C, int64_t ldc, const snvrag_epilogue_t* epi,
-                     const snvrag_anorm_t* anorm, void* stream);
+                     const snvrag_rownorm_t* rownorm, void* stream);
 
 /* LayerNorm over the last dim, eps as given (torch default 1e-5):
  *   y = LN(x + r) * gamma + beta                  (r optional: residual of sublayer.py:15-16)
@@ -222,6 +224,9 @@ typedef struct {
   const float* lnf_g; const float* lnf_b;  /* feed_forward.norm [4D] */
   const void* w2; const float* b2;         /* [D, 4D], [D] */
   const float* ln2_g; const float* ln2_b;  /* output_sublayer.norm */
+  /* feed_forward.norm folded into w_2 (fused path): w2g = w2 diag(lnf_g),
+   * b2g = b2 + w2 lnf_b, c2g = w2 lnf_g */
+  const void* w2g; const float* b2g; const float* c2g;
 } snvrag_layer_t;
 
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);

@@ -66,7 +66,8 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
   const int dh = D / heads;
   const float scale = 1.0f / sqrtf((float)dh);
 
-  const bool fused = (D == 64 || D == 128 || D == 256 || D == 384) && !getenv("SNVRAG_UNFUSED_LN");
+  const bool fused = (D == 64 || D == 128 || D == 256 || D == 384) && !getenv("SNVRAG_UNFUSED_LN") &&
+                     layers[0].w2g && layers[0].b2g && layers[0].c2g;
   for (int64_t s0 = 0; s0 < nseq; s0 += cs) {
     const int64_t ns = std::min<int64_t>(cs, nseq - s0);
     const int64_t M = ns * L;
@@ -91,12 +92,12 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
         e.bias = ly.b1; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.stats_out = (float*)stats;
         rc = snvrag_linear(dtype, dtype, M, 4 * D, D, x1, D, ly.w1, D, h, 4 * D, &e, stream);
         if (rc) return rc;
-        // x = LN2(x1 + lrelu(LN_f(h) W2^T + b2)); LN_f applied to A while staging (one launch)
-        snvrag_anorm_t an{(const float*)stats, n_stat_parts, 4 * D, ly.lnf_g, ly.lnf_b, 1e-5f};
+        // x = LN2(x1 + lrelu(LN_f(h) W2^T + b2)); LN_f folded into W2 and the epilogue (one launch)
+        snvrag_rownorm_t rn{(const float*)stats, n_stat_parts, 4 * D, 1e-5f, ly.c2g};
         e = snvrag_epilogue_t{};
-        e.bias = ly.b2; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.resid = x1; e.ld_resid = D;
+        e.bias = ly.b2g; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.resid = x1; e.ld_resid = D;
         e.ln_g = ly.ln2_g; e.ln_b = ly.ln2_b; e.ln_eps = 1e-5f;
-        rc = snvrag_linear_ex(dtype, dtype, M, D, 4 * D, h, 4 * D, ly.w2, 4 * D, xc, D, &e, &an, stream);
+        rc = snvrag_linear_ex(dtype, dtype, M, D, 4 * D, h, 4 * D, ly.w2g, 4 * D, xc, D, &e, &rn, stream);
         if (rc) return rc;
         continue;
       }

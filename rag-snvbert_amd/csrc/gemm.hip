@@ -207,7 +207,7 @@ static int launch_linear(long M, long N, long K, const void* A, long lda, const 
 }
 
 int rows_linear(int din, int dout, long M, long N, long K, const void* A, long lda, const void* W, long ldw,
-                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm, hipStream_t s);
+                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_rownorm_t* anorm, hipStream_t s);
 
 }  // namespace snvrag
 
@@ -221,7 +221,7 @@ extern "C" int snvrag_linear(int dtype_in, int dtype_out, int64_t M, int64_t N, 
 
 extern "C" int snvrag_linear_ex(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                                 const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
-                                int64_t ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm,
+                                int64_t ldc, const snvrag_epilogue_t* epi, const snvrag_rownorm_t* anorm,
                                 void* stream) {
   SNV_CHECK_ARG(M >= 0 && N > 0 && K > 0, "bad shape");
   SNV_CHECK_ARG(A && W && C, "null pointer");

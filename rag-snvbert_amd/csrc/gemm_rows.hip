@@ -3,9 +3,12 @@
 // C[128 x BN] tiles, BN = 64*NW (NW = 6 -> 384 = the model width D, so one tile
 // holds whole output rows), 512 threads = 8 waves in a 2 (M) x 4 (N) grid, each
 // wave 64 x 16*NW = 4 x NW MFMA 16x16 tiles.  Operands are staged with
-// global_load_lds (16 B / lane, 1 KiB = 8 rows per wave instruction) into two
-// LDS stages; the st_16x32-style XOR swizzle of the fragment reads is applied on
-// the SOURCE address (the LDS image of a glds is lane-linear) — guide §5 rule 21.
+// global_load_lds (16 B / lane, 1 KiB per wave instruction) into a 4-stage LDS
+// ring of 64-B K-tile rows with three K-tiles in flight across raw s_barriers
+// (counted s_waitcnt vmcnt(N); guide §5 'Pipelining across barriers'); narrow
+// tiles use a 2-stage ring of 128-B rows.  The XOR swizzle of the ds_read_b128
+// fragment reads is applied on the SOURCE address (the LDS image of a glds is
+// lane-linear) — guide §5 rule 21.
 //
 // Epilogue options (all fused, no extra HBM pass):
 //   bias, two rank-1 row*col terms (the reference's cat([x, af, af_p]) columns),
@@ -14,13 +17,15 @@
 //     EmbeddingFusionModule / rag fusion / hap head norms, + act + (base + s*y*maf(af))
 //   * or row statistics (sum, sumsq) of this tile's columns -> stats[tile_n][M]
 //     (FeedForward's LayerNorm(4D), consumed by the next GEMM's A operand)
-// A-operand option: LayerNorm applied on the fly from such statistics
-// (feed_forward.py:20: w_2(norm(x)) without materialising norm(x)).
+// Row-norm option: a LayerNorm of the A operand folded algebraically into the
+// epilogue, acc' = rstd_m * (A W'^T) - rstd_m * mean_m * c1 with W' = W diag(gamma),
+// c1 = W gamma and beta folded into the bias (feed_forward.py:20, w_2(norm(x)),
+// without ever materialising norm(x)); mean/rstd from the producer's row stats.
 #include "common.h"
 
 namespace snvrag {
 
-constexpr int R_BM = 128, R_ROWB = 128;
+constexpr int R_BM = 128;
 
 struct EpiX {
   const float* bias;
@@ -34,32 +39,50 @@ struct EpiX {
   float* stats_out;
 };
 
-struct ANorm {
-  const float* stats; int n_parts; int dim; const float* g; const float* b; float eps;
+// LayerNorm of the A operand folded into the epilogue (see snvrag_rownorm_t):
+//   acc' = rstd_m * acc - rstd_m * mean_m * c1[n]
+struct RowNorm {
+  const float* stats; int n_parts; int dim; float eps; const float* c1;
 };
 
-__device__ __forceinline__ int rswz(int row, int chunk) { return row * R_ROWB + ((chunk ^ (row & 7)) << 4); }
+template <int ROWB>
+__device__ __forceinline__ int rswz(int row, int chunk) {
+  if constexpr (ROWB == 128) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
 __device__ __forceinline__ float maf_w(float af) {
   const float maf = fminf(af, 1.0f - af);
   return fminf(log1pf(1.0f / (maf + 1e-6f)), 3.0f);
 }
 
-template <typename TI, typename TO, int NW, bool ANORM>
+// DEEP: 64-B K-tile rows, 4 LDS stages, 3 tiles in flight (counted vmcnt, raw barriers)
+// else: 128-B K-tile rows, 2 stages, vmcnt(0) + barrier per tile.
+template <typename TI, typename TO, int NW, bool DEEP, bool ROWNORM>
 __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, const TI* __restrict__ A, long lda,
                                                         const TI* __restrict__ W, long ldw, TO* __restrict__ C,
-                                                        long ldc, EpiX epi, ANorm an, int n_tiles_n) {
+                                                        long ldc, EpiX epi, RowNorm rn, int n_tiles_n) {
   constexpr int BN = 64 * NW;
-  constexpr int EPC = 16 / sizeof(TI);             // elements per 16-B chunk
-  constexpr int EPT = R_ROWB / sizeof(TI);         // K elements per K-tile
-  constexpr int STAGE = (R_BM + BN) * R_ROWB;
+  constexpr int ROWB = DEEP ? 64 : 128;
+  constexpr int NST = DEEP ? 4 : 2;
+  constexpr int CPR = ROWB / 16;                   // 16-B chunks per tile row
+  constexpr int RPI = 1024 / ROWB;                 // rows per 1-KiB glds wave instruction
+  constexpr int EPC = 16 / sizeof(TI);
+  constexpr int EPT = ROWB / sizeof(TI);           // K elements per K-tile
+  constexpr int STAGE = (R_BM + BN) * ROWB;
+  constexpr int A_INSTR = R_BM / RPI / 8;          // per wave (8 waves)
+  constexpr int W_INSTR = BN / RPI / 8;
+  constexpr int P = A_INSTR + W_INSTR;             // glds per wave per K-tile
+  static_assert(BN % (RPI * 8) == 0 && R_BM % (RPI * 8) == 0, "tile rows must split over 8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float2* rowstat = reinterpret_cast<float2*>(smem + 2 * STAGE);   // ANORM: (mean, rstd) per tile row
+  float2* rowstat = reinterpret_cast<float2*>(smem + NST * STAGE);
 
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
@@ -75,64 +98,37 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   const TI* Wb = W + (long)n0 * ldw;
   const int nk = K / EPT;
 
-  if constexpr (ANORM) {
+  if constexpr (ROWNORM) {
     if (tid < R_BM) {
       float s = 0.f, ss = 0.f;
       const int m = min(m0 + tid, M - 1);
-      for (int p = 0; p < an.n_parts; ++p) {
-        const float2 st = reinterpret_cast<const float2*>(an.stats)[(long)p * M + m];
+      for (int p = 0; p < rn.n_parts; ++p) {
+        const float2 st = reinterpret_cast<const float2*>(rn.stats)[(long)p * M + m];
         s += st.x; ss += st.y;
       }
-      const float mean = s / an.dim;
-      const float var = fmaxf(ss / an.dim - mean * mean, 0.f);
-      rowstat[tid] = make_float2(mean, 1.0f / sqrtf(var + an.eps));
+      const float mean = s / rn.dim;
+      const float var = fmaxf(ss / rn.dim - mean * mean, 0.f);
+      const float rstd = 1.0f / sqrtf(var + rn.eps);
+      rowstat[tid] = make_float2(rstd, -rstd * mean);
     }
-    __syncthreads();
   }
 
-  // ---- staging ----
-  auto issue_w = [&](int stage, int k0) {
-    char* Wt = smem + stage * STAGE + R_BM * R_ROWB;
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int r0 = wave * 8 * NW + j * 8;
-      const int r = r0 + (lane >> 3), c = (lane & 7) ^ (r & 7);
-      const int rs = r < nrows ? r : nrows - 1;
-      glds16(Wb + (long)rs * ldw + k0 + c * EPC, Wt + r0 * R_ROWB);
-    }
-  };
-  auto issue_a = [&](int stage, int k0) {
+  auto issue = [&](int stage, int k0) {
     char* At = smem + stage * STAGE;
+    char* Wt = At + R_BM * ROWB;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r0 = wave * 16 + j * 8;
-      const int r = r0 + (lane >> 3), c = (lane & 7) ^ (r & 7);
+    for (int j = 0; j < A_INSTR; ++j) {
+      const int r0 = (wave * A_INSTR + j) * RPI;
+      const int r = r0 + lane / CPR, c = (lane % CPR) ^ (ROWB == 128 ? ((r >> 1) & 7) : ((r >> 2) & 3));
       const int rs = r < mrows ? r : mrows - 1;
-      glds16(Ab + (long)rs * lda + k0 + c * EPC, At + r0 * R_ROWB);
+      glds16(Ab + (long)rs * lda + k0 + c * EPC, At + r0 * ROWB);
     }
-  };
-  // ANORM: A chunks through registers (2 per thread), normalised before the LDS write
-  u32x4 ar[2];
-  auto load_a_regs = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 512 * i, r = id >> 3, c = id & 7;
-      ar[i] = r < mrows ? *reinterpret_cast<const u32x4*>(Ab + (long)r * lda + k0 + c * EPC) : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto store_a_norm = [&](int stage, int k0) {
-    char* At = smem + stage * STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int id = tid + 512 * i, r = id >> 3, c = id & 7;
-      const float2 st = rowstat[r];
-      const int kb = k0 + c * EPC;
-      TI* e = reinterpret_cast<TI*>(&ar[i]);
-      TI o[EPC];
-#pragma unroll
-      for (int j = 0; j < EPC; ++j)
-        o[j] = from_f32<TI>((to_f32(e[j]) - st.x) * st.y * an.g[kb + j] + an.b[kb + j]);
-      *reinterpret_cast<u32x4*>(At + rswz(r, c)) = *reinterpret_cast<u32x4*>(o);
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int r0 = (wave * W_INSTR + j) * RPI;
+      const int r = r0 + lane / CPR, c = (lane % CPR) ^ (ROWB == 128 ? ((r >> 1) & 7) : ((r >> 2) & 3));
+      const int rs = r < nrows ? r : nrows - 1;
+      glds16(Wb + (long)rs * ldw + k0 + c * EPC, Wt + r0 * ROWB);
     }
   };
 
@@ -142,34 +138,16 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
 #pragma unroll
     for (int j = 0; j < NW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue
-  if constexpr (ANORM) {
-    load_a_regs(0);
-    store_a_norm(0, 0);
-  } else {
-    issue_a(0, 0);
-  }
-  issue_w(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      if constexpr (ANORM) load_a_regs((kt + 1) * EPT);
-      else issue_a(cur ^ 1, (kt + 1) * EPT);
-      issue_w(cur ^ 1, (kt + 1) * EPT);
-    }
-    const char* At = smem + cur * STAGE;
-    const char* Wt = At + R_BM * R_ROWB;
+  auto compute = [&](int stage) {
+    const char* At = smem + stage * STAGE;
+    const char* Wt = At + R_BM * ROWB;
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
+    for (int kc = 0; kc < CPR / 4; ++kc) {
       u32x4 a[4], b[NW];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(At + rswz(wm + 16 * t + li, 4 * kc + lg));
+      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(At + rswz<ROWB>(wm + 16 * t + li, 4 * kc + lg));
 #pragma unroll
-      for (int t = 0; t < NW; ++t) b[t] = *reinterpret_cast<const u32x4*>(Wt + rswz(wn + 16 * t + li, 4 * kc + lg));
+      for (int t = 0; t < NW; ++t) b[t] = *reinterpret_cast<const u32x4*>(Wt + rswz<ROWB>(wn + 16 * t + li, 4 * kc + lg));
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -185,11 +163,34 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
           }
         }
     }
-    if constexpr (ANORM) {
-      if (more) store_a_norm(cur ^ 1, (kt + 1) * EPT);
+  };
+
+  if constexpr (DEEP) {
+    // prologue: tiles 0..2 in flight
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (t < nk) issue(t, t * EPT);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = min(NST - 2, nk - 1 - kt);     // tiles allowed to stay in flight
+      if (ahead >= 2) vm_wait<2 * P>();
+      else if (ahead == 1) vm_wait<P>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();                    // tile kt landed everywhere; stage kt-1 free
+      if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, (kt + NST - 1) * EPT);
+      compute(kt % NST);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  } else {
+    issue(0, 0);
+    vm_wait<0>();
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) issue(cur ^ 1, (kt + 1) * EPT);
+      compute(cur);
+      vm_wait<0>();
+      __syncthreads();
+    }
   }
 
   // ---------------------------------------------------------------- epilogue --
@@ -200,16 +201,20 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm + 16 * mt + 4 * lg + i;
+      const int rl = wm + 16 * mt + 4 * lg + i;
+      const int m = m0 + rl;
       const long mr = epi.row_period > 0 ? (m % epi.row_period) : m;
       const bool mv = m < M;
       const float r1 = (epi.row1 && mv) ? epi.row1[mr * epi.row1_stride] : 0.f;
       const float r2 = (epi.row2 && mv) ? epi.row2[mr * epi.row2_stride] : 0.f;
+      float2 rs = make_float2(1.f, 0.f);
+      if constexpr (ROWNORM) rs = rowstat[rl];
 #pragma unroll
       for (int nt = 0; nt < NW; ++nt) {
         const int n = n0 + wn + 16 * nt + li;
         float x = acc[mt][nt][i];
         if (n < N) {
+          if constexpr (ROWNORM) x = rs.x * x + rs.y * rn.c1[n];
           if (epi.bias) x += epi.bias[n];
           if (epi.row1) x += r1 * epi.col1[n];
           if (epi.row2) x += r2 * epi.col2[n];
@@ -332,35 +337,45 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   }
 }
 
-template <typename TI, typename TO, int NW>
-static int launch_rows(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
-                       const EpiX& e, const ANorm* an, hipStream_t s) {
+template <typename TI, typename TO, int NW, bool DEEP, bool RN>
+static int launch_rows_v(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
+                         const EpiX& e, const RowNorm& rn, hipStream_t s) {
   constexpr int BN = 64 * NW;
+  constexpr int ROWB = DEEP ? 64 : 128, NST = DEEP ? 4 : 2;
   const int tn = cdiv(N, BN), tm = cdiv(M, R_BM);
   const long nb = (long)tn * tm;
   SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
-  const size_t lds = 2 * (size_t)(R_BM + BN) * R_ROWB + R_BM * sizeof(float2);
-  ANorm a = an ? *an : ANorm{};
-  if (an) {
-    auto kern = rows_gemm_kernel<TI, TO, NW, true>;
-    static bool attr = false;
-    if (!attr) { SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); attr = true; }
-    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
-                       (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
-  } else {
-    auto kern = rows_gemm_kernel<TI, TO, NW, false>;
-    static bool attr = false;
-    if (!attr) { SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); attr = true; }
-    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
-                       (const TI*)W, ldw, (TO*)C, ldc, e, a, tn);
+  const size_t lds = NST * (size_t)(R_BM + BN) * ROWB + R_BM * sizeof(float2);
+  auto kern = rows_gemm_kernel<TI, TO, NW, DEEP, RN>;
+  static bool attr = false;
+  if (!attr) {
+    SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
   }
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), lds, s, (int)M, (int)N, (int)K, (const TI*)A, lda,
+                     (const TI*)W, ldw, (TO*)C, ldc, e, rn, tn);
   SNV_LAUNCH_CHECK();
   return 0;
 }
 
+template <typename TI, typename TO, int NW>
+static int launch_rows(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
+                       const EpiX& e, const RowNorm* rn, hipStream_t s) {
+  // deep glds ring for the wide tiles (3 or 4 glds per wave per K-tile); K must hold 64-B tiles
+  constexpr bool DEEP_OK = NW == 4 || NW == 6;
+  const bool deep = DEEP_OK && !getenv("SNVRAG_GEMM_SHALLOW");
+  RowNorm r = rn ? *rn : RowNorm{};
+  if (deep) {
+    if (rn) return launch_rows_v<TI, TO, NW, DEEP_OK, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+    return launch_rows_v<TI, TO, NW, DEEP_OK, false>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+  }
+  if (rn) return launch_rows_v<TI, TO, NW, false, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+  return launch_rows_v<TI, TO, NW, false, false>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+}
+
 template <typename TI, typename TO>
 static int dispatch_nw(int nw, long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C,
-                       long ldc, const EpiX& e, const ANorm* an, hipStream_t s) {
+                       long ldc, const EpiX& e, const RowNorm* an, hipStream_t s) {
   switch (nw) {
     case 1: return launch_rows<TI, TO, 1>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
     case 2: return launch_rows<TI, TO, 2>(M, N, K, A, lda, W, ldw, C, ldc, e, an, s);
@@ -380,7 +395,7 @@ int rows_pick_nw(long N, bool need_full_row) {
 }
 
 int rows_linear(int din, int dout, long M, long N, long K, const void* A, long lda, const void* W, long ldw,
-                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_anorm_t* anorm, hipStream_t s) {
+                void* C, long ldc, const snvrag_epilogue_t* epi, const snvrag_rownorm_t* anorm, hipStream_t s) {
   const bool full = epi && epi->ln_g;
   const int nw = rows_pick_nw(N, full);
   SNV_CHECK_ARG(nw > 0, full ? "LayerNorm epilogue needs N in {64,128,256,384}" : "N must be a multiple of 64");
@@ -396,12 +411,13 @@ int rows_linear(int din, int dout, long M, long N, long K, const void* A, long l
     e.post_af = epi->post_af; e.post_af_period = epi->post_af_period; e.post_maf = epi->post_maf;
     e.stats_out = epi->stats_out;
   }
-  ANorm an{};
+  RowNorm an{};
   if (anorm) {
-    an.stats = anorm->stats; an.n_parts = anorm->n_parts; an.dim = (int)anorm->dim; an.g = anorm->g;
-    an.b = anorm->b; an.eps = anorm->eps;
+    an.stats = anorm->stats; an.n_parts = anorm->n_parts; an.dim = (int)anorm->dim; an.eps = anorm->eps;
+    an.c1 = anorm->c1;
+    SNV_CHECK_ARG(an.stats && an.c1, "rownorm needs stats and c1");
   }
-  const ANorm* ap = anorm ? &an : nullptr;
+  const RowNorm* ap = anorm ? &an : nullptr;
   if (din == SNVRAG_BF16 && dout == SNVRAG_BF16) return dispatch_nw<bf16, bf16>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
   if (din == SNVRAG_BF16) return dispatch_nw<bf16, float>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);
   if (dout == SNVRAG_F32) return dispatch_nw<float, float>(nw, M, N, K, A, lda, W, ldw, C, ldc, e, ap, s);

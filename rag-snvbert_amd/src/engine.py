@@ -149,6 +149,8 @@ class Engine:
         P.layers_t, P.layers = [], []
         for blk in bert.transformer_blocks:
             a, ff = blk.attention, blk.feed_forward
+            w2g, b2g, c2g = K.fold_layernorm(ff.w_2.weight.detach().to(dev), ff.w_2.bias.detach().to(dev),
+                                             ff.norm.weight.detach().to(dev), ff.norm.bias.detach().to(dev), T)
             t = dict(w_qkv=cvt(torch.cat([l.weight for l in a.linear_layers], 0)),
                      b_qkv=f32(torch.cat([l.bias for l in a.linear_layers], 0)),
                      w_o=cvt(a.output_layer.weight), b_o=f32(a.output_layer.bias),
@@ -156,7 +158,8 @@ class Engine:
                      w1=cvt(ff.w_1.weight), b1=f32(ff.w_1.bias),
                      lnf_g=f32(ff.norm.weight), lnf_b=f32(ff.norm.bias),
                      w2=cvt(ff.w_2.weight), b2=f32(ff.w_2.bias),
-                     ln2_g=f32(blk.output_sublayer.norm.weight), ln2_b=f32(blk.output_sublayer.norm.bias))
+                     ln2_g=f32(blk.output_sublayer.norm.weight), ln2_b=f32(blk.output_sublayer.norm.bias),
+                     w2g=w2g, b2g=b2g, c2g=c2g)
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}))
         if fm is None:

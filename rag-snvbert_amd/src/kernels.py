@@ -33,13 +33,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            post_base: Optional[torch.Tensor] = None, post_scale: float = 1.0,
            post_af: Optional[torch.Tensor] = None, post_af_period: int = 0, post_maf: bool = False,
            stats_out: Optional[torch.Tensor] = None,
-           anorm: Optional[Tuple[torch.Tensor, int, int, torch.Tensor, torch.Tensor]] = None,
+           rownorm: Optional[Tuple[torch.Tensor, int, int, torch.Tensor]] = None,
            out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """out[m, n] = act(x[m] . w[n] + bias[n] + row1[m]*col1[n] + row2[m]*col2[n]) + resid[m, n],
     optionally followed by a fused LayerNorm over the row (``ln=(g, b)``, + ``ln_act`` and the
     ``post_base + post_scale * y * maf(post_af)`` tail), or writing row statistics
-    (``stats_out`` float32 [n_tiles, M, 2]); ``anorm=(stats, n_parts, dim, g, b)`` applies a
-    LayerNorm to ``x`` while it is staged."""
+    (``stats_out`` float32 [n_tiles, M, 2]); ``rownorm=(stats, n_parts, dim, c1)`` folds a
+    LayerNorm of ``x`` into the epilogue (``w`` must be pre-scaled by gamma, ``c1 = w_orig @ gamma``,
+    beta folded into ``bias``) — see :func:`fold_layernorm`."""
     N.require_gpu(x, w)
     K = x.shape[-1]
     M = x.numel() // K
@@ -67,13 +68,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         e.post_af, e.post_af_period, e.post_maf = ptr(_c(post_af)), post_af_period, int(post_maf)
     e.stats_out = ptr(stats_out)
     an = None
-    if anorm is not None:
-        st, parts, dim, g, b = anorm
-        an = N.ANormS(ptr(st), parts, dim, ptr(g), ptr(b), 1e-5)
+    if rownorm is not None:
+        st, parts, dim, c1 = rownorm
+        an = N.RowNormS(ptr(st), parts, dim, 1e-5, ptr(c1))
     check(N.lib().snvrag_linear_ex(_dt(x.dtype), _dt(od), M, Nn, K, ptr(_c(x)), K, ptr(_c(w)), K,
                                    ptr(out), Nn, C.byref(e), C.byref(an) if an is not None else None,
                                    stream_ptr()), "linear")
     return out
+
+
+def fold_layernorm(w: torch.Tensor, b: torch.Tensor, g: torch.Tensor, beta: torch.Tensor, dtype: torch.dtype):
+    """LN(x) W^T + b = rstd*(x (W diag g)^T) - rstd*mean*(W g) + (W beta + b): returns (W', bias', c1)."""
+    w64 = w.double()
+    wg = (w64 * g.double()[None, :]).to(dtype).contiguous()
+    return wg, (w64 @ beta.double() + b.double()).float().contiguous(), (w64 @ g.double()).float().contiguous()
 
 
 def stat_tiles(n: int) -> int:

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -37,8 +37,8 @@ class Epilogue(C.Structure):
                 ("stats_out", vp)]
 
 
-class ANormS(C.Structure):
-    _fields_ = [("stats", vp), ("n_parts", C.c_int), ("dim", i64), ("g", vp), ("b", vp), ("eps", f32)]
+class RowNormS(C.Structure):
+    _fields_ = [("stats", vp), ("n_parts", C.c_int), ("dim", i64), ("eps", f32), ("c1", vp)]
 
 
 class LnPost(C.Structure):
@@ -64,7 +64,7 @@ class GtW(C.Structure):
 
 class LayerW(C.Structure):
     _fields_ = [(n, vp) for n in ("w_qkv", "b_qkv", "w_o", "b_o", "ln1_g", "ln1_b", "w1", "b1",
-                                  "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b")]
+                                  "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")]
 
 
 _SIGS = {
@@ -73,7 +73,7 @@ _SIGS = {
     "snvrag_device_info": ([C.c_int, C.c_char_p, C.c_int], C.c_int),
     "snvrag_linear": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), vp], C.c_int),
     "snvrag_linear_ex": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue),
-                          C.POINTER(ANormS), vp], C.c_int),
+                          C.POINTER(RowNormS), vp], C.c_int),
     "snvrag_layernorm": ([C.c_int, C.c_int, i64, i64, vp, i64, vp, i64, vp, vp, f32, vp, i64,
                           C.POINTER(LnPost), vp], C.c_int),
     "snvrag_attention": ([C.c_int, i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, f32, vp], C.c_int),

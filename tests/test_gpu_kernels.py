@@ -252,8 +252,9 @@ def test_linear_fused_layernorm_and_tail(dt, n):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_linear_stats_then_anorm_matches_ffn(dt):
-    """h = lrelu(x W1 + b1) with row stats -> out = lrelu(LN(h) W2 + b2): FeedForward of feed_forward.py."""
+def test_linear_stats_then_rownorm_matches_ffn(dt):
+    """h = lrelu(x W1 + b1) with row stats -> out = lrelu(LN(h) W2 + b2) with the LN folded into
+    the second GEMM (W2 diag(g), bias W2 b + b2, c1 = W2 g): FeedForward of feed_forward.py."""
     g = torch.Generator(device="cpu").manual_seed(1)
     M, D = 777, 384
     x = torch.randn(M, D, generator=g).to(DEV, dt)
@@ -268,7 +269,8 @@ def test_linear_stats_then_anorm_matches_ffn(dt):
     # stats are taken from the f32 accumulators, before the output is rounded to dt
     st_tol = 1e-4 if dt == torch.float32 else 2e-3
     torch.testing.assert_close(stats.sum(0)[:, 0].double(), hr.sum(1), rtol=st_tol, atol=st_tol * 100)
-    out = K().linear(h, w2, b2, act=2, slope=0.1, anorm=(stats, parts, 4 * D, gf, bf))
+    w2g, b2g, c1 = K().fold_layernorm(w2.float(), b2, gf, bf, dt)
+    out = K().linear(h, w2g, b2g, act=2, slope=0.1, rownorm=(stats, parts, 4 * D, c1))
     hn = torch.nn.functional.layer_norm(hr, (4 * D,), gf.double(), bf.double(), 1e-5)
     ref = torch.nn.functional.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
     tol = 1e-4 if dt == torch.float32 else 5e-2

@@ -26,5 +26,6 @@ for s in $STEPS; do
     bench)   step bench 900 python bench.py --steps ${BSTEPS:-5} --warmup 2 ${BENCH_ARGS:-} ;;
     benchab) step bench_old 900 env SNVRAG_GEMM_TILE128=1 SNVRAG_UNFUSED_LN=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0
              step bench_tile128_fusedoff 900 env SNVRAG_UNFUSED_LN=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0 ;;
+    shallow) step bench_shallow 900 env SNVRAG_GEMM_SHALLOW=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0 ;;
   esac
 done
