@@ -75,6 +75,20 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Sum over aligned groups of W (2/4/8/16) consecutive lanes, result in every lane of the
+// group; DPP lane moves (quad_perm xor1/xor2, row_half_mirror, row_mirror) instead of
+// ds_bpermute round trips through the LDS.
+template <int CTRL> __device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int W> __device__ __forceinline__ float group_sum(float v) {
+  static_assert(W == 2 || W == 4 || W == 8 || W == 16, "group width");
+  v += dpp_mov<0xB1>(v);                    // quad_perm [1,0,3,2]
+  if constexpr (W >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (W >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: quad q <-> 1-q
+  if constexpr (W >= 16) v += dpp_mov<0x140>(v); // row_mirror: half h <-> 1-h
+  return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

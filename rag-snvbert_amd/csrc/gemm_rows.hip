@@ -58,6 +58,29 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+__device__ __forceinline__ void load8(const float* p, float* t) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  t[0] = a.x; t[1] = a.y; t[2] = a.z; t[3] = a.w; t[4] = b.x; t[5] = b.y; t[6] = b.z; t[7] = b.w;
+}
+__device__ __forceinline__ void load8(const bf16* p, float* t) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    t[2 * e] = __uint_as_float(a[e] << 16);
+    t[2 * e + 1] = __uint_as_float(a[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void store8(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = (bf16)v[e];
+  *reinterpret_cast<bf16x8*>(p) = a;
+}
+
 __device__ __forceinline__ float maf_w(float af) {
   const float maf = fminf(af, 1.0f - af);
   return fminf(log1pf(1.0f / (maf + 1e-6f)), 3.0f);
@@ -83,6 +106,7 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   static_assert(BN % (RPI * 8) == 0 && R_BM % (RPI * 8) == 0, "tile rows must split over 8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* rowstat = reinterpret_cast<float2*>(smem + NST * STAGE);
+  float* colv = reinterpret_cast<float*>(smem + NST * STAGE + R_BM * sizeof(float2));  // [6][BN]
 
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
@@ -111,6 +135,15 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
       const float rstd = 1.0f / sqrtf(var + rn.eps);
       rowstat[tid] = make_float2(rstd, -rstd * mean);
     }
+  }
+
+  // per-column epilogue vectors (c1, bias, col1, col2, ln_g, ln_b) staged once in LDS
+  {
+    const float* cp[6] = {ROWNORM ? rn.c1 : nullptr, epi.bias, epi.row1 ? epi.col1 : nullptr,
+                          epi.row2 ? epi.col2 : nullptr, epi.ln_g, epi.ln_b};
+#pragma unroll
+    for (int v = 0; v < 6; ++v)
+      if (cp[v] && tid < BN) colv[v * BN + tid] = cp[v][n0 + tid];
   }
 
   auto issue = [&](int stage, int k0) {
@@ -194,146 +227,137 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   }
 
   // ---------------------------------------------------------------- epilogue --
-  // values in acc: row m = m0 + wm + 16 mt + 4 lg + i, col n = n0 + wn + 16 nt + li
-  float* red = reinterpret_cast<float*>(smem);           // [128][4] partial row sums (stage memory reuse)
-  float* red2 = red + R_BM * 4;
+  // Accumulators go to LDS as f32 (one 64-row half at a time, the ring is free), then
+  // every wave walks whole rows: RL lanes per row, CPL 8-column chunks per lane, so
+  // every global access (bias/LN vectors, residual, output) is a 16/32-B vector and
+  // the LayerNorm reductions stay inside RL lanes.
+  constexpr int SLD = BN + 4;                      // f32 row stride: rows 4 apart hit different banks
+  constexpr int RL = BN / 8 >= 16 ? 16 : BN / 8;   // lanes per row
+  constexpr int CPL = BN / 8 / RL;                 // 8-column chunks per lane
+  constexpr int RPW = 64 / RL;                     // rows per wave per pass
+  static_assert(64 * SLD * 4 <= NST * STAGE, "epilogue tile must fit the LDS ring");
+  float* tile = reinterpret_cast<float*>(smem);
+  const int sub = lane % RL, rw = lane / RL;
+  const bool do_ln = epi.ln_g != nullptr;
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    if (wmi == half) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = wm + 16 * mt + 4 * lg + i;
-      const int m = m0 + rl;
-      const long mr = epi.row_period > 0 ? (m % epi.row_period) : m;
+        for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tile[(16 * mt + 4 * lg + i) * SLD + wn + 16 * nt + li] = acc[mt][nt][i];
+    }
+    __syncthreads();
+    constexpr int NIT = 64 / (8 * RPW);            // row passes per wave per half
+    float res[NIT][CPL][8];
+    if (epi.resid) {                               // issue every residual load of this half first
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int m = m0 + 64 * half + (wave + 8 * it) * RPW + rw;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          if (m < M) load8(reinterpret_cast<const TO*>(epi.resid) + (long)m * epi.ld_resid + n0 + 8 * (sub + RL * j), res[it][j]);
+          else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) res[it][j][e] = 0.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int rl = (wave + 8 * it) * RPW + rw;
+      const int m = m0 + 64 * half + rl;
       const bool mv = m < M;
+      float v[CPL][8];
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) load8(tile + rl * SLD + 8 * (sub + RL * j), v[j]);
+      const long mr = epi.row_period > 0 ? (m % epi.row_period) : m;
       const float r1 = (epi.row1 && mv) ? epi.row1[mr * epi.row1_stride] : 0.f;
       const float r2 = (epi.row2 && mv) ? epi.row2[mr * epi.row2_stride] : 0.f;
       float2 rs = make_float2(1.f, 0.f);
-      if constexpr (ROWNORM) rs = rowstat[rl];
+      if constexpr (ROWNORM) rs = rowstat[64 * half + rl];
 #pragma unroll
-      for (int nt = 0; nt < NW; ++nt) {
-        const int n = n0 + wn + 16 * nt + li;
-        float x = acc[mt][nt][i];
-        if (n < N) {
-          if constexpr (ROWNORM) x = rs.x * x + rs.y * rn.c1[n];
-          if (epi.bias) x += epi.bias[n];
-          if (epi.row1) x += r1 * epi.col1[n];
-          if (epi.row2) x += r2 * epi.col2[n];
-          x = apply_act(epi.act, x, epi.slope);
-          if (epi.resid && mv) x += to_f32(reinterpret_cast<const TO*>(epi.resid)[(long)m * epi.ld_resid + n]);
-        } else {
-          x = 0.f;
+      for (int j = 0; j < CPL; ++j) {
+        const int c = 8 * (sub + RL * j);
+        float t[8];
+        if constexpr (ROWNORM) {
+          load8(colv + 0 * BN + c, t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[j][e] = rs.x * v[j][e] + rs.y * t[e];
         }
-        acc[mt][nt][i] = x;
-      }
-    }
-  }
-  const bool do_ln = epi.ln_g != nullptr;
-  if (do_ln || epi.stats_out) {
-    // pass 1: row sums (and sums of squares for stats) over this wave's columns
+        if (epi.bias) {
+          load8(colv + 1 * BN + c, t);
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+          for (int e = 0; e < 8; ++e) v[j][e] += t[e];
+        }
+        if (epi.row1) {
+          load8(colv + 2 * BN + c, t);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float s = 0.f, ss = 0.f;
+          for (int e = 0; e < 8; ++e) v[j][e] = fmaf(r1, t[e], v[j][e]);
+        }
+        if (epi.row2) {
+          load8(colv + 3 * BN + c, t);
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt) { const float x = acc[mt][nt][i]; s += x; ss += x * x; }
+          for (int e = 0; e < 8; ++e) v[j][e] = fmaf(r2, t[e], v[j][e]);
+        }
+        if (epi.act) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); ss += __shfl_xor(ss, o, 64); }
-        if (li == 0) {
-          const int rl = wm + 16 * mt + 4 * lg + i;
-          red[rl * 4 + wni] = s;
-          red2[rl * 4 + wni] = ss;
+          for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.act, v[j][e], epi.slope);
+        }
+        if (epi.resid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[j][e] += res[it][j][e];
         }
       }
-    __syncthreads();
-    if (epi.stats_out && !do_ln) {
-      if (tid < R_BM && m0 + tid < M) {
-        const float s = red[tid * 4] + red[tid * 4 + 1] + red[tid * 4 + 2] + red[tid * 4 + 3];
-        const float ss = red2[tid * 4] + red2[tid * 4 + 1] + red2[tid * 4 + 2] + red2[tid * 4 + 3];
-        reinterpret_cast<float2*>(epi.stats_out)[(long)tn * M + m0 + tid] = make_float2(s, ss);
-      }
-    }
-  }
-  if (do_ln) {
-    // two-pass LayerNorm over the BN (= N) columns of each row
-    float mean[4][4];
+      if (do_ln) {
+        float s = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+        for (int j = 0; j < CPL; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = wm + 16 * mt + 4 * lg + i;
-        mean[mt][i] = (red[rl * 4] + red[rl * 4 + 1] + red[rl * 4 + 2] + red[rl * 4 + 3]) / (float)N;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
+          for (int e = 0; e < 8; ++e) s += v[j][e];
+        const float mean = group_sum<RL>(s) / (float)N;
         float q = 0.f;
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt) { const float d = acc[mt][nt][i] - mean[mt][i]; q += d * d; }
+        for (int j = 0; j < CPL; ++j)
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
-        if (li == 0) red[(wm + 16 * mt + 4 * lg + i) * 4 + wni] = q;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = wm + 16 * mt + 4 * lg + i;
-        const int m = m0 + rl;
-        const float var = (red[rl * 4] + red[rl * 4 + 1] + red[rl * 4 + 2] + red[rl * 4 + 3]) / (float)N;
-        const float rstd = 1.0f / sqrtf(var + epi.ln_eps);
+          for (int e = 0; e < 8; ++e) { const float d = v[j][e] - mean; q = fmaf(d, d, q); }
+        const float rstd = 1.0f / sqrtf(group_sum<RL>(q) / (float)N + epi.ln_eps);
         float w = 1.0f;
-        if (epi.post_maf && m < M) {
-          const long ar = epi.post_af_period > 0 ? m % epi.post_af_period : m;
-          w = maf_w(epi.post_af[ar]);
-        }
+        if (epi.post_maf && mv) w = maf_w(epi.post_af[epi.post_af_period > 0 ? m % epi.post_af_period : m]);
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt) {
-          const int n = n0 + wn + 16 * nt + li;
-          float y = (acc[mt][nt][i] - mean[mt][i]) * rstd * epi.ln_g[n] + epi.ln_b[n];
-          y = apply_act(epi.ln_act, y, 0.f);
-          if (epi.post_base && m < M)
-            y = to_f32(reinterpret_cast<const TO*>(epi.post_base)[(long)m * epi.ld_post + n]) + epi.post_scale * (y * w);
-          acc[mt][nt][i] = y;
+        for (int j = 0; j < CPL; ++j) {
+          const int c = 8 * (sub + RL * j);
+          float g[8], bb[8];
+          load8(colv + 4 * BN + c, g);
+          load8(colv + 5 * BN + c, bb);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.ln_act, (v[j][e] - mean) * rstd * g[e] + bb[e], 0.f);
+          if (epi.post_base && mv) {
+            load8(reinterpret_cast<const TO*>(epi.post_base) + (long)m * epi.ld_post + n0 + c, g);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[j][e] = g[e] + epi.post_scale * (v[j][e] * w);
+          }
         }
       }
-  }
-  // store: bf16 tiles go through LDS (the stages are free) for row-contiguous 16-B stores
-  if constexpr (sizeof(TO) == 2) {
-    constexpr int SLD = BN + 8;                                 // padded row (elements)
-    TO* st = reinterpret_cast<TO*>(smem);
-    __syncthreads();                                            // LN scratch reads done
+      if (epi.stats_out) {
+        float s = 0.f, ss = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+        for (int j = 0; j < CPL; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+          for (int e = 0; e < 8; ++e) { s += v[j][e]; ss = fmaf(v[j][e], v[j][e], ss); }
+        s = group_sum<RL>(s);
+        ss = group_sum<RL>(ss);
+        if (sub == 0 && mv) reinterpret_cast<float2*>(epi.stats_out)[(long)tn * M + m] = make_float2(s, ss);
+      }
+      if (mv) {
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt)
-          st[(wm + 16 * mt + 4 * lg + i) * SLD + wn + 16 * nt + li] = from_f32<TO>(acc[mt][nt][i]);
-    __syncthreads();
-    constexpr int CPR = BN / 8;
-    for (int id = tid; id < R_BM * CPR; id += 512) {
-      const int rl = id / CPR, c = (id % CPR) * 8;
-      const int m = m0 + rl, n = n0 + c;
-      if (m < M && n < N)
-        *reinterpret_cast<u32x4*>(C + (long)m * ldc + n) = *reinterpret_cast<const u32x4*>(st + rl * SLD + c);
+        for (int j = 0; j < CPL; ++j) store8(C + (long)m * ldc + n0 + 8 * (sub + RL * j), v[j]);
+      }
     }
-  } else {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm + 16 * mt + 4 * lg + i;
-        if (m >= M) continue;
-#pragma unroll
-        for (int nt = 0; nt < NW; ++nt) {
-          const int n = n0 + wn + 16 * nt + li;
-          if (n < N) C[(long)m * ldc + n] = from_f32<TO>(acc[mt][nt][i]);
-        }
-      }
+    __syncthreads();
   }
 }
 
@@ -345,7 +369,7 @@ static int launch_rows_v(long M, long N, long K, const void* A, long lda, const 
   const int tn = cdiv(N, BN), tm = cdiv(M, R_BM);
   const long nb = (long)tn * tm;
   SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
-  const size_t lds = NST * (size_t)(R_BM + BN) * ROWB + R_BM * sizeof(float2);
+  const size_t lds = NST * (size_t)(R_BM + BN) * ROWB + R_BM * sizeof(float2) + 6 * BN * sizeof(float);
   auto kern = rows_gemm_kernel<TI, TO, NW, DEEP, RN>;
   static bool attr = false;
   if (!attr) {
@@ -363,7 +387,7 @@ static int launch_rows(long M, long N, long K, const void* A, long lda, const vo
                        const EpiX& e, const RowNorm* rn, hipStream_t s) {
   // deep glds ring for the wide tiles (3 or 4 glds per wave per K-tile); K must hold 64-B tiles
   constexpr bool DEEP_OK = NW == 4 || NW == 6;
-  const bool deep = DEEP_OK && !getenv("SNVRAG_GEMM_SHALLOW");
+  const bool deep = DEEP_OK && getenv("SNVRAG_GEMM_DEEP");   // measured: the 2-stage 128-B ring is faster
   RowNorm r = rn ? *rn : RowNorm{};
   if (deep) {
     if (rn) return launch_rows_v<TI, TO, NW, DEEP_OK, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);

@@ -28,6 +28,11 @@ def sharded_search(local_keys: torch.Tensor, k: int, group=None,
     world = dist.get_world_size(group)
     if world == 1:
         return local_keys
-    out = torch.empty((world,) + tuple(local_keys.shape), dtype=local_keys.dtype, device=local_keys.device)
-    dist.all_gather_into_tensor(out, local_keys.contiguous(), group=group)
-    return merge_keys_gathered(out, k, merge_fn)
+    # keys travel as their int64 bit pattern (collectives have no uint64 reduction need here)
+    src = local_keys.contiguous().view(torch.int64)
+    out = torch.empty((world,) + tuple(src.shape), dtype=torch.int64, device=src.device)
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(out.unbind(0)), src, group=group)
+    else:
+        dist.all_gather_into_tensor(out, src, group=group)
+    return merge_keys_gathered(out.view(local_keys.dtype), k, merge_fn)
