@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 3
+#define SNVRAG_ABI_VERSION 4
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -104,6 +104,9 @@ int snvrag_layernorm(int dtype_in, int dtype_out, int64_t M, int64_t N,
 int snvrag_attention(int dtype, int64_t nseq, int64_t L, int heads, int dh,
                      const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out,
                      float scale, void* stream);
+/* Waves (32 queries each) of the bf16 dh=32 kernel that overflowed the fixed-shift
+ * softmax and were recomputed with the exact online-max path since the last reset. */
+int snvrag_attention_fallbacks(int reset);
 
 /* ------------------------------------------------------------------------
  * Embedding  (model/embedding/bert.py:66-77, af_embedding.py:79-91,
@@ -227,6 +230,9 @@ typedef struct {
   /* feed_forward.norm folded into w_2 (fused path): w2g = w2 diag(lnf_g),
    * b2g = b2 + w2 lnf_b, c2g = w2 lnf_g */
   const void* w2g; const float* b2g; const float* c2g;
+  /* factor already folded into the q rows of w_qkv / b_qkv (0 = none); the bf16 engine
+   * folds log2(e)/sqrt(dh) so attention's exp2 needs no per-score scaling */
+  float q_scale;
 } snvrag_layer_t;
 
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);

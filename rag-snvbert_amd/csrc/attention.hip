@@ -198,6 +198,275 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, con
   }
 }
 
+// ------------------------------------------------------- bf16, head dim 32 --
+// attn32: one workgroup = 4 waves x 32 queries (two 16-query MFMA column tiles per
+// wave, sharing every K / V^T fragment read) of one (sequence, head); K/V stream
+// through LDS in 64-key tiles, register-staged and double buffered (loads of tile
+// t+1 in flight under tile t's MFMAs).  At dh = 32 the exp, not the MFMA, bounds
+// the loop, so the softmax VALU is cut to one v_exp_f32 + half a cvt per score:
+//  * Q arrives pre-scaled by log2(e)/sqrt(dh) (folded into W_q by the engine), or is
+//    scaled once when loaded;
+//  * the shift is fixed per query after the first key tile (m_q = exact max of
+//    tile 0) and enters as the MFMA's C operand (S^T = K Q^T - m_q), so later
+//    tiles run no max, no subtraction and no O rescale (softmax is shift-invariant;
+//    m_q <= the true max, so the dominant terms never underflow);
+//  * the row sum l_q comes out of an extra MFMA against a ones matrix (same
+//    bf16-rounded P that multiplies V).
+// If a later score exceeds m_q by more than f32 can hold (l or O not finite), that
+// wave recomputes its queries with an exact online-max softmax straight from global
+// memory (attn32_online) — correctness never depends on the data range.
+namespace a32 {
+constexpr int QPW = 32, WAVES = 4, QPB = QPW * WAVES, KT = 64;
+constexpr int TB = KT * 64;                        // one K or V tile: 64 keys x 64 B
+// K tile: 64-B rows, chunk XOR (-(key>>2))&3 — conflict-free for the ds_read_b128 lane groups
+__device__ __forceinline__ int k_off(int key, int chunk) { return key * 64 + ((chunk ^ ((-(key >> 2)) & 3)) << 4); }
+// V tile: 64-B rows, 32-B halves swapped on (key>>2)&1 — conflict-free ds_read_b64_tr_b16
+__device__ __forceinline__ int v_off(int key, int half) { return key * 64 + ((half ^ ((key >> 2) & 1)) << 5); }
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+struct State {
+  f32x4 o[2][2];     // [e][qt]: O^T rows 16e + 4lg + r, query column li
+  f32x4 ls[2];       // [qt]: row sums (all four entries equal)
+  f32x4 negm[2];     // [qt]: -m_q broadcast (MFMA C operand)
+};
+
+template <int NKT, bool MASK, bool FIRST>
+__device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
+                                     State& st, int li, int lg) {
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 s[NKT][2];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kt + k_off(16 * kt + li, lg));
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt], FIRST ? zero : st.negm[qt], 0, 0, 0);
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (kbase + 16 * kt + 4 * lg + r >= L) {
+          s[kt][0][r] = -INFINITY;
+          s[kt][1][r] = -INFINITY;
+        }
+  }
+  if constexpr (FIRST) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      st.negm[qt] = f32x4{-mx, -mx, -mx, -mx};
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) s[kt][qt] += st.negm[qt];
+    }
+  }
+  constexpr int NCB = (NKT + 1) / 2;
+  bf16x8 pb[NCB][2];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kt = 2 * cb + (j >> 2);
+        pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
+      }
+  const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int k0 = 32 * cb + 4 * lg + tq;
+      const bf16x8 vf = cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[cb][qt], st.o[e][qt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) st.ls[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[cb][qt], st.ls[qt], 0, 0, 0);
+  }
+}
+
+template <bool FIRST>
+__device__ __forceinline__ void tile_any(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
+                                         State& st, int li, int lg) {
+  const int rem = L - kbase;
+  if (rem >= KT) tile<4, false, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
+  else if (rem <= 16) tile<1, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
+  else if (rem <= 32) tile<2, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
+  else tile<4, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
+}
+
+// Exact online-max softmax for one wave's 32 queries, K/V read from global memory
+// (16 keys per step).  Only runs when the fixed-shift pass overflowed.
+__device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, long ld, int L, const bf16x8 (&qf)[2],
+                                           State& st, int li, int lg) {
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 2; ++e) st.o[e][0] = st.o[e][1] = zero;
+  for (int k0 = 0; k0 < L; k0 += 16) {
+    const int kr = k0 + li;
+    const bf16x8 kf = kr < L ? *reinterpret_cast<const bf16x8*>(Kp + (long)kr * ld + 8 * lg) : bf16x8{};
+    bf16x8 vf[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int key = k0 + 4 * lg + j;
+        vf[e][j] = (j < 4 && key < L) ? Vp[(long)key * ld + 16 * e + li] : (bf16)0.f;
+      }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt], zero, 0, 0, 0);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (k0 + 4 * lg + r >= L) sc[r] = -INFINITY;
+        mx = fmaxf(mx, sc[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qt], mx), alpha = exp2f(m[qt] - mn);
+      bf16x8 pb{};
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bf16 pr = (bf16)exp2f(sc[r] - mn);
+        pb[r] = pr;
+        ps += (float)pr;
+      }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l[qt] = l[qt] * alpha + ps;
+      m[qt] = mn;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[e], pb, st.o[e][qt] * alpha, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) st.ls[qt] = f32x4{l[qt], l[qt], l[qt], l[qt]};
+}
+}  // namespace a32
+
+template <bool PRESCALED>
+__global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __restrict__ qkv, long ld,
+                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
+                                                   int* __restrict__ n_fallback) {
+  using namespace a32;
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * TB];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int D = H * 32;
+  const long base = (long)seq * L * ld;
+  const bf16* Qp = qkv + base + h * 32;
+  const bf16* Kp = qkv + base + D + h * 32;
+  const bf16* Vp = qkv + base + 2 * D + h * 32;
+  const int q0 = qb * QPB + wave * QPW;
+  const bool active = q0 < L;                      // wave-uniform
+
+  bf16x8 qf[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = q0 + 16 * qt + li;
+    bf16x8 v = q < L ? *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + 8 * lg) : bf16x8{};
+    if constexpr (!PRESCALED) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * scale_log2e);
+    }
+    qf[qt] = v;
+  }
+
+  // loader: thread -> (key = tid / 4, 16-B chunk = tid % 4) of K and of V
+  const int lkey = tid >> 2, lch = tid & 3;
+  u32x4 kr = {0u, 0u, 0u, 0u}, vr = {0u, 0u, 0u, 0u};
+  const bf16* kp_l = Kp + (long)lkey * ld + 8 * lch;
+  const bf16* vp_l = Vp + (long)lkey * ld + 8 * lch;
+#define A32_LOAD(t)                                                         \
+  {                                                                         \
+    const bool ok = (t) * KT + lkey < L;                                    \
+    const long off = (long)(t) * KT * ld;                                   \
+    kr = ok ? *reinterpret_cast<const u32x4*>(kp_l + off) : u32x4{0u, 0u, 0u, 0u}; \
+    vr = ok ? *reinterpret_cast<const u32x4*>(vp_l + off) : u32x4{0u, 0u, 0u, 0u}; \
+  }
+#define A32_STORE(stage)                                                                      \
+  {                                                                                           \
+    *reinterpret_cast<u32x4*>(smem[stage] + k_off(lkey, lch)) = kr;                           \
+    *reinterpret_cast<u32x4*>(smem[stage] + TB + v_off(lkey, lch >> 1) + 16 * (lch & 1)) = vr; \
+  }
+
+  State st;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    st.o[0][qt] = st.o[1][qt] = st.ls[qt] = zero;
+    st.negm[qt] = zero;
+  }
+  const int ntile = (L + KT - 1) / KT;
+  A32_LOAD(0);
+  A32_STORE(0);
+  __syncthreads();
+  for (int t = 0; t < ntile; ++t) {
+    const bool more = t + 1 < ntile;
+    if (more) A32_LOAD(t + 1);
+    if (active) {
+      const char* Kt = smem[t & 1];
+      if (t == 0) tile_any<true>(Kt, Kt + TB, 0, L, qf, st, li, lg);
+      else tile_any<false>(Kt, Kt + TB, t * KT, L, qf, st, li, lg);
+    }
+    if (more) A32_STORE((t + 1) & 1);
+    __syncthreads();
+  }
+#undef A32_LOAD
+#undef A32_STORE
+  if (!active) return;
+
+  bool bad = false;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float l = st.ls[qt][0];
+    bad |= !(l > 0.f && l < INFINITY);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(st.o[e][qt][r]);
+  }
+  if (__ballot(bad)) {
+    if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
+    attn32_online(Kp, Vp, ld, L, qf, st, li, lg);
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = q0 + 16 * qt + li;
+    if (q >= L) continue;
+    const float inv = 1.0f / st.ls[qt][0];
+    bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * 32;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(st.o[e][qt][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * e + 4 * lg) = w;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- f32 path --
 template <int DH>
 __global__ __launch_bounds__(64) void attn_fwd_f32(int nseq, int L, int H, const float* __restrict__ qkv,
@@ -244,11 +513,31 @@ __global__ __launch_bounds__(64) void attn_fwd_f32(int nseq, int L, int H, const
   }
 }
 
+// device counter of waves that took the exact online-softmax fallback (tests read it)
+static int* attn_fallback_counter() {
+  static int* p = nullptr;
+  if (!p && hipMalloc(&p, sizeof(int)) == hipSuccess) (void)hipMemset(p, 0, sizeof(int));
+  return p;
+}
+
 template <int DH>
 static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, long ld, void* out,
                        long ldo, float scale, hipStream_t s) {
   evlog_begin(s);
-  if (dtype == SNVRAG_BF16) {
+  if (DH == 32 && dtype == SNVRAG_BF16 && !getenv("SNVRAG_ATTN_V1")) {
+    const int nqb = cdiv(L, a32::QPB);
+    const long nb = (long)nqb * H * nseq;
+    SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
+    const float sl2 = scale * 1.4426950408889634f;
+    const bool pre = fabsf(sl2 - 1.0f) < 1e-6f;      // Q already carries log2(e)/sqrt(dh)
+    int* cnt = attn_fallback_counter();
+    if (pre)
+      hipLaunchKernelGGL(attn32_bf16<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                         (bf16*)out, ldo, 1.0f, nqb, cnt);
+    else
+      hipLaunchKernelGGL(attn32_bf16<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                         (bf16*)out, ldo, sl2, nqb, cnt);
+  } else if (dtype == SNVRAG_BF16) {
     const int nqb = cdiv(L, AQ);
     const long nb = (long)nqb * H * nseq;
     SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
@@ -266,6 +555,15 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
 }  // namespace snvrag
 
 using namespace snvrag;
+
+extern "C" int snvrag_attention_fallbacks(int reset) {
+  int* p = attn_fallback_counter();
+  if (!p) return fail(__func__, "no device counter");
+  int v = 0;
+  SNV_HIP(hipMemcpy(&v, p, sizeof(int), hipMemcpyDeviceToHost));
+  if (reset) SNV_HIP(hipMemset(p, 0, sizeof(int)));
+  return v;
+}
 
 extern "C" int snvrag_attention(int dtype, int64_t nseq, int64_t L, int heads, int dh,
                                 const void* qkv, int64_t ld_qkv, void* out, int64_t ld_out,

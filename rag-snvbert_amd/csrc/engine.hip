@@ -79,7 +79,9 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       e.bias = ly.b_qkv;
       rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
       if (rc) return rc;
-      rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, scale, stream);
+      // q rows may carry a folded factor (the bf16 engine folds log2(e)/sqrt(dh))
+      const float sc = ly.q_scale > 0.f ? scale / ly.q_scale : scale;
+      rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, sc, stream);
       if (rc) return rc;
       if (fused) {
         // x1 = LN1(x + attn Wo^T + bo)                       (one launch)

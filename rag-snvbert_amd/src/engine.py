@@ -21,6 +21,8 @@ from __future__ import annotations
 import weakref
 from typing import Dict, Optional
 
+import math
+
 import torch
 import torch.nn as nn
 
@@ -151,8 +153,14 @@ class Engine:
             a, ff = blk.attention, blk.feed_forward
             w2g, b2g, c2g = K.fold_layernorm(ff.w_2.weight.detach().to(dev), ff.w_2.bias.detach().to(dev),
                                              ff.norm.weight.detach().to(dev), ff.norm.bias.detach().to(dev), T)
-            t = dict(w_qkv=cvt(torch.cat([l.weight for l in a.linear_layers], 0)),
-                     b_qkv=f32(torch.cat([l.bias for l in a.linear_layers], 0)),
+            # bf16: fold log2(e)/sqrt(dh) into the q rows so attention's exp2 takes raw scores
+            qs = math.log2(math.e) / math.sqrt(a.dims) if T == torch.bfloat16 else 0.0
+            wq = torch.cat([l.weight for l in a.linear_layers], 0).detach().to(dev).float().clone()
+            bq = torch.cat([l.bias for l in a.linear_layers], 0).detach().to(dev).float().clone()
+            if qs:
+                wq[:D] *= qs
+                bq[:D] *= qs
+            t = dict(w_qkv=cvt(wq), b_qkv=f32(bq),
                      w_o=cvt(a.output_layer.weight), b_o=f32(a.output_layer.bias),
                      ln1_g=f32(blk.input_sublayer.norm.weight), ln1_b=f32(blk.input_sublayer.norm.bias),
                      w1=cvt(ff.w_1.weight), b1=f32(ff.w_1.bias),
@@ -161,7 +169,7 @@ class Engine:
                      ln2_g=f32(blk.output_sublayer.norm.weight), ln2_b=f32(blk.output_sublayer.norm.bias),
                      w2g=w2g, b2g=b2g, c2g=c2g)
             P.layers_t.append(t)
-            P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}))
+            P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:
             return P
         hc = fm.hap_classifier

@@ -125,6 +125,14 @@ def attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int,
     return out
 
 
+def attention_fallbacks(reset: bool = True) -> int:
+    """Waves that took the exact online-max path of the bf16 dh=32 kernel (see attention.hip)."""
+    n = N.lib().snvrag_attention_fallbacks(int(reset))
+    if n < 0:
+        check(n, "attention_fallbacks")
+    return n
+
+
 # ---------------------------------------------------------------- embedding --
 def af_features(af: torch.Tensor, freqs: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     N.require_gpu(af)

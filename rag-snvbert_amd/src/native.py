@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -64,7 +64,7 @@ class GtW(C.Structure):
 
 class LayerW(C.Structure):
     _fields_ = [(n, vp) for n in ("w_qkv", "b_qkv", "w_o", "b_o", "ln1_g", "ln1_b", "w1", "b1",
-                                  "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")]
+                                  "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")] + [("q_scale", f32)]
 
 
 _SIGS = {
@@ -77,6 +77,7 @@ _SIGS = {
     "snvrag_layernorm": ([C.c_int, C.c_int, i64, i64, vp, i64, vp, i64, vp, vp, f32, vp, i64,
                           C.POINTER(LnPost), vp], C.c_int),
     "snvrag_attention": ([C.c_int, i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, f32, vp], C.c_int),
+    "snvrag_attention_fallbacks": ([C.c_int], C.c_int),
     "snvrag_af_features": ([C.c_int, i64, vp, vp, C.c_int, vp, vp], C.c_int),
     "snvrag_embed_tokens": ([C.c_int, i64, i64, i64, vp, vp, i64, vp, vp, C.c_int, i64, vp, vp], C.c_int),
     "snvrag_posfeat": ([i64, i64, vp, C.POINTER(PosfeatW), vp, vp], C.c_int),

@@ -297,3 +297,41 @@ def test_encoder_fused_equals_unfused(dt, monkeypatch):
     K().encoder_forward(b, P.layers, 12, ws)
     tol = 2e-4 if dt == torch.float32 else 6e-2
     torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
+
+
+def _attn_ref(qkv, nseq, L, H, dh):
+    q, k, v = qkv.float().view(nseq, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q @ k.transpose(-1, -2) / dh ** 0.5, -1)
+    return (p @ v).permute(0, 2, 1, 3).reshape(nseq * L, H * dh)
+
+
+@pytest.mark.parametrize("L", [1030, 64, 77, 16, 5])
+def test_attention_dh32_bf16_fixed_shift(L):
+    """bf16 dh=32 kernel (fixed per-query shift + ones-MFMA row sums) vs fp32 softmax;
+    L covers full tiles, a 1-key..48-key tail and L < one tile."""
+    torch.manual_seed(L)
+    nseq, H, dh = 3, 4, 32
+    qkv = (torch.randn(nseq * L, 3 * H * dh, device=DEV) * 1.5).to(torch.bfloat16)
+    K().attention_fallbacks(True)
+    out = K().attention(qkv, nseq, L, H, dh)
+    ref = _attn_ref(qkv, nseq, L, H, dh)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    assert K().attention_fallbacks(True) == 0
+
+
+def test_attention_dh32_overflow_takes_exact_fallback():
+    """Scores far above the first key tile's max overflow the fixed shift: the affected
+    waves must recompute with the online-max path and still match."""
+    torch.manual_seed(1)
+    nseq, L, H, dh = 2, 300, 2, 32
+    qkv = torch.randn(nseq * L, 3 * H * dh, device=DEV) * 0.1
+    D = H * dh
+    qkv[:, :D] = 4.0                       # |q| large
+    qkv[200, D:2 * D] = 8.0                # one key (seq 0, position 200) with a huge score
+    qkv = qkv.to(torch.bfloat16)
+    K().attention_fallbacks(True)
+    out = K().attention(qkv, nseq, L, H, dh)
+    ref = _attn_ref(qkv, nseq, L, H, dh)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    assert K().attention_fallbacks(True) > 0
