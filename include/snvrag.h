@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 4
+#define SNVRAG_ABI_VERSION 5
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -189,11 +189,16 @@ int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const
 /* Scan: every block scans a contiguous range of the panel and keeps an exact
  * per-query top-k (k <= 32) of its range; partial lists (ascending uint64 keys
  * ((D + 2^30) << 32 | ref_index), UINT64_MAX padding) -> part_keys [n_parts, nq, k].
- * ref_offset is added to ref indices (panel shards).  Returns n_parts via *n_parts_out. */
+ * ref_offset is added to ref indices (panel shards).  th_init (nullable, [nq]) is a per-query
+ * strict upper bound on the distances worth keeping (e.g. from snvrag_knn_threshold over a
+ * sample of the panel: any bound >= the true k-th distance + 1 leaves the result exact). */
 int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq);
 int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_codes, int32_t n_sites_pad,
                     const void* lut, int32_t nq, int limbs, int k, int64_t ref_offset,
-                    uint64_t* part_keys, int32_t n_parts, void* stream);
+                    uint64_t* part_keys, int32_t n_parts, const int32_t* th_init, void* stream);
+/* th_out[q] = D of keys[q][k-1] + 1 (INT32_MAX when that slot is padding): the strict
+ * threshold a second scan may start from. */
+int snvrag_knn_threshold(const uint64_t* keys, int32_t nq, int k, int32_t* th_out, void* stream);
 /* Merge n_lists sorted lists per query into the global top-k (exact (D, idx) order). */
 size_t snvrag_topk_merge_ws_bytes(int32_t n_lists, int32_t nq, int k);
 int snvrag_topk_merge(const uint64_t* keys, int32_t n_lists, int32_t nq, int k,

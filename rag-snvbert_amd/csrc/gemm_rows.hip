@@ -303,7 +303,10 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[j][e] = fmaf(r2, t[e], v[j][e]);
         }
-        if (epi.act) {
+        if (epi.act == SNVRAG_ACT_LRELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[j][e] = v[j][e] >= 0.f ? v[j][e] : v[j][e] * epi.slope;
+        } else if (epi.act) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.act, v[j][e], epi.slope);
         }
@@ -334,7 +337,11 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
           load8(colv + 4 * BN + c, g);
           load8(colv + 5 * BN + c, bb);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.ln_act, (v[j][e] - mean) * rstd * g[e] + bb[e], 0.f);
+          for (int e = 0; e < 8; ++e) v[j][e] = (v[j][e] - mean) * rstd * g[e] + bb[e];
+          if (epi.ln_act) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.ln_act, v[j][e], 0.f);
+          }
           if (epi.post_base && mv) {
             load8(reinterpret_cast<const TO*>(epi.post_base) + (long)m * epi.ld_post + n0 + c, g);
 #pragma unroll

@@ -44,7 +44,47 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long arow = Aq ? ((aq_period > 0 ? q % aq_period : q) * (long)L) : 0;
   float cacc = 0.f;
-  for (int l = wave; l < L; l += 4) {
+  // Without AF terms u = W[t]: every squared distance depends on (token, panel token)
+  // only, so the block tabulates them once (same lane order and wave_sum as the
+  // per-position loop, hence identical values) for tokens < 8 and looks them up.
+  __shared__ float tab[8][6];                     // [t][tok0, tok1, sos, eos, pad, mask]
+  const bool fast = !Aq && !Ar;
+  if (fast) {
+    for (int e = wave; e < 48; e += 4) {
+      const int t = e / 6, c = e % 6;
+      const int rt = c == 0 ? tok0 : c == 1 ? tok1 : c == 2 ? 2 : c == 3 ? 3 : c == 4 ? 0 : mask_tok;
+      float acc = 0.f;
+      if (t < 7)
+        for (int d = lane; d < D; d += 64) {
+          const float a = W[(long)t * D + d] - W[(long)rt * D + d];
+          acc = fmaf(a, a, acc);
+        }
+      acc = wave_sum(acc);
+      if (lane == 0) tab[t][c] = acc;
+    }
+    __syncthreads();
+  }
+  bool done = false;
+  if (fast) {
+    // one position per thread; a token >= 7 anywhere sends the query to the general loop
+    float cpart = 0.f;
+    int odd = 0;
+    for (int l = tid; l < L; l += 256) {
+      const int t = (int)tok_q[(long)q * L + l];
+      if (t >= 7 || t < 0) { odd = 1; continue; }
+      const bool is_site = l >= 1 && l <= n_sites;
+      const bool varying = is_site && !site_mask[l - 1];
+      const int c = l == 0 ? 2 : is_site ? 5 : l == n_sites + 1 ? 3 : 4;
+      if (is_site) sdelta[l - 1] = varying ? (tab[t][1] - tab[t][0]) : 0.f;
+      cpart += varying ? tab[t][0] : tab[t][c];
+    }
+    done = !__syncthreads_or(odd);
+    if (done) {
+      cpart = wave_sum(cpart);
+      if (lane == 0) cacc = cpart;
+    }
+  }
+  for (int l = wave; l < L && !done; l += 4) {
     const int t = (int)tok_q[(long)q * L + l];
     const bool is_site = l >= 1 && l <= n_sites;
     const bool varying = is_site && !site_mask[l - 1];
@@ -164,7 +204,8 @@ __device__ __forceinline__ void compact_row(uint64_t* buf, int row, int cnt, int
 template <int KSMAX, int LIMBS>
 __global__ __launch_bounds__(256) void scan_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
                                                    int KS, const int8_t* __restrict__ lut, int nq, int k,
-                                                   long range, long ref_offset, uint64_t* __restrict__ parts) {
+                                                   long range, long ref_offset, uint64_t* __restrict__ parts,
+                                                   const int* __restrict__ th_init) {
   __shared__ __attribute__((aligned(16))) uint64_t sbuf[4][16 * SCAN_CAP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -189,7 +230,11 @@ __global__ __launch_bounds__(256) void scan_kernel(const uint8_t* __restrict__ c
 
   int th[4], cnt[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { th[i] = INT_MAX; cnt[i] = 0; }
+  for (int i = 0; i < 4; ++i) {
+    const int q = qt * 16 + 4 * lg + i;
+    th[i] = (th_init && q < nq) ? th_init[q] : INT_MAX;
+    cnt[i] = 0;
+  }
 
   for (long r0 = r_begin; r0 < r_end; r0 += 16) {
     const long r = r0 + li;
@@ -389,9 +434,203 @@ __global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long
   }
 }
 
+// ------------------------------------------------------------ scan v2 ---
+// One workgroup = 8 waves = 8 query tiles (128 queries) over one contiguous panel
+// range.  The panel codes stream HBM -> LDS ONCE per workgroup (global_load_lds,
+// 1 KiB per wave instruction, 3-stage ring of 32 haplotypes with counted vmcnt)
+// and every wave reads them from LDS for its own query tile, whose LUT limbs stay
+// in VGPRs for the whole scan — the v1 kernel instead had each wave fetch the
+// codes itself (8x the L2->CU traffic).  Rows are n_sites_pad bytes (multiple of
+// 256); the 16-B chunk c of row r sits at c ^ (r & 15) so the 16 rows of a
+// ds_read_b128 B fragment hit 16 different bank groups.
+constexpr int S2_R = 32;                  // haplotypes per LDS stage
+constexpr int S2_CAP = 64;                // candidate slots per query (k <= 32 plus 16+ of slack)
+constexpr int S2_TH = S2_CAP - 16;  // compact when more than 48 held
+
+__device__ __forceinline__ void compact_row2(uint64_t* buf, int row, int cnt, int k, int lane, int& new_cnt,
+                                             int& new_th) {
+  uint64_t key = lane < cnt ? buf[row * S2_CAP + lane] : KEY_MAX;
+  key = wave_sort64(key, lane);
+  if (lane < k) buf[row * S2_CAP + lane] = key;
+  new_cnt = cnt < k ? cnt : k;
+  const uint64_t kth = shfl64(key, k - 1);
+  new_th = (cnt >= k) ? (int)(kth >> 32) - KEY_BIAS : INT_MAX;
+}
+
+template <int KS, int LIMBS, int MODE = 0>   // MODE (diagnostics only): 1 = loads only, 2 = compute only
+__global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
+                                                    const int8_t* __restrict__ lut, int nq, int k, long range,
+                                                    long ref_offset, uint64_t* __restrict__ parts,
+                                                    const int* __restrict__ th_init) {
+  constexpr int ROWB = KS * 64;                        // staged row bytes
+  constexpr int STAGE = S2_R * ROWB;
+  constexpr int PPW = STAGE / 1024 / 8;                // glds pieces per wave per stage
+  constexpr int NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;  // ring depth within 96 KiB
+  static_assert(NST >= 2, "stage too large");
+  static_assert(ROWB % 256 == 0 && PPW >= 1, "rows must be multiples of 256 B");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + NST * STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int nqt = (nq + 15) >> 4;
+  const int qt = blockIdx.y * 8 + wave;
+  const bool active = qt < nqt;                         // wave-uniform; every wave still loads + syncs
+  uint64_t* buf = cand + wave * 16 * S2_CAP;
+  const int part = blockIdx.x;
+  const long r_begin = (long)part * range;
+  const long r_end = min(n_ref, r_begin + range);
+  const int nstage = r_end > r_begin ? (int)((r_end - r_begin + S2_R - 1) / S2_R) : 0;
+
+  // LUT limbs: unconditional loads (inactive waves read the last tile) retired BEFORE the
+  // loop — a load still pending inside it would make hipcc wait vmcnt(0), draining the ring
+  const int qtc = active ? qt : nqt - 1;
+  i32x4 a[LIMBS][KS];
+#pragma unroll
+  for (int lb = 0; lb < LIMBS; ++lb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      a[lb][ks] = *reinterpret_cast<const i32x4*>(lut + ((((long)qtc * LIMBS + lb) * KS + ks) * 64 + lane) * 16);
+#pragma unroll
+  for (int lb = 0; lb < LIMBS; ++lb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(a[lb][ks]));
+
+  auto issue = [&](int st, long r0) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int piece = wave * PPW + j;
+      const int byte = piece * 1024 + lane * 16;
+      const int row = byte / ROWB, ch = (byte % ROWB) >> 4;
+      long r = r0 + row;
+      r = r < r_end ? r : r_end - 1;
+      const int src_ch = ch ^ (row & 15);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(codes + r * ld + src_ch * 16),
+                                       (__attribute__((address_space(3))) void*)(smem + st * STAGE + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  int th[4], cnt[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = qtc * 16 + 4 * lg + i;
+    th[i] = (th_init && q < nq) ? th_init[q] : INT_MAX;
+    cnt[i] = 0;
+  }
+  asm volatile("" ::"v"(th[0]), "v"(th[1]), "v"(th[2]), "v"(th[3]));   // retire before the ring starts
+
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (j < nstage) issue(j, r_begin + (long)j * S2_R);
+  for (int it = 0; it < nstage; ++it) {
+    // retire stage it; up to NST-2 younger stages stay in flight across the barrier
+    if (NST == 3 && it + 1 < nstage) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (MODE != 2 && it + NST - 1 < nstage) issue((it + NST - 1) % NST, r_begin + (long)(it + NST - 1) * S2_R);
+    if (!active || MODE == 1) continue;
+    const char* st = smem + (it % NST) * STAGE;
+    const long r0 = r_begin + (long)it * S2_R;
+    // B fragments (16 haplotypes x 64 sites) of both 16-row groups as one stream,
+    // read PF ahead of their MFMAs so LDS latency hides under the MFMA chain
+    constexpr int RG = S2_R / 16, F = RG * KS, PF = 4;
+    auto bfrag = [&](int f) {
+      const int row = 16 * (f / KS) + li, ks = f % KS;
+      return *reinterpret_cast<const i32x4*>(st + row * ROWB + (((4 * ks + lg) ^ (row & 15)) << 4));
+    };
+    i32x4 bq[PF];
+#pragma unroll
+    for (int f = 0; f < PF; ++f) bq[f] = bfrag(f);
+    i32x4 acc[RG][LIMBS];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+      for (int lb = 0; lb < LIMBS; ++lb) acc[rg][lb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const i32x4 b = bq[f % PF];
+      if (f + PF < F) bq[f % PF] = bfrag(f + PF);
+#pragma unroll
+      for (int lb = 0; lb < LIMBS; ++lb)
+        acc[f / KS][lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[lb][f % KS], b, acc[f / KS][lb], 0, 0, 0);
+    }
+    // pin the interleave (hipcc otherwise sinks each read to just before its MFMA):
+    // PF reads, then per fragment {1 read, LIMBS MFMAs}
+    __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      if (f + PF < F) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, LIMBS, 0);
+    }
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+      const long r = r0 + 16 * rg + li;
+      const bool rv = r < r_end;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = LIMBS == 2 ? acc[rg][0][i] * 128 + acc[rg][1][i] : acc[rg][0][i];
+        const bool pass = rv && d < th[i];
+        const uint64_t m = __ballot(pass);
+        if (m) {
+          const uint32_t gb = (uint32_t)(m >> (16 * lg)) & 0xFFFFu;
+          if (pass) {
+            const int pre = __popc(gb & ((1u << li) - 1u));
+            buf[(4 * lg + i) * S2_CAP + cnt[i] + pre] = make_key(d, (uint32_t)(r + ref_offset));
+          }
+          cnt[i] += __popc(gb);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint64_t need = __ballot(cnt[i] > S2_TH);
+        while (need) {
+          const int src = __builtin_ctzll(need);
+          const int g = src >> 4;
+          need &= ~(0xFFFFull << (16 * g));
+          int nc, nt;
+          compact_row2(buf, 4 * g + i, __shfl(cnt[i], src, 64), k, lane, nc, nt);
+          if (lg == g) { cnt[i] = nc; th[i] = nt; }
+        }
+      }
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * g + i;
+      const int c = __shfl(cnt[i], 16 * g, 64);
+      int nc, nt;
+      compact_row2(buf, row, c, k, lane, nc, nt);
+      const int q = qt * 16 + row;
+      if (q < nq && lane < k)
+        parts[((long)part * nq + q) * k + lane] = lane < nc ? buf[row * S2_CAP + lane] : KEY_MAX;
+    }
+  }
+}
+
+template <int KS, int LB>
+static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* codes, long n_ref, long ld,
+                         const int8_t* lut, int k, long range, long off, uint64_t* parts, const int* th) {
+  constexpr size_t STAGE = (size_t)S2_R * KS * 64;
+  constexpr size_t NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;
+  const size_t lds = NST * STAGE + 8 * 16 * S2_CAP * sizeof(uint64_t);
+  auto kern = scan2_kernel<KS, LB, 0>;
+  if constexpr (KS == 16 && LB == 2) {
+    const char* m = getenv("SNVRAG_SCAN_MODE");
+    if (m && m[0] == '1') kern = scan2_kernel<KS, LB, 1>;
+    if (m && m[0] == '2') kern = scan2_kernel<KS, LB, 2>;
+  }
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 g((unsigned)n_parts, (unsigned)(((nq + 15) / 16 + 7) / 8));
+  hipLaunchKernelGGL(kern, g, dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th);
+}
+
 static int scan_parts(long n_ref) {
-  // ~2048 refs per range, at least 16, at most 4096 parts
+  // ~2048 refs per range at least; large panels get a multiple of 256 ranges (one
+  // workgroup per CU per round, no tail round)
   long p = (n_ref + 2047) / 2048;
+  if (p >= 256) p = 256 * ((n_ref + 256L * 8192 - 1) / (256L * 8192));
   if (p < 1) p = 1;
   if (p > 4096) p = 4096;
   return (int)p;
@@ -399,8 +638,9 @@ static int scan_parts(long n_ref) {
 
 template <int KSM, int LB>
 static void launch_scan(dim3 g, hipStream_t s, const uint8_t* codes, long n_ref, long ld, int KS,
-                        const int8_t* lut, int nq, int k, long range, long off, uint64_t* parts) {
-  hipLaunchKernelGGL((scan_kernel<KSM, LB>), g, dim3(256), 0, s, codes, n_ref, ld, KS, lut, nq, k, range, off, parts);
+                        const int8_t* lut, int nq, int k, long range, long off, uint64_t* parts, const int* th) {
+  hipLaunchKernelGGL((scan_kernel<KSM, LB>), g, dim3(256), 0, s, codes, n_ref, ld, KS, lut, nq, k, range, off, parts,
+                     th);
 }
 
 }  // namespace snvrag
@@ -418,7 +658,7 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
   SNV_CHECK_ARG(tok_q && W && site_mask && lut_out && exp_out, "null pointer");
   SNV_CHECK_ARG(limbs == 1 || limbs == 2, "limbs must be 1 or 2");
   SNV_CHECK_ARG(n_sites_pad % 64 == 0 && n_sites_pad >= n_sites && n_sites + 2 <= L, "site padding");
-  SNV_CHECK_ARG(n_sites_pad <= 17 * 64, "window longer than 1088 sites");
+  SNV_CHECK_ARG(n_sites_pad <= 20 * 64, "window longer than 1280 sites");
   if (nq == 0) return 0;
   hipStream_t s = as_stream(stream);
   const size_t sh = (size_t)(n_sites_pad + 4) * sizeof(float);
@@ -433,15 +673,32 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
   return 0;
 }
 
+__global__ void threshold_kernel(const uint64_t* __restrict__ keys, int nq, int k, int* __restrict__ th) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const uint64_t key = keys[(long)q * k + k - 1];
+  th[q] = key == KEY_MAX ? INT_MAX : (int)(key >> 32) - KEY_BIAS + 1;
+}
+
+extern "C" int snvrag_knn_threshold(const uint64_t* keys, int32_t nq, int k, int32_t* th_out, void* stream) {
+  SNV_CHECK_ARG(keys && th_out && k >= 1, "bad arguments");
+  if (nq == 0) return 0;
+  hipLaunchKernelGGL(threshold_kernel, dim3((nq + 255) / 256), dim3(256), 0, as_stream(stream), keys, (int)nq, k,
+                     (int*)th_out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq) { (void)nq; return scan_parts(n_ref); }
 
 extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_codes, int32_t n_sites_pad,
                                const void* lut, int32_t nq, int limbs, int k, int64_t ref_offset,
-                               uint64_t* part_keys, int32_t n_parts, void* stream) {
+                               uint64_t* part_keys, int32_t n_parts, const int32_t* th_init, void* stream) {
   SNV_CHECK_ARG(codes && lut && part_keys, "null pointer");
   SNV_CHECK_ARG(k >= 1 && k <= 32, "k must be in [1, 32]");
   SNV_CHECK_ARG(limbs == 1 || limbs == 2, "limbs");
-  SNV_CHECK_ARG(n_sites_pad % 64 == 0 && n_sites_pad <= 17 * 64 && ld_codes >= n_sites_pad, "site padding");
+  SNV_CHECK_ARG(n_sites_pad % 64 == 0 && ld_codes >= n_sites_pad &&
+                    n_sites_pad <= (n_sites_pad % 256 == 0 ? 20 * 64 : 17 * 64), "site padding");
   SNV_CHECK_ARG(ld_codes % 16 == 0 && ((uintptr_t)codes % 16) == 0, "codes must be 16-byte aligned rows");
   SNV_CHECK_ARG(n_parts >= 1, "n_parts");
   SNV_CHECK_ARG(n_ref + ref_offset < (1LL << 32), "panel index must fit 32 bits");
@@ -454,16 +711,27 @@ extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_c
   hipStream_t s = as_stream(stream);
   const int8_t* L8 = (const int8_t*)lut;
   evlog_begin(s);
+  const bool v2 = n_sites_pad % 256 == 0 && n_sites_pad <= 1280 && !getenv("SNVRAG_SCAN_V1");
+  if (v2) {
+#define SCAN2(K_)                                                                                          \
+  case K_:                                                                                                 \
+    if (limbs == 2) launch_scan2<K_, 2>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init); \
+    else launch_scan2<K_, 1>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init);          \
+    break;
+    switch (KS) { SCAN2(4) SCAN2(8) SCAN2(12) SCAN2(16) SCAN2(20) }
+#undef SCAN2
+  } else {
 #define SCAN(KSM)                                                                                   \
   do {                                                                                              \
-    if (limbs == 2) launch_scan<KSM, 2>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys); \
-    else launch_scan<KSM, 1>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys);           \
+    if (limbs == 2) launch_scan<KSM, 2>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys, th_init); \
+    else launch_scan<KSM, 1>(g, s, codes, n_ref, ld_codes, KS, L8, nq, k, range, ref_offset, part_keys, th_init);           \
   } while (0)
   if (KS <= 4) SCAN(4);
   else if (KS <= 8) SCAN(8);
   else if (KS <= 16) SCAN(16);
   else SCAN(17);
 #undef SCAN
+  }
   SNV_LAUNCH_CHECK();
   // algorithmic bytes: every code byte of the window once + LUT + partial lists
   evlog_end(s, EV_KNN_SCAN, (double)n_ref * n_sites_pad + (double)nq * n_sites_pad * limbs +

@@ -219,14 +219,24 @@ def knn_lut(tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, n_sit
 
 
 def knn_scan(codes: torch.Tensor, n_sites_pad: int, lut: torch.Tensor, nq: int, limbs: int, k: int,
-             ref_offset: int = 0, n_parts: Optional[int] = None) -> torch.Tensor:
+             ref_offset: int = 0, n_parts: Optional[int] = None, th_init: Optional[torch.Tensor] = None) -> torch.Tensor:
     n_ref, ld = codes.shape
     if n_parts is None:
         n_parts = N.lib().snvrag_knn_scan_parts(n_ref, nq)
     parts = torch.empty(n_parts, nq, k, device=codes.device, dtype=torch.int64)
+    if th_init is not None:
+        assert th_init.dtype == torch.int32 and th_init.numel() == nq
     check(N.lib().snvrag_knn_scan(ptr(_c(codes)), n_ref, ld, n_sites_pad, ptr(lut), nq, limbs, k, ref_offset,
-                                  ptr(parts), n_parts, stream_ptr()), "knn_scan")
+                                  ptr(parts), n_parts, ptr(th_init), stream_ptr()), "knn_scan")
     return parts
+
+
+def knn_threshold(keys: torch.Tensor, k: int) -> torch.Tensor:
+    """Per-query strict start threshold (int32 [nq]) from merged keys [nq, k]."""
+    nq = keys.shape[0]
+    th = torch.empty(nq, device=keys.device, dtype=torch.int32)
+    check(N.lib().snvrag_knn_threshold(ptr(_c(keys)), nq, k, ptr(th), stream_ptr()), "knn_threshold")
+    return th
 
 
 def topk_merge(keys: torch.Tensor, k: int) -> torch.Tensor:
@@ -263,7 +273,7 @@ def rag_mean(idx: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tens
 
 def panel_synth(n_ref: int, n_sites: int, af: torch.Tensor, seed: int, ld: Optional[int] = None) -> torch.Tensor:
     N.require_gpu(af)
-    ld = ld or ((n_sites + 63) // 64) * 64
+    ld = ld or max(256, ((n_sites + 255) // 256) * 256)
     codes = torch.empty(n_ref, ld, device=af.device, dtype=torch.uint8)
     check(N.lib().snvrag_panel_synth(ptr(codes), n_ref, ld, n_sites, ptr(_c(af)), seed, stream_ptr()),
           "panel_synth")

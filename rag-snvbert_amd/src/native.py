@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -89,7 +89,8 @@ _SIGS = {
     "snvrag_knn_lut": ([i64, i64, i64, vp, vp, vp, i64, vp, vp, i32, i32, C.c_int, C.c_int, C.c_int,
                         C.c_int, vp, vp, vp, vp], C.c_int),
     "snvrag_knn_scan_parts": ([i64, i32], C.c_int),
-    "snvrag_knn_scan": ([vp, i64, i64, i32, vp, i32, C.c_int, C.c_int, i64, vp, i32, vp], C.c_int),
+    "snvrag_knn_scan": ([vp, i64, i64, i32, vp, i32, C.c_int, C.c_int, i64, vp, i32, vp, vp], C.c_int),
+    "snvrag_knn_threshold": ([vp, i32, C.c_int, vp, vp], C.c_int),
     "snvrag_topk_merge_ws_bytes": ([i32, i32, C.c_int], sz),
     "snvrag_topk_merge": ([vp, i32, i32, C.c_int, vp, vp, sz, vp], C.c_int),
     "snvrag_knn_decode": ([vp, i32, C.c_int, vp, vp, vp, vp, vp], C.c_int),

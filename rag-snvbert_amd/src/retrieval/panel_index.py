@@ -20,7 +20,8 @@ from .. import kernels as K
 
 
 def pad_sites(n_sites: int) -> int:
-    return max(64, ((n_sites + 63) // 64) * 64)
+    """Index row length: a multiple of 256 B so the scan's 16-row LDS swizzle stays inside a row."""
+    return max(256, ((n_sites + 255) // 256) * 256)
 
 
 class PanelIndex:
@@ -69,9 +70,25 @@ class PanelIndex:
         return K.knn_lut(tok_q.long().contiguous(), W, site_mask, self.n_sites, self.n_sites_pad, limbs,
                          Aq, aq_period, Ar)
 
-    def scan_keys(self, lut: torch.Tensor, nq: int, limbs: int, k: int) -> torch.Tensor:
-        """Exact local top-k keys [nq, k] (uint64 in int64 storage) with global indices."""
-        parts = K.knn_scan(self.codes, self.n_sites_pad, lut, nq, limbs, k, self.ref_offset)
+    SAMPLE_MIN = 1 << 17       # panels at least this large get a threshold pre-pass
+
+    def scan_keys(self, lut: torch.Tensor, nq: int, limbs: int, k: int, presample: Optional[bool] = None) -> torch.Tensor:
+        """Exact local top-k keys [nq, k] (uint64 in int64 storage) with global indices.
+
+        Large panels first scan a 1/32 prefix of the panel: its k-th best distance is an
+        upper bound on the panel's, so the full scan can start from it (strictly above it
+        nothing can enter the top-k) and keeps far fewer candidates; the result is the
+        same exact top-k."""
+        n_ref = self.codes.shape[0]
+        if presample is None:
+            presample = n_ref >= self.SAMPLE_MIN
+        th = None
+        if presample:
+            m = max(16 * k, ((n_ref // 32) + 15) // 16 * 16)
+            sample = K.knn_scan(self.codes[:m], self.n_sites_pad, lut, nq, limbs, k, self.ref_offset,
+                                n_parts=max(1, min(256, m // 128)))
+            th = K.knn_threshold(K.topk_merge(sample, k), k)
+        parts = K.knn_scan(self.codes, self.n_sites_pad, lut, nq, limbs, k, self.ref_offset, th_init=th)
         return K.topk_merge(parts, k)
 
     def search(self, tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: int = 2,

@@ -179,6 +179,24 @@ def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
     np.testing.assert_array_equal(kk[valid], knn_np.pack_key(od, oi)[valid])
 
 
+@pytest.mark.parametrize("tie", [False, True])
+def test_knn_presample_threshold_is_exact(tie):
+    """Threshold pre-pass over a panel prefix, then the full scan from that threshold:
+    keys identical to the plain scan and to the oracle (also with massive distance ties)."""
+    from src.retrieval import PanelIndex
+    n_ref, n_sites, nq, k = 40000, 300, 40, 32
+    W, panel, site_mask, tok = _rand_case(n_ref, n_sites, nq, 77, tie)
+    idx_t = PanelIndex.from_alleles(panel, np.zeros(1030, np.float32), DEV)
+    Wt, smask = torch.from_numpy(W).to(DEV), torch.from_numpy(site_mask).to(DEV)
+    lut, _, _ = idx_t.lut(torch.from_numpy(tok).to(DEV), Wt, smask, 2)
+    plain = idx_t.scan_keys(lut, nq, 2, k, presample=False)
+    pre = idx_t.scan_keys(lut, nq, 2, k, presample=True)
+    torch.testing.assert_close(pre, plain, rtol=0, atol=0)
+    dq = decode_lut(lut, nq, idx_t.n_sites_pad, 2)[:, :n_sites]
+    oi, od = knn_np.knn(panel, dq, k)
+    np.testing.assert_array_equal(pre.cpu().numpy().view(np.uint64), knn_np.pack_key(od, oi))
+
+
 def test_knn_shard_offsets_and_merge():
     """Panel split in 3 contiguous shards with global offsets + merge == unsplit search."""
     from src.retrieval import PanelIndex

@@ -48,6 +48,11 @@ def main():
         "oproj N384 K384 plain": (lambda: K.linear(x, w[(D, D)], bias[D]), M, D, D, 0),
         "ffn1 N1536 K384 +lrelu+stats": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D], act=N.ACT_LRELU, slope=0.1,
                                                           stats_out=stats), M, 4 * D, D, 0),
+        "ffn1 N1536 K384 +lrelu": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D], act=N.ACT_LRELU, slope=0.1),
+                                   M, 4 * D, D, 0),
+        "ffn1 N1536 K384 +stats": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D], stats_out=stats), M, 4 * D, D, 0),
+        "oproj N384 K384 +resid": (lambda: K.linear(x, w[(D, D)], bias[D], resid=x), M, D, D, 1),
+        "oproj N384 K384 +LN": (lambda: K.linear(x, w[(D, D)], bias[D], ln=(lg, lb)), M, D, D, 0),
         "ffn1 N1536 K384 plain": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D]), M, 4 * D, D, 0),
         "ffn2 N384 K1536 +rownorm+resid+LN": (lambda: K.linear(h, w[(D, 4 * D)], bias[D], act=N.ACT_LRELU, slope=0.1,
                                                                resid=x, ln=(lg, lb),
@@ -55,12 +60,12 @@ def main():
                                               M, D, 4 * D, 1),
         "ffn2 N384 K1536 plain": (lambda: K.linear(h, w[(D, 4 * D)], bias[D]), M, D, 4 * D, 0),
     }
-    variants = [("deep", {}), ("shallow", {"SNVRAG_GEMM_SHALLOW": "1"}), ("tile128", {"SNVRAG_GEMM_TILE128": "1"})]
+    variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
     for name, (fn, m, n, k, extra) in cases.items():
         flop = 2.0 * m * n * k
         byts = 2.0 * (m * k + n * k + m * n * (1 + extra))
         for vn, env in variants:
-            for kk in ("SNVRAG_GEMM_SHALLOW", "SNVRAG_GEMM_TILE128"):
+            for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
                 os.environ.pop(kk, None)
             os.environ.update(env)
             try:
@@ -69,8 +74,10 @@ def main():
                 print(f"{name:36s} {vn:8s} n/a ({str(e)[:60]})", flush=True)
                 continue
             print(f"{name:36s} {vn:8s} {ms:8.3f} ms {flop / ms / 1e9:8.1f} TF/s {byts / ms / 1e6:8.1f} GB/s", flush=True)
-        for kk in ("SNVRAG_GEMM_SHALLOW", "SNVRAG_GEMM_TILE128"):
+        for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
             os.environ.pop(kk, None)
+        if not os.environ.get("GM_TORCH"):
+            continue
         a = h if k == 4 * D else x
         ww = w[(n, k)]
         ms = timeit(lambda: torch.matmul(a, ww.t()))

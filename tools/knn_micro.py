@@ -1,0 +1,73 @@
+"""kNN scan micro-benchmark at the bench shape (1M haplotypes x 1024 sites, 128 queries).
+
+Times knn_scan alone for several k and both scan kernels, to separate the code-streaming
+cost from the top-k maintenance cost.  Prints ms and GB/s of compulsory code bytes.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
+from src import kernels as K  # noqa: E402
+from src.retrieval import PanelIndex  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    n_ref = int(os.environ.get("KM_N", 1 << 20))
+    S, nq, L = 1024, 128, 1030
+    dev = "cuda"
+    rng = np.random.default_rng(0)
+    af = torch.from_numpy(rng.beta(0.3, 3.0, S).astype(np.float32)).to(dev)
+    index = PanelIndex.synthetic(n_ref, S, af, torch.zeros(L, device=dev), 7)
+    W = torch.randn(12, 384, device=dev)
+    mask = (rng.random(S) < 0.6).astype(np.uint8)
+    alle = (rng.random((nq, S)) < af.cpu().numpy()[None]).astype(np.int64)
+    tok = np.zeros((nq, L), np.int64)
+    tok[:, 0], tok[:, S + 1] = 2, 3
+    tok[:, 1:S + 1] = np.where(mask[None] == 1, 4, 5 + alle)
+    tok = torch.from_numpy(tok).to(dev)
+    smask = torch.from_numpy(mask).to(dev)
+    lut, exps, consts = index.lut(tok, W, smask, 2)
+    byts = n_ref * index.n_sites_pad
+    for ver in ("v2", "v1"):
+        if ver == "v1":
+            os.environ["SNVRAG_SCAN_V1"] = "1"
+        else:
+            os.environ.pop("SNVRAG_SCAN_V1", None)
+        for k in (1, 8, 32):
+            ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, k, 0))
+            print(f"scan {ver} k={k:2d}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
+    os.environ.pop("SNVRAG_SCAN_V1", None)
+    for mode, name in (("1", "loads only"), ("2", "compute only")):
+        os.environ["SNVRAG_SCAN_MODE"] = mode
+        ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 1, 0))
+        print(f"scan v2 k=1 {name}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
+    os.environ.pop("SNVRAG_SCAN_MODE", None)
+    ms = timeit(lambda: index.lut(tok, W, smask, 2))
+    print(f"lut: {ms:7.3f} ms", flush=True)
+    parts = K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 32, 0)
+    ms = timeit(lambda: K.topk_merge(parts, 32))
+    print(f"merge of {parts.shape[0]} parts k=32: {ms:7.3f} ms", flush=True)
+    for pre in (False, True):
+        ms = timeit(lambda: index.scan_keys(lut, nq, 2, 32, presample=pre))
+        print(f"scan_keys k=32 presample={pre}: {ms:7.3f} ms", flush=True)
+    ms = timeit(lambda: index.search(tok, W, smask, 32))
+    print(f"search k=32 (lut+scan+merge+decode): {ms:7.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
