@@ -168,18 +168,23 @@ def main():
                     work_per_launch=float(work[sel].mean()), total_ms_per_step=float(ms[sel].sum()) / args.steps,
                     rate=float(work[sel].sum() / (ms[sel].sum() * 1e-3)))
 
-    gemm, attn, ln, scan = agg(1), agg(2), agg(3), agg(4)
+    gemm, attn, ln, scan, ffn = agg(1), agg(2), agg(3), agg(4), agg(8)
     ms_step = elapsed / args.steps * 1e3
     value = masked_per_step * world * args.steps / elapsed
     knn_qps = 2 * B * world * args.steps / elapsed
     if rank != 0:
         return
     peak_f = BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_PEAK_TFLOPS
-    roofline = dict(bound="mfma", kernel="linear_kernel (all encoder/head GEMMs)",
-                    achieved=round(gemm["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",
-                    frac=round(gemm["rate"] / 1e12 / peak_f, 4), traffic=None,
-                    avg_launch_ms=round(gemm["avg_ms"], 4),
-                    algorithmic_per_launch=f"{gemm['work_per_launch']:.4g} FLOP (2*M*N*K averaged over launches)")
+    # roofline object = the MFMA kernel class with the most time per step
+    mf = [("rows_gemm_kernel (encoder QKV/out-proj + fusion/head GEMMs)", gemm, "2*M*N*K averaged over launches"),
+          ("ffn_kernel (fused FFN sublayer, 12 launches)", ffn, "2*M*D*8D = 16*M*D^2 per launch"),
+          ("attn32_bf16 (attention)", attn, "4*L^2*dh*H*nseq per launch")]
+    name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
+    roofline = dict(bound="mfma", kernel=name,
+                    achieved=round(dom["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",
+                    frac=round(dom["rate"] / 1e12 / peak_f, 4), traffic=None,
+                    avg_launch_ms=round(dom["avg_ms"], 4),
+                    algorithmic_per_launch=f"{dom['work_per_launch']:.4g} FLOP ({per})")
     extra = {
         "kernels": {
             "attention": dict(achieved_tflops=round(attn["rate"] / 1e12, 2), frac=round(attn["rate"] / 1e12 / peak_f, 4),
@@ -187,7 +192,11 @@ def main():
             "knn_scan": dict(bound="hbm", achieved_gbs=round(scan["rate"] / 1e9, 1), peak=HBM_PEAK_GBS,
                              frac=round(scan["rate"] / 1e9 / HBM_PEAK_GBS, 4), avg_launch_ms=round(scan["avg_ms"], 4),
                              bytes_per_launch=scan["work_per_launch"]),
-            "gemm": dict(ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
+            "gemm": dict(achieved_tflops=round(gemm["rate"] / 1e12, 2), frac=round(gemm["rate"] / 1e12 / peak_f, 4),
+                         ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
+            "ffn_fused": (dict(achieved_tflops=round(ffn["rate"] / 1e12, 2), frac=round(ffn["rate"] / 1e12 / peak_f, 4),
+                               ms_per_step=round(ffn["total_ms_per_step"], 3), avg_launch_ms=round(ffn["avg_ms"], 4))
+                          if ffn else None),
             "layernorm": (dict(ms_per_step=round(ln["total_ms_per_step"], 3), achieved_gbs=round(ln["rate"] / 1e9, 1))
                           if ln else "fused into GEMM epilogues/prologues"),
         },

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 5
+#define SNVRAG_ABI_VERSION 6
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -238,7 +238,29 @@ typedef struct {
   /* factor already folded into the q rows of w_qkv / b_qkv (0 = none); the bf16 engine
    * folds log2(e)/sqrt(dh) so attention's exp2 needs no per-score scaling */
   float q_scale;
+  /* optional (bf16, D in {128,256,384}): fused FFN weight stream from snvrag_ffn_pack
+   * and its vector table (see snvrag_ffn_forward); NULL = unfused GEMM path */
+  const void* ffn_w; const float* ffn_v;
 } snvrag_layer_t;
+
+/* ------------------------------------------------------------------------
+ * Fused FFN sublayer (model/utils/feed_forward.py:18-21 + the output
+ * SublayerConnection, model/transformer.py:34, sublayer.py:15-16), bf16, eval:
+ *   out = LN2(x1 + lrelu(LN_f(lrelu(x1 W1^T + b1)) W2^T + b2))
+ * in ONE launch; the [M, 4D] hidden never reaches HBM.  The weights are first
+ * packed (once per model) into a fragment-ordered bf16 stream of
+ * snvrag_ffn_pack_bytes(D) bytes:
+ *   snvrag_ffn_pack(D, w1 [4D,D], w2g [D,4D], out, stream)
+ * with w2g = w2 diag(lnf_g) (the FFN LayerNorm's gamma folded in).  vec is an
+ * f32 table of 8*D floats (16-byte aligned):
+ *   [b1 4D | b2' D | c1 D | ln2_g D | ln2_b D]
+ * with b2' = b2 + w2 lnf_b and c1[n] = sum_k w2g[n,k] (of the bf16 values).
+ * x1 and out are [M, D] bf16 and must not alias.  D in {128, 256, 384}.
+ * ---------------------------------------------------------------------- */
+size_t snvrag_ffn_pack_bytes(int D);
+int snvrag_ffn_pack(int D, const void* w1, const void* w2g, void* out, void* stream);
+int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
+                       const float* vec, float eps, void* stream);
 
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);
 int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,

@@ -89,6 +89,12 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
         e.bias = ly.b_o; e.resid = xc; e.ld_resid = D; e.ln_g = ly.ln1_g; e.ln_b = ly.ln1_b; e.ln_eps = 1e-5f;
         rc = snvrag_linear(dtype, dtype, M, D, D, att, D, ly.w_o, D, x1, D, &e, stream);
         if (rc) return rc;
+        if (dtype == SNVRAG_BF16 && ly.ffn_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN")) {
+          // x = LN2(x1 + FFN(x1)) with the 4D hidden kept in registers (one launch)
+          rc = snvrag_ffn_forward(M, D, x1, xc, ly.ffn_w, ly.ffn_v, 1e-5f, stream);
+          if (rc) return rc;
+          continue;
+        }
         // h = lrelu(x1 W1^T + b1), row stats of h for the FFN LayerNorm (one launch)
         e = snvrag_epilogue_t{};
         e.bias = ly.b1; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.stats_out = (float*)stats;

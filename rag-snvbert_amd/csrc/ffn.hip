@@ -1,0 +1,351 @@
+// Fused FFN sublayer as ONE kernel (bf16, eval):
+//
+//   h   = lrelu(x1 W1^T + b1)                           feed_forward.py:20 (w_1, LeakyReLU 0.1)
+//   out = LN2(x1 + lrelu(LN_f(h) W2^T + b2))            feed_forward.py:20-21, sublayer.py:15-16
+//
+// The [M, 4D] hidden never reaches HBM.  A workgroup owns 128 token rows (4 waves
+// x 32 rows, one wave per SIMD).  Each wave's x1 rows sit in LDS in MFMA B-operand
+// order (96 KiB at D = 384); the weights stream once per workgroup through a
+// 4-slot LDS ring of 16 KiB slabs (LDS-DMA, three slabs in flight across raw
+// barriers).  Every MFMA computes a TRANSPOSED tile (weight rows x token rows), so
+// a lane ends up holding one token row's values:
+//   * phase 1 (W1):  h^T   = W1_c . x1^T       per 64-wide hidden chunk c;
+//   * phase 2 (W2):  out^T += W2'_c . h_c^T     with h_c^T taken straight from the
+//                    phase-1 accumulators (bf16), its k order baked into W2'.
+// The FFN LayerNorm over the 4D hidden is folded: with
+// W2' = W2 diag(g_f), c1 = rowsum(W2') and b2' = b2 + W2 b_f,
+//   LN_f(h) W2^T + b2 = rstd*(h W2'^T) - rstd*mean*c1 + b2',
+// mean/rstd from per-lane running sums of h (f32, before bf16 rounding).
+// W2' rows are permuted so lane (li, lg) holds output columns 32s + 8lg + j (j < 8):
+// residual, LayerNorm and the 16-byte stores work on whole 8-column runs of one
+// row, and the row reductions are two lane shuffles.
+#include "common.h"
+
+namespace snvrag {
+
+constexpr int FF_SLAB = 16384;   // bytes per weight slab = 16 fragment blocks of 1 KiB
+constexpr int FF_NSLOT = 4;      // LDS ring slots
+constexpr int FF_PD = 3;         // slabs in flight (<= NSLOT - 1)
+constexpr int FF_ROWS = 128;     // token rows per workgroup (4 waves x 32)
+
+// vector table (f32) offsets, in units of D: b1[4D] b2' c1 g2 be2
+enum { FV_B1 = 0, FV_B2 = 4, FV_C1 = 5, FV_G2 = 6, FV_BE2 = 7, FV_N = 8 };
+
+// output column held by A-row r (0..15) of 16-row weight tile T (see header comment)
+__host__ __device__ constexpr int ffn_perm(int T, int r) { return 32 * (T >> 1) + 8 * (r >> 2) + 4 * (T & 1) + (r & 3); }
+
+template <int D> struct FfnShape {
+  static constexpr int KS = D / 32;              // 32-wide k steps over D
+  static constexpr int NT = D / 16;              // 16-wide column tiles over D
+  static constexpr int NB = D / 128;             // 128-wide blocks (W1 k blocks / W2 column blocks)
+  static constexpr int NCH = 4 * D / 64;         // 64-wide hidden chunks
+  static constexpr int SPC = 2 * NB;             // slabs per hidden chunk (W1 then W2)
+  static constexpr int NSLAB = NCH * SPC;
+  static constexpr int XT = 4 * 2 * KS * 1024;   // x1 tile bytes in LDS
+  static constexpr int LDS = XT + FF_NSLOT * FF_SLAB;
+};
+
+__device__ __forceinline__ void ff_glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int BPW> __device__ __forceinline__ void ff_wait(int younger) {
+  // wait until at most `younger` slabs (BPW LDS-DMA instructions each) of this wave are in flight
+  switch (younger) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BPW) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * BPW) : "memory"); break;
+  }
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  bf16 x = (bf16)a, y = (bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+// element j (0..7) of a bf16x8 held as u32x4
+__device__ __forceinline__ float bfx(const u32x4& v, int j) { return (j & 1) ? bf_hi(v[j >> 1]) : bf_lo(v[j >> 1]); }
+
+__device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// RT 16-row tiles per wave, NWV waves: RT = 2, NWV = 4 (one wave per SIMD, 512 registers)
+// or RT = 1, NWV = 8 (two waves per SIMD, 256 registers each); 128 rows either way.
+template <int D, int RT, int NWV, int DBG>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV / 4, NWV / 4)))
+void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* __restrict__ out, const char* __restrict__ ws,
+                const float* __restrict__ vec, float eps) {
+  using S = FfnShape<D>;
+  constexpr int KS = S::KS, NT = S::NT, NB = S::NB, NSLAB = S::NSLAB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  constexpr int BPW = 16 / NWV;                    // 1-KiB blocks of a slab loaded per wave
+  static_assert(RT * 16 * NWV == FF_ROWS, "tile rows");
+  const long rbase = (long)blockIdx.x * FF_ROWS + wave * 16 * RT;
+  // this wave's x1 rows, B-operand fragment blocks [rt][s], lane-linear 16 B each
+  char* xt = smem + wave * (RT * KS * 1024);
+  const char* xtl = xt + lane * 16;
+  char* ring = smem + S::XT;
+
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const long r = min(rbase + rt * 16 + li, (long)M - 1);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) ff_glds16(x1 + r * D + 32 * s + 8 * lg, xt + (rt * KS + s) * 1024);
+  }
+
+  // Workgroups start at different hidden chunks (the FFN sums over chunks, so any
+  // order is the same sum): concurrent CUs of an XCD then read different slabs
+  // instead of all hitting the same L2 channels with the same 16 KiB.
+  const int rot = (int)(blockIdx.x % S::NCH);
+  auto issue = [&](int i) {
+    if (DBG != 1 && i < NSLAB) {
+      int cc = i / S::SPC + rot;
+      cc = cc >= S::NCH ? cc - S::NCH : cc;
+      const char* src = ws + ((long)cc * S::SPC + i % S::SPC) * FF_SLAB + wave * BPW * 1024 + lane * 16;
+      char* dst = ring + (i % FF_NSLOT) * FF_SLAB + wave * BPW * 1024;
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) ff_glds16(src + j * 1024, dst + j * 1024);
+    }
+  };
+  // slab i landed for every wave (and, at i = 0, this wave's x1 rows), slab i-1's slot
+  // free; then keep FF_PD slabs in flight
+  auto step = [&](int i) -> const char* {
+    if (DBG != 1) {
+      ff_wait<BPW>(min(FF_PD - 1, NSLAB - 1 - i));
+      __builtin_amdgcn_s_barrier();
+    }
+    issue(i + FF_PD);
+    return ring + (i % FF_NSLOT) * FF_SLAB + lane * 16;
+  };
+#pragma unroll
+  for (int i = 0; i < FF_PD; ++i) issue(i);
+
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float st1[RT], st2[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) st1[rt] = st2[rt] = 0.f;
+  int slab = 0;
+#pragma unroll 1
+  for (int c0 = 0; c0 < S::NCH; ++c0) {
+    const int c = c0 + rot >= S::NCH ? c0 + rot - S::NCH : c0 + rot;
+    float4 bias1[4];                                 // b1 of this chunk's hidden units (L2-resident)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bias1[t] = *reinterpret_cast<const float4*>(vec + FV_B1 * D + c * 64 + 16 * t + 4 * lg);
+    f32x4 h[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) h[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {               // W1 slabs: 4 hidden tiles x 4 k steps
+      const char* sl = step(slab++);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        u32x4 a[4], b[RT];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 4 + s) * 1024);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + kb * 4 + s) * 1024);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            if (DBG == 2) h[rt][t][0] += __builtin_bit_cast(float, a[t][0] ^ b[rt][0]);
+            else h[rt][t] = mfma_bf16(a[t], b[rt], h[rt][t]);
+          }
+      }
+    }
+    // bias + LeakyReLU(0.1) + LN_f running sums; pack h^T as phase-2 B operands
+    u32x4 hf[RT][2];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float hv[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bb[4] = {bias1[t].x, bias1[t].y, bias1[t].z, bias1[t].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = h[rt][t][i] + bb[i];
+          v = v >= 0.f ? v : 0.1f * v;
+          st1[rt] += v;
+          st2[rt] = fmaf(v, v, st2[rt]);
+          hv[t][i] = v;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        hf[rt][s2] = u32x4{pack_bf2(hv[2 * s2][0], hv[2 * s2][1]), pack_bf2(hv[2 * s2][2], hv[2 * s2][3]),
+                           pack_bf2(hv[2 * s2 + 1][0], hv[2 * s2 + 1][1]),
+                           pack_bf2(hv[2 * s2 + 1][2], hv[2 * s2 + 1][3])};
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {               // W2' slabs: 8 column tiles x 2 k steps
+      const char* sl = step(slab++);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 a[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 2 + s2) * 1024);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            if (DBG == 2) acc[rt][nb * 8 + t][0] += __builtin_bit_cast(float, a[t][0] ^ hf[rt][s2][0]);
+            else acc[rt][nb * 8 + t] = mfma_bf16(a[t], hf[rt][s2], acc[rt][nb * 8 + t]);
+          }
+      }
+    }
+  }
+
+  // ---------------- epilogue: out = LN2(x1 + lrelu(rstd*acc - rstd*mean*c1 + b2'))
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float s1 = st1[rt], s2 = st2[rt];
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    const float hm = s1 * (1.0f / (4 * D));
+    const float hr = 1.0f / sqrtf(fmaxf(s2 * (1.0f / (4 * D)) - hm * hm, 0.f) + eps);
+    float sum = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const u32x4 xr = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + s) * 1024);
+      const float* c1 = vec + FV_C1 * D + 32 * s + 8 * lg;
+      const float* b2 = vec + FV_B2 * D + 32 * s + 8 * lg;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float u = hr * acc[rt][2 * s + (j >> 2)][j & 3] - hr * hm * c1[j] + b2[j];
+        u = u >= 0.f ? u : 0.1f * u;
+        const float v = u + bfx(xr, j);
+        acc[rt][2 * s + (j >> 2)][j & 3] = v;
+        sum += v;
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float mean = sum * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const float d = acc[rt][t][i] - mean; q = fmaf(d, d, q); }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rstd = 1.0f / sqrtf(q * (1.0f / D) + eps);
+    const long r = rbase + rt * 16 + li;
+    if (r < M) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float* g = vec + FV_G2 * D + 32 * s + 8 * lg;
+        const float* b = vec + FV_BE2 * D + 32 * s + 8 * lg;
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (acc[rt][2 * s + (j >> 2)][j & 3] - mean) * rstd * g[j] + b[j];
+        *reinterpret_cast<u32x4*>(out + r * D + 32 * s + 8 * lg) =
+            u32x4{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+      }
+    }
+  }
+}
+
+// one thread per 16-byte piece of the stream: per hidden chunk, NB W1 slabs
+// (block t*4+s: W1[hidden 16t+li][k 128kb+32s+8lg..]) then NB W2' slabs (block
+// t*2+s2: W2'[perm(8nb+t, li)][hidden 32s2 + 16(j/4) + 4lg + j%4, j < 8])
+__global__ void ffn_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w1, const bf16* __restrict__ w2g,
+                                bf16* __restrict__ out) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pieces) return;
+  const int NB = D / 128, SPC = 2 * NB;
+  const long slab = p / 1024;
+  const int b = (int)((p / 64) % 16), L = (int)(p % 64), li = L & 15, lg = L >> 4;
+  const int c = (int)(slab / SPC), r = (int)(slab % SPC);
+  bf16 v[8];
+  if (r < NB) {
+    const int t = b / 4, s = b % 4;
+    const long hid = (long)c * 64 + 16 * t + li;
+    const int k0 = r * 128 + 32 * s + 8 * lg;
+    for (int j = 0; j < 8; ++j) v[j] = w1[hid * D + k0 + j];
+  } else {
+    const int nb = r - NB, t = b / 2, s2 = b % 2;
+    const int n = ffn_perm(nb * 8 + t, li);
+    for (int j = 0; j < 8; ++j) {
+      const long hid = (long)c * 64 + 32 * s2 + 16 * (j >> 2) + 4 * lg + (j & 3);
+      v[j] = w2g[(long)n * 4 * D + hid];
+    }
+  }
+  for (int j = 0; j < 8; ++j) out[p * 8 + j] = v[j];
+}
+
+static bool ffn_d_ok(int D) { return D == 128 || D == 256 || D == 384; }
+
+template <int D>
+static int launch_ffn(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps, hipStream_t s) {
+  constexpr size_t lds = FfnShape<D>::LDS;
+  static const int dbg = getenv("SNVRAG_FFN_DBG") ? atoi(getenv("SNVRAG_FFN_DBG")) : 0;
+  static const bool one = getenv("SNVRAG_FFN_1W") != nullptr;   // one wave per SIMD variant
+  auto kern = one ? (dbg == 1 ? ffn_kernel<D, 2, 4, 1> : dbg == 2 ? ffn_kernel<D, 2, 4, 2> : ffn_kernel<D, 2, 4, 0>)
+                  : (dbg == 1 ? ffn_kernel<D, 1, 8, 1> : dbg == 2 ? ffn_kernel<D, 1, 8, 2> : ffn_kernel<D, 1, 8, 0>);
+  const int nthr = one ? 256 : 512;
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(nthr), lds, s, (int)M, (const bf16*)x1, (bf16*)out,
+                     (const char*)ws, vec, eps);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" size_t snvrag_ffn_pack_bytes(int D) {
+  switch (D) {
+    case 128: return (size_t)FfnShape<128>::NSLAB * FF_SLAB;
+    case 256: return (size_t)FfnShape<256>::NSLAB * FF_SLAB;
+    case 384: return (size_t)FfnShape<384>::NSLAB * FF_SLAB;
+    default: return 0;
+  }
+}
+
+extern "C" int snvrag_ffn_pack(int D, const void* w1, const void* w2g, void* out, void* stream) {
+  SNV_CHECK_ARG(ffn_d_ok(D), "fused FFN needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(w1 && w2g && out, "null pointer");
+  const long pieces = (long)(snvrag_ffn_pack_bytes(D) / 16);
+  hipLaunchKernelGGL(ffn_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
+                     (const bf16*)w1, (const bf16*)w2g, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
+                                  const float* vec, float eps, void* stream) {
+  SNV_CHECK_ARG(ffn_d_ok(D), "fused FFN needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(x1 && out && wstream && vec, "null pointer");
+  SNV_CHECK_ARG(x1 != out, "x1 and out must not alias");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)x1 % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wstream % 16) == 0 &&
+                    ((uintptr_t)vec % 16) == 0,
+                "x1/out/wstream/vec must be 16-byte aligned");
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  int rc;
+  switch (D) {
+    case 128: rc = launch_ffn<128>(M, x1, out, wstream, vec, eps, s); break;
+    case 256: rc = launch_ffn<256>(M, x1, out, wstream, vec, eps, s); break;
+    default: rc = launch_ffn<384>(M, x1, out, wstream, vec, eps, s); break;
+  }
+  if (rc) return rc;
+  evlog_end(s, EV_BLOCK, 2.0 * M * (double)D * D * 8);
+  return 0;
+}

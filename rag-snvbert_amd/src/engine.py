@@ -168,6 +168,10 @@ class Engine:
                      w2=cvt(ff.w_2.weight), b2=f32(ff.w_2.bias),
                      ln2_g=f32(blk.output_sublayer.norm.weight), ln2_b=f32(blk.output_sublayer.norm.bias),
                      w2g=w2g, b2g=b2g, c2g=c2g)
+            if T == torch.bfloat16 and D in (128, 256, 384):
+                # fused FFN: one fragment-ordered weight stream + vector table (csrc/ffn.hip)
+                t["ffn_w"] = K.ffn_pack(t["w1"], w2g)
+                t["ffn_v"] = K.ffn_vec(t["b1"], b2g, w2g, t["ln2_g"], t["ln2_b"])
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:

@@ -84,6 +84,39 @@ def fold_layernorm(w: torch.Tensor, b: torch.Tensor, g: torch.Tensor, beta: torc
     return wg, (w64 @ beta.double() + b.double()).float().contiguous(), (w64 @ g.double()).float().contiguous()
 
 
+def ffn_pack(w1: torch.Tensor, w2g: torch.Tensor) -> torch.Tensor:
+    """Fragment-ordered bf16 weight stream of the fused FFN kernel (csrc/ffn.hip)."""
+    D = w1.shape[1]
+    nbytes = int(N.lib().snvrag_ffn_pack_bytes(D))
+    if nbytes == 0:
+        raise ValueError(f"fused FFN needs D in (128, 256, 384), got {D}")
+    out = torch.empty(nbytes, device=w1.device, dtype=torch.uint8)
+    ws = [_c(t.to(torch.bfloat16)) for t in (w1, w2g)]
+    assert tuple(ws[0].shape) == (4 * D, D) and tuple(ws[1].shape) == (D, 4 * D)
+    check(N.lib().snvrag_ffn_pack(D, ptr(ws[0]), ptr(ws[1]), ptr(out), stream_ptr()), "ffn_pack")
+    return out
+
+
+def ffn_vec(b1, b2g, w2g, ln2_g, ln2_b) -> torch.Tensor:
+    """[b1 (4D) | b2' | c1 | ln2_g | ln2_b] f32; c1 = row sums of the bf16 w2g."""
+    c1 = w2g.to(torch.bfloat16).double().sum(1).float()
+    return torch.cat([t.detach().float().reshape(-1) for t in (b1, b2g, c1, ln2_g, ln2_b)]).contiguous()
+
+
+def ffn_forward(x1: torch.Tensor, wstream: torch.Tensor, vec: torch.Tensor, eps: float = 1e-5,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = LN2(x1 + FFN(x1)) in one launch (bf16; model/utils/feed_forward.py:18-21)."""
+    N.require_gpu(x1)
+    assert x1.dtype == torch.bfloat16
+    D = x1.shape[-1]
+    M = x1.numel() // D
+    if out is None:
+        out = torch.empty_like(x1)
+    check(N.lib().snvrag_ffn_forward(M, D, ptr(_c(x1)), ptr(out), ptr(wstream), ptr(vec), eps, stream_ptr()),
+          "ffn_forward")
+    return out
+
+
 def stat_tiles(n: int) -> int:
     """Column tiles of the row-panel GEMM for an N (the stats_out leading dim)."""
     for bn in (384, 256, 128, 64):

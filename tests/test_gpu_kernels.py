@@ -295,6 +295,32 @@ def test_linear_stats_then_rownorm_matches_ffn(dt):
     torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("D,M", [(384, 777), (384, 128 * 3), (128, 300), (256, 1), (384, 4 * 1030)])
+def test_ffn_fused_kernel(D, M):
+    """One-launch FFN sublayer (csrc/ffn.hip): out = LN2(x1 + lrelu(LN_f(lrelu(x1 W1^T + b1)) W2^T + b2))
+    (feed_forward.py:18-21 + sublayer.py:15-16) vs float64 torch on the same bf16 operands."""
+    g = torch.Generator(device="cpu").manual_seed(D + M)
+    x1 = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+    w_o = (torch.randn(D, D, generator=g) / math.sqrt(D)).to(DEV)
+    w1 = (torch.randn(4 * D, D, generator=g) / math.sqrt(D)).to(DEV)
+    w2 = (torch.randn(D, 4 * D, generator=g) / math.sqrt(4 * D)).to(DEV)
+    b1, b2 = torch.randn(4 * D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    gf, bf = (1 + 0.2 * torch.randn(4 * D, generator=g)).to(DEV), (0.1 * torch.randn(4 * D, generator=g)).to(DEV)
+    g2, be2 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    zero = torch.zeros(D, device=DEV)
+    w2g, b2g, _ = K().fold_layernorm(w2, b2, gf, bf, torch.bfloat16)
+    ws = K().ffn_pack(w1.to(torch.bfloat16), w2g)
+    vec = K().ffn_vec(b1, b2g, w2g, g2, be2)
+    out = K().ffn_forward(x1, ws, vec)
+    xd = x1.double()
+    h = torch.nn.functional.leaky_relu(xd @ w1.to(torch.bfloat16).double().T + b1.double(), 0.1)
+    hn = torch.nn.functional.layer_norm(h, (4 * D,), gf.double(), bf.double(), 1e-5)
+    f = torch.nn.functional.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
+    ref = torch.nn.functional.layer_norm(xd + f, (D,), g2.double(), be2.double(), 1e-5)
+    torch.testing.assert_close(out.double(), ref, rtol=5e-2, atol=5e-2)
+    assert (out.double() - ref).abs().mean() < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_encoder_fused_equals_unfused(dt, monkeypatch):
     """Encoder stack with LN fused into GEMM epilogues/prologues == the 8-launch unfused stack."""

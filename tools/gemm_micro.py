@@ -60,10 +60,16 @@ def main():
                                               M, D, 4 * D, 1),
         "ffn2 N384 K1536 plain": (lambda: K.linear(h, w[(D, 4 * D)], bias[D]), M, D, 4 * D, 0),
     }
+    w2g, b2g, _ = K.fold_layernorm(w[(D, 4 * D)].float(), bias[D], torch.ones(4 * D, device=dev),
+                                   torch.zeros(4 * D, device=dev), dt)
+    ffn_ws = K.ffn_pack(w[(4 * D, D)], w2g)
+    ffn_v = K.ffn_vec(bias[4 * D], b2g, w2g, lg, lb)
+    ffn_out = torch.empty_like(x)
+    cases["ffn fused (W1+W2, 2 GEMMs)"] = (lambda: K.ffn_forward(x, ffn_ws, ffn_v, out=ffn_out), M, 8 * D, D, -2)
     variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
     for name, (fn, m, n, k, extra) in cases.items():
         flop = 2.0 * m * n * k
-        byts = 2.0 * (m * k + n * k + m * n * (1 + extra))
+        byts = 2.0 * (m * k + n * k + m * n * (1 + extra)) if extra >= 0 else 2.0 * 2 * m * k
         for vn, env in variants:
             for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
                 os.environ.pop(kk, None)
