@@ -209,7 +209,8 @@ int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const int32_t* ex
 
 /* Mean of the k retrieved neighbours' COMPLETE-token embeddings
  * (embedding_rag_dataset.py:406-438 re-encode + bert.py:176-179 K-mean), eval:
- * out[q,l,:] = mean_j W[tok_j(l)] + pe[l] + Ar[l]; tokens: <sos>, alleles, <eos>, <pad>. */
+ * out[q,l,:] = mean_j W[tok_j(l)] + pe[l] + Ar[l]; tokens: <sos>, alleles, <eos>, <pad>.
+ * 1 <= k <= 128 (negative indices = no neighbour, excluded from the mean). */
 int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
                     const uint8_t* codes, int64_t ld_codes, int32_t n_sites,
                     const float* W, const float* pe, const float* Ar,

@@ -128,45 +128,48 @@ __global__ __launch_bounds__(256) void posfeat_kernel(int L, const float* __rest
 // ------------------------------------------------------------------- AF gate --
 // fusion.py:82-86: gate = sigmoid(W2 gelu(W1 c + b1) + b2), enc = gelu(LN(Wj c + bj)),
 // out = af + rs * gate * enc.  One wave per row m; D <= 1024.
+// Lane-per-row layout: the 32 gate hiddens of a row sit in the lane's VGPRs and the
+// per-column weights (g2_w row, j_w, LN affine) are wave-uniform scalar loads, so the
+// [D x 32] gate GEMV costs 32 v_fma per element with no cross-lane traffic.  The
+// joint-encoder LayerNorm is two passes over the D columns of the 2-input Linear.
 template <typename T>
 __global__ __launch_bounds__(256) void af_gate_kernel(long M, int D, const float* __restrict__ af,
                                                       const float* __restrict__ afp, snvrag_afgate_w_t w,
                                                       T* __restrict__ out) {
-  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (m >= M) return;
-  const float a0 = af[m], a1 = afp[m];
-  // hidden 32 of the gate: lanes 0..31 compute one unit each, then broadcast
-  float hid = 0.f;
-  if (lane < 32) hid = gelu_erf(w.g1_w[lane * 2] * a0 + w.g1_w[lane * 2 + 1] * a1 + w.g1_b[lane]);
-  constexpr int MAXP = 16;        // D <= 1024
-  float enc[MAXP];
+  constexpr int V = 16 / sizeof(T);
+  // 64 rows per workgroup; its 4 waves split the D output columns
+  const long m = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int cpw = ((D / V + 3) / 4) * V;
+  const int c_lo = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * cpw);
+  const int c_hi = min(D, c_lo + cpw);
+  const bool ok = m < M;
+  const float a0 = ok ? af[m] : 0.f, a1 = ok ? afp[m] : 0.f;
+  float hid[32];
+#pragma unroll
+  for (int u = 0; u < 32; ++u) hid[u] = gelu_erf(w.g1_w[u * 2] * a0 + w.g1_w[u * 2 + 1] * a1 + w.g1_b[u]);
   float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXP; ++i) {
-    const int n = lane + 64 * i;
-    enc[i] = 0.f;
-    if (n < D) { enc[i] = w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n]; s += enc[i]; }
-  }
-  const float mean = wave_sum(s) / D;
+  for (int n = 0; n < D; ++n) s += w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n];
+  const float mean = s / D;
   float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXP; ++i) {
-    const int n = lane + 64 * i;
-    if (n < D) { const float d = enc[i] - mean; q += d * d; }
+  for (int n = 0; n < D; ++n) {
+    const float d = w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n] - mean;
+    q += d * d;
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / D + 1e-5f);
+  const float rstd = 1.0f / sqrtf(q / D + 1e-5f);
+  for (int n0 = c_lo; n0 < c_hi; n0 += V) {
+    T o[V];
 #pragma unroll
-  for (int i = 0; i < MAXP; ++i) {
-    const int n = lane + 64 * i;
-    if (n < D) {
+    for (int j = 0; j < V; ++j) {
+      const int n = n0 + j;
       float g = w.g2_b[n];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) g = fmaf(w.g2_w[n * 32 + u], __shfl(hid, u, 64), g);
+      for (int u = 0; u < 32; ++u) g = fmaf(w.g2_w[n * 32 + u], hid[u], g);
       g = 1.0f / (1.0f + expf(-g));
-      const float e = gelu_erf((enc[i] - mean) * rstd * w.ln_w[n] + w.ln_b[n]);
-      out[m * D + n] = from_f32<T>(a0 + w.res_scale * (g * e));
+      const float enc = w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n];
+      const float e = gelu_erf((enc - mean) * rstd * w.ln_w[n] + w.ln_b[n]);
+      o[j] = from_f32<T>(a0 + w.res_scale * (g * e));
     }
+    if (ok) *reinterpret_cast<u32x4*>(out + m * D + n0) = *reinterpret_cast<u32x4*>(o);
   }
 }
 
@@ -333,13 +336,13 @@ extern "C" int snvrag_posfeat(int64_t B, int64_t L, const float* pos, const snvr
 extern "C" int snvrag_af_gate(int dtype_out, int64_t M, int64_t D, const float* af, const float* af_p,
                               const snvrag_afgate_w_t* w, void* out, void* stream) {
   SNV_CHECK_ARG(af && af_p && w && out, "null pointer");
-  SNV_CHECK_ARG(D <= 1024, "D <= 1024");
+  SNV_CHECK_ARG(D % 8 == 0, "D % 8");
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   if (dtype_out == SNVRAG_BF16)
-    hipLaunchKernelGGL(af_gate_kernel<bf16>, dim3(cdiv(M, 4)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (bf16*)out);
+    hipLaunchKernelGGL(af_gate_kernel<bf16>, dim3(cdiv(M, 64)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (bf16*)out);
   else
-    hipLaunchKernelGGL(af_gate_kernel<float>, dim3(cdiv(M, 4)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (float*)out);
+    hipLaunchKernelGGL(af_gate_kernel<float>, dim3(cdiv(M, 64)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (float*)out);
   SNV_LAUNCH_CHECK();
   return 0;
 }

@@ -29,6 +29,12 @@ __device__ __forceinline__ uint64_t make_key(int d, uint32_t idx) {
   return ((uint64_t)(uint32_t)(d + KEY_BIAS) << 32) | idx;
 }
 
+__device__ __forceinline__ int gcd_u(int a, int b) {   // a, b >= 0; gcd(0, b) = b
+  uint32_t x = (uint32_t)a, y = (uint32_t)b;
+  while (y) { const uint32_t t = x % y; x = y; y = t; }
+  return (int)x;
+}
+
 // ------------------------------------------------------------------- LUT ---
 // One workgroup per query.  Positions l = 0..L-1 contribute to the constant
 // C_q; unmasked sites s (l = s + 1) contribute Delta_q[s].
@@ -138,29 +144,65 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
   // quantise + scatter into fragment order: [qt][limb][ks][lane(64)][16]
   const int qt = q >> 4, qr = q & 15;
   const int KS = n_sites_pad / 64;
-  for (int s = tid; s < n_sites_pad; s += 256) {
+  auto quant = [&](int s) {
     float v = rintf(sdelta[s] * sc);
     v = fminf(fmaxf(v, (float)-qmax), (float)qmax);
-    const int dq = (int)v;
+    return (int)v;
+  };
+  auto frag = [&](int s) {               // offset of site s of this query inside one [ks][lane][16] plane
     const int ks = s >> 6, within = s & 63, g = within >> 4, j = within & 15;
-    const int ln = g * 16 + qr;
+    return ((long)ks * 64 + g * 16 + qr) * 16 + j;
+  };
+  int gl = 0;                            // gcd of the nonzero |dq| of this thread's sites
+  for (int s = tid; s < n_sites_pad; s += 256) {
+    const int dq = quant(s);
     if (limbs == 2) {
       const int hi = dq >> 7, lo = dq & 127;
-      lut[((((long)qt * 2 + 0) * KS + ks) * 64 + ln) * 16 + j] = (int8_t)hi;
-      lut[((((long)qt * 2 + 1) * KS + ks) * 64 + ln) * 16 + j] = (int8_t)lo;
+      lut[((long)qt * 2 + 0) * KS * 1024 + frag(s)] = (int8_t)hi;
+      lut[((long)qt * 2 + 1) * KS * 1024 + frag(s)] = (int8_t)lo;
+      gl = gcd_u(gl, dq < 0 ? -dq : dq);
     } else {
-      lut[(((long)qt * KS + ks) * 64 + ln) * 16 + j] = (int8_t)dq;
+      lut[(long)qt * KS * 1024 + frag(s)] = (int8_t)dq;
     }
+  }
+  if (limbs != 2) return;
+  // 1-limb reduction: with g = gcd_s |dq_s|, D_2limb = g * sum_s (dq_s/g) a_r[s],
+  // so when max |dq|/g fits int8 the scan may run one limb of dq/g and multiply by g —
+  // identical integer distances, identical (distance, index) order.
+  __shared__ int sg[4];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) gl = gcd_u(gl, __shfl_xor(gl, o, 64));
+  if (lane == 0) sg[wave] = gl;
+  __syncthreads();
+  const int g = gcd_u(gcd_u(sg[0], sg[1]), gcd_u(sg[2], sg[3]));
+  int8_t* lut1 = lut + (long)((nq + 15) >> 4) * 2 * KS * 1024;
+  int* mult = reinterpret_cast<int*>(lut1 + (long)((nq + 15) >> 4) * KS * 1024);
+  int* any_wide = mult + ((nq + 15) & ~15);
+  bool fits = true;
+  for (int s = tid; s < n_sites_pad; s += 256) {
+    const int dq = quant(s);
+    const int r = g ? dq / g : 0;
+    fits &= r >= -127 && r <= 127;
+    lut1[(long)qt * KS * 1024 + frag(s)] = (int8_t)r;
+  }
+  fits = __syncthreads_and(fits);
+  if (tid == 0) {
+    mult[q] = g;
+    if (!fits) atomicOr(any_wide, 1);
   }
 }
 
 // padding rows of the last query tile must be zero
 __global__ void lut_zero_pad_kernel(int8_t* lut, int nq, int KS, int limbs) {
-  const int qt = nq >> 4;
+  const int qt = nq >> 4, nqt = (nq + 15) >> 4;
   const long per_tile = (long)limbs * KS * 64 * 16;
+  int8_t* lut1 = lut + (long)nqt * 2 * KS * 1024;      // one-limb region (limbs == 2)
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < per_tile; i += (long)gridDim.x * blockDim.x) {
     const int ln = (int)((i / 16) % 64);
-    if ((ln & 15) >= (nq & 15)) lut[qt * per_tile + i] = 0;
+    if ((ln & 15) >= (nq & 15)) {
+      lut[qt * per_tile + i] = 0;
+      if (limbs == 2 && i < per_tile / 2) lut1[(long)qt * KS * 1024 + i] = 0;
+    }
   }
 }
 
@@ -351,59 +393,73 @@ __global__ void decode_kernel(const uint64_t* __restrict__ keys, int nq, int k, 
 }
 
 // ------------------------------------------------------------- rag mean ---
+// A workgroup owns RM_P token positions x RM_Q queries: the per-position rows
+// (W[tok0], W[tok1] - W[tok0], pe, A_r) are loaded once and reused for all RM_Q
+// queries, and the neighbour alt-allele counts come from independent byte loads
+// (neighbour indices staged in LDS first), so no load waits on another.
+constexpr int RM_P = 8, RM_Q = 16, RM_KMAX = 128;
+
 template <typename T>
-__global__ __launch_bounds__(256) void rag_mean_kernel(int L, int D, int k, const int64_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void rag_mean_kernel(int nq, int L, int D, int k, const int64_t* __restrict__ idx,
                                                        const uint8_t* __restrict__ codes, long ld, int n_sites,
                                                        const float* __restrict__ W, const float* __restrict__ pe,
                                                        const float* __restrict__ Ar, int tok0, int tok1, int sos,
                                                        int eos, int pad, T* __restrict__ out) {
-  __shared__ float frac[64];
-  __shared__ int nvalid_s;
-  const int q = blockIdx.y, l0 = blockIdx.x * 64, tid = threadIdx.x;
-  if (tid == 0) {
-    int nv = 0;
-    for (int j = 0; j < k; ++j) nv += idx[(long)q * k + j] >= 0;
-    nvalid_s = nv;
+  __shared__ int64_t sidx[RM_Q * RM_KMAX];
+  __shared__ float frac[RM_Q][RM_P];
+  __shared__ int nvalid[RM_Q];
+  const int l0 = blockIdx.x * RM_P, q0 = blockIdx.y * RM_Q, tid = threadIdx.x;
+  for (int i = tid; i < RM_Q * k; i += 256) {
+    const int q = q0 + i / k;
+    sidx[i] = q < nq ? idx[(long)q * k + i % k] : -1;
   }
   __syncthreads();
-  const int nv = nvalid_s;
-  if (tid < 64) {
-    const int l = l0 + tid;
-    float f = 0.f;
-    if (l >= 1 && l <= n_sites && nv > 0) {
-      int c = 0;
-      for (int j = 0; j < k; ++j) {
-        const int64_t r = idx[(long)q * k + j];
-        if (r >= 0) c += codes[r * ld + (l - 1)];
-      }
-      f = (float)c / (float)nv;
+  if (tid < RM_Q * RM_P) {
+    const int qq = tid / RM_P, p = tid % RM_P, l = l0 + p;
+    const bool site = l >= 1 && l <= n_sites;
+    int c = 0, nv = 0;
+#pragma unroll 8
+    for (int j = 0; j < k; ++j) {
+      const int64_t r = sidx[qq * k + j];
+      nv += r >= 0;
+      c += (r >= 0 && site) ? codes[r * ld + (l - 1)] : 0;
     }
-    frac[tid] = f;
+    frac[qq][p] = nv > 0 ? (float)c / (float)nv : 0.f;
+    if (p == 0) nvalid[qq] = nv;
   }
   __syncthreads();
   constexpr int V = 16 / sizeof(T);
   const int cpr = D / V;
-  for (int id = tid; id < 64 * cpr; id += 256) {
-    const int rl = id / cpr, c = (id % cpr) * V;
-    const int l = l0 + rl;
+  const int nqb = min(RM_Q, nq - q0);
+  for (int id = tid; id < RM_P * cpr; id += 256) {
+    const int p = id / cpr, c = (id % cpr) * V;
+    const int l = l0 + p;
     if (l >= L) break;
     int t;
     const bool site = l >= 1 && l <= n_sites;
     if (l == 0) t = sos; else if (site) t = tok0; else if (l == n_sites + 1) t = eos; else t = pad;
-    const float f = frac[rl];
-    float v[V];
+    float w0[V], dw[V], pp[V], ar[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      float w = W[(long)t * D + c + j];
-      if (site) w = nv > 0 ? w + f * (W[(long)tok1 * D + c + j] - w) : 0.f;
-      float x = w + pe[(long)l * D + c + j];
-      if (Ar) x += Ar[(long)l * D + c + j];
-      v[j] = x;
+      w0[j] = W[(long)t * D + c + j];
+      dw[j] = site ? W[(long)tok1 * D + c + j] - w0[j] : 0.f;
+      pp[j] = pe[(long)l * D + c + j];
+      ar[j] = Ar ? Ar[(long)l * D + c + j] : 0.f;
     }
-    T o[V];
+    for (int qq = 0; qq < nqb; ++qq) {
+      const float f = frac[qq][p];
+      const bool any = nvalid[qq] > 0;
+      T o[V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = from_f32<T>(v[j]);
-    *reinterpret_cast<u32x4*>(out + ((long)q * L + l) * D + c) = *reinterpret_cast<u32x4*>(o);
+      for (int j = 0; j < V; ++j) {
+        float w = w0[j];
+        if (site) w = any ? w + f * dw[j] : 0.f;
+        float x = w + pp[j];
+        if (Ar) x += ar[j];
+        o[j] = from_f32<T>(x);
+      }
+      *reinterpret_cast<u32x4*>(out + ((long)(q0 + qq) * L + l) * D + c) = *reinterpret_cast<u32x4*>(o);
+    }
   }
 }
 
@@ -446,6 +502,9 @@ __global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long
 constexpr int S2_R = 32;                  // haplotypes per LDS stage
 constexpr int S2_CAP = 64;                // candidate slots per query (k <= 32 plus 16+ of slack)
 constexpr int S2_TH = S2_CAP - 16;  // compact when more than 48 held
+#ifndef S2_QTW1
+#define S2_QTW1 1                         // query tiles per wave of the reduced one-limb scan
+#endif
 
 __device__ __forceinline__ void compact_row2(uint64_t* buf, int row, int cnt, int k, int lane, int& new_cnt,
                                              int& new_th) {
@@ -457,43 +516,54 @@ __device__ __forceinline__ void compact_row2(uint64_t* buf, int row, int cnt, in
   new_th = (cnt >= k) ? (int)(kth >> 32) - KEY_BIAS : INT_MAX;
 }
 
-template <int KS, int LIMBS, int MODE = 0>   // MODE (diagnostics only): 1 = loads only, 2 = compute only
-__global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
-                                                    const int8_t* __restrict__ lut, int nq, int k, long range,
-                                                    long ref_offset, uint64_t* __restrict__ parts,
-                                                    const int* __restrict__ th_init) {
+// One body, two shapes:
+//   LIMBS = 2, QTW = 1: 8 computing waves, one 16-query tile each (LUT hi/lo limbs);
+//   LIMBS = 1, QTW = 2: the reduced LUT (lut_kernel: dq/g fits one limb, distance = g *
+//                       D_1limb): 4 computing waves, two query tiles each, so every B
+//                       fragment read from LDS feeds two MFMAs — half the LDS read traffic
+//                       of the 2-limb shape, whose 8 waves x 32 KiB per stage saturate
+//                       the 128 B/clk LDS port.  Waves 4..7 only stream codes.
+template <int KS, int LIMBS, int QTW, int MODE>
+__device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict__ codes, long n_ref, long ld,
+                                           const int8_t* __restrict__ lut, const int* __restrict__ mult, int nq,
+                                           int k, long range, long ref_offset, uint64_t* __restrict__ parts,
+                                           const int* __restrict__ th_init) {
   constexpr int ROWB = KS * 64;                        // staged row bytes
   constexpr int STAGE = S2_R * ROWB;
   constexpr int PPW = STAGE / 1024 / 8;                // glds pieces per wave per stage
   constexpr int NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;  // ring depth within 96 KiB
   static_assert(NST >= 2, "stage too large");
   static_assert(ROWB % 256 == 0 && PPW >= 1, "rows must be multiples of 256 B");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + NST * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int nqt = (nq + 15) >> 4;
-  const int qt = blockIdx.y * 8 + wave;
-  const bool active = qt < nqt;                         // wave-uniform; every wave still loads + syncs
-  uint64_t* buf = cand + wave * 16 * S2_CAP;
+  const int qt0 = blockIdx.y * 8 + wave * QTW;
+  const bool active = wave * QTW < 8 && qt0 < nqt;     // wave-uniform; every wave still loads + syncs
   const int part = blockIdx.x;
   const long r_begin = (long)part * range;
   const long r_end = min(n_ref, r_begin + range);
   const int nstage = r_end > r_begin ? (int)((r_end - r_begin + S2_R - 1) / S2_R) : 0;
 
-  // LUT limbs: unconditional loads (inactive waves read the last tile) retired BEFORE the
+  // LUT limbs: unconditional loads (inactive tiles read the last tile) retired BEFORE the
   // loop — a load still pending inside it would make hipcc wait vmcnt(0), draining the ring
-  const int qtc = active ? qt : nqt - 1;
-  i32x4 a[LIMBS][KS];
+  int qtc[QTW];
+#pragma unroll
+  for (int t = 0; t < QTW; ++t) qtc[t] = min(qt0 + t, nqt - 1);
+  i32x4 a[LIMBS][QTW][KS];
 #pragma unroll
   for (int lb = 0; lb < LIMBS; ++lb)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      a[lb][ks] = *reinterpret_cast<const i32x4*>(lut + ((((long)qtc * LIMBS + lb) * KS + ks) * 64 + lane) * 16);
+    for (int t = 0; t < QTW; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        a[lb][t][ks] = *reinterpret_cast<const i32x4*>(lut + ((((long)qtc[t] * LIMBS + lb) * KS + ks) * 64 + lane) * 16);
 #pragma unroll
   for (int lb = 0; lb < LIMBS; ++lb)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(a[lb][ks]));
+    for (int t = 0; t < QTW; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(a[lb][t][ks]));
 
   auto issue = [&](int st, long r0) {
 #pragma unroll
@@ -510,14 +580,20 @@ __global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ 
     }
   };
 
-  int th[4], cnt[4];
+  int th[QTW][4], cnt[QTW][4], mul[QTW][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = qtc * 16 + 4 * lg + i;
-    th[i] = (th_init && q < nq) ? th_init[q] : INT_MAX;
-    cnt[i] = 0;
-  }
-  asm volatile("" ::"v"(th[0]), "v"(th[1]), "v"(th[2]), "v"(th[3]));   // retire before the ring starts
+  for (int t = 0; t < QTW; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = qtc[t] * 16 + 4 * lg + i;
+      th[t][i] = (th_init && q < nq) ? th_init[q] : INT_MAX;
+      mul[t][i] = mult ? mult[q] : 1;
+      cnt[t][i] = 0;
+    }
+#pragma unroll
+  for (int t = 0; t < QTW; ++t)   // retire before the ring starts
+    asm volatile("" ::"v"(th[t][0]), "v"(th[t][1]), "v"(th[t][2]), "v"(th[t][3]), "v"(mul[t][0]), "v"(mul[t][1]),
+                 "v"(mul[t][2]), "v"(mul[t][3]));
 
 #pragma unroll
   for (int j = 0; j < NST - 1; ++j)
@@ -541,77 +617,120 @@ __global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ 
     i32x4 bq[PF];
 #pragma unroll
     for (int f = 0; f < PF; ++f) bq[f] = bfrag(f);
-    i32x4 acc[RG][LIMBS];
+    i32x4 acc[RG][QTW][LIMBS];
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
-      for (int lb = 0; lb < LIMBS; ++lb) acc[rg][lb] = i32x4{0, 0, 0, 0};
+      for (int t = 0; t < QTW; ++t)
+#pragma unroll
+        for (int lb = 0; lb < LIMBS; ++lb) acc[rg][t][lb] = i32x4{0, 0, 0, 0};
 #pragma unroll
     for (int f = 0; f < F; ++f) {
       const i32x4 b = bq[f % PF];
       if (f + PF < F) bq[f % PF] = bfrag(f + PF);
 #pragma unroll
-      for (int lb = 0; lb < LIMBS; ++lb)
-        acc[f / KS][lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[lb][f % KS], b, acc[f / KS][lb], 0, 0, 0);
+      for (int t = 0; t < QTW; ++t)
+#pragma unroll
+        for (int lb = 0; lb < LIMBS; ++lb)
+          acc[f / KS][t][lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[lb][t][f % KS], b, acc[f / KS][t][lb], 0, 0, 0);
     }
     // pin the interleave (hipcc otherwise sinks each read to just before its MFMA):
-    // PF reads, then per fragment {1 read, LIMBS MFMAs}
+    // PF reads, then per fragment {1 read, QTW*LIMBS MFMAs}
     __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
 #pragma unroll
     for (int f = 0; f < F; ++f) {
       if (f + PF < F) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, LIMBS, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, QTW * LIMBS, 0);
     }
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg) {
       const long r = r0 + 16 * rg + li;
       const bool rv = r < r_end;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int d = LIMBS == 2 ? acc[rg][0][i] * 128 + acc[rg][1][i] : acc[rg][0][i];
-        const bool pass = rv && d < th[i];
-        const uint64_t m = __ballot(pass);
-        if (m) {
-          const uint32_t gb = (uint32_t)(m >> (16 * lg)) & 0xFFFFu;
-          if (pass) {
-            const int pre = __popc(gb & ((1u << li) - 1u));
-            buf[(4 * lg + i) * S2_CAP + cnt[i] + pre] = make_key(d, (uint32_t)(r + ref_offset));
-          }
-          cnt[i] += __popc(gb);
-        }
-      }
+      for (int t = 0; t < QTW; ++t) {
+        uint64_t* buf = cand + (wave * QTW + t) * 16 * S2_CAP;
+        int dd[4];
+        bool anyp = false;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint64_t need = __ballot(cnt[i] > S2_TH);
-        while (need) {
-          const int src = __builtin_ctzll(need);
-          const int g = src >> 4;
-          need &= ~(0xFFFFull << (16 * g));
-          int nc, nt;
-          compact_row2(buf, 4 * g + i, __shfl(cnt[i], src, 64), k, lane, nc, nt);
-          if (lg == g) { cnt[i] = nc; th[i] = nt; }
+        for (int i = 0; i < 4; ++i) {
+          dd[i] = LIMBS == 2 ? acc[rg][t][0][i] * 128 + acc[rg][t][1][i] : acc[rg][t][0][i] * mul[t][i];
+          anyp |= dd[i] < th[t][i];
+        }
+        if (!__ballot(rv && anyp)) continue;   // the common case once the threshold is tight
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int d = dd[i];
+          const bool pass = rv && d < th[t][i];
+          const uint64_t m = __ballot(pass);
+          if (m) {
+            const uint32_t gb = (uint32_t)(m >> (16 * lg)) & 0xFFFFu;
+            if (pass) {
+              const int pre = __popc(gb & ((1u << li) - 1u));
+              buf[(4 * lg + i) * S2_CAP + cnt[t][i] + pre] = make_key(d, (uint32_t)(r + ref_offset));
+            }
+            cnt[t][i] += __popc(gb);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint64_t need = __ballot(cnt[t][i] > S2_TH);
+          while (need) {
+            const int src = __builtin_ctzll(need);
+            const int g = src >> 4;
+            need &= ~(0xFFFFull << (16 * g));
+            int nc, nt;
+            compact_row2(buf, 4 * g + i, __shfl(cnt[t][i], src, 64), k, lane, nc, nt);
+            if (lg == g) { cnt[t][i] = nc; th[t][i] = nt; }
+          }
         }
       }
     }
   }
   if (!active) return;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    for (int g = 0; g < 4; ++g) {
-      const int row = 4 * g + i;
-      const int c = __shfl(cnt[i], 16 * g, 64);
-      int nc, nt;
-      compact_row2(buf, row, c, k, lane, nc, nt);
-      const int q = qt * 16 + row;
-      if (q < nq && lane < k)
-        parts[((long)part * nq + q) * k + lane] = lane < nc ? buf[row * S2_CAP + lane] : KEY_MAX;
+  for (int t = 0; t < QTW; ++t) {
+    if (qt0 + t >= nqt) break;
+    uint64_t* buf = cand + (wave * QTW + t) * 16 * S2_CAP;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      for (int g = 0; g < 4; ++g) {
+        const int row = 4 * g + i;
+        const int c = __shfl(cnt[t][i], 16 * g, 64);
+        int nc, nt;
+        compact_row2(buf, row, c, k, lane, nc, nt);
+        const int q = (qt0 + t) * 16 + row;
+        if (q < nq && lane < k)
+          parts[((long)part * nq + q) * k + lane] = lane < nc ? buf[row * S2_CAP + lane] : KEY_MAX;
+      }
     }
   }
 }
 
+// MODE (diagnostics only): 1 = loads only, 2 = compute only.  A 2-limb launch whose LUT
+// reduced to one limb for every query (wide == 0, written by lut_kernel) runs the
+// 1-limb two-tile body instead — decided on the device, no host round trip.
+template <int KS, int LIMBS, int MODE = 0>
+__global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
+                                                    const int8_t* __restrict__ lut, int nq, int k, long range,
+                                                    long ref_offset, uint64_t* __restrict__ parts,
+                                                    const int* __restrict__ th_init, const int* __restrict__ wide) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (LIMBS == 2 && KS <= 16) {   // (KS = 20: two tiles of A would spill)
+    if (wide && *wide == 0) {
+      const long nqt = (nq + 15) >> 4;
+      const int8_t* lut1 = lut + nqt * 2 * KS * 1024;
+      const int* mult = reinterpret_cast<const int*>(lut1 + nqt * KS * 1024);
+      scan2_body<KS, 1, S2_QTW1, MODE>(smem, codes, n_ref, ld, lut1, mult, nq, k, range, ref_offset, parts, th_init);
+      return;
+    }
+  }
+  scan2_body<KS, LIMBS, 1, MODE>(smem, codes, n_ref, ld, lut, nullptr, nq, k, range, ref_offset, parts, th_init);
+}
+
 template <int KS, int LB>
 static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* codes, long n_ref, long ld,
-                         const int8_t* lut, int k, long range, long off, uint64_t* parts, const int* th) {
+                         const int8_t* lut, int k, long range, long off, uint64_t* parts, const int* th,
+                         const int* wide) {
   constexpr size_t STAGE = (size_t)S2_R * KS * 64;
   constexpr size_t NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;
   const size_t lds = NST * STAGE + 8 * 16 * S2_CAP * sizeof(uint64_t);
@@ -623,7 +742,7 @@ static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* code
   }
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 g((unsigned)n_parts, (unsigned)(((nq + 15) / 16 + 7) / 8));
-  hipLaunchKernelGGL(kern, g, dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th);
+  hipLaunchKernelGGL(kern, g, dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th, wide);
 }
 
 static int scan_parts(long n_ref) {
@@ -647,8 +766,15 @@ static void launch_scan(dim3 g, hipStream_t s, const uint8_t* codes, long n_ref,
 
 using namespace snvrag;
 
+// LUT buffer: [nqt][limbs][KS][64 lanes][16 B] fragments; for limbs == 2 followed by the
+// reduced one-limb fragments [nqt][KS][64][16], int32 mult[nqt*16] and int32 wide flag.
+static size_t lut_tail_offset(int64_t nq, int32_t n_sites_pad) {
+  return (size_t)((nq + 15) / 16) * 3 * (n_sites_pad / 64) * 1024;
+}
 extern "C" size_t snvrag_knn_lut_bytes(int64_t nq, int32_t n_sites_pad, int limbs) {
-  return (size_t)((nq + 15) / 16) * limbs * (n_sites_pad / 64) * 64 * 16;
+  const size_t main = (size_t)((nq + 15) / 16) * limbs * (n_sites_pad / 64) * 64 * 16;
+  if (limbs != 2) return main;
+  return lut_tail_offset(nq, n_sites_pad) + (size_t)((nq + 15) / 16) * 16 * 4 + 16;
 }
 
 extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
@@ -662,6 +788,10 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
   if (nq == 0) return 0;
   hipStream_t s = as_stream(stream);
   const size_t sh = (size_t)(n_sites_pad + 4) * sizeof(float);
+  if (limbs == 2) {   // mult[] and the wide flag start at zero
+    char* tail = (char*)lut_out + lut_tail_offset(nq, n_sites_pad);
+    SNV_HIP(hipMemsetAsync(tail, 0, (size_t)((nq + 15) / 16) * 16 * 4 + 16, s));
+  }
   hipLaunchKernelGGL(lut_kernel, dim3((unsigned)nq), dim3(256), sh, s, (int)L, (int)D, tok_q, W, Aq,
                      (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, (int)nq, tok0, tok1, mask_tok,
                      limbs, (int8_t*)lut_out, exp_out, const_out);
@@ -710,13 +840,18 @@ extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_c
   dim3 g((unsigned)n_parts, (unsigned)(((nq + 15) / 16 + 3) / 4));
   hipStream_t s = as_stream(stream);
   const int8_t* L8 = (const int8_t*)lut;
+  // lut_kernel's "some query needs two limbs" flag (limbs == 2 buffers only)
+  const int* wide = (limbs == 2 && !getenv("SNVRAG_KNN_NO_REDUCE"))
+                        ? reinterpret_cast<const int*>(L8 + lut_tail_offset(nq, n_sites_pad) +
+                                                       (size_t)((nq + 15) / 16) * 16 * 4)
+                        : nullptr;
   evlog_begin(s);
   const bool v2 = n_sites_pad % 256 == 0 && n_sites_pad <= 1280 && !getenv("SNVRAG_SCAN_V1");
   if (v2) {
 #define SCAN2(K_)                                                                                          \
   case K_:                                                                                                 \
-    if (limbs == 2) launch_scan2<K_, 2>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init); \
-    else launch_scan2<K_, 1>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init);          \
+    if (limbs == 2) launch_scan2<K_, 2>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init, wide); \
+    else launch_scan2<K_, 1>(n_parts, nq, s, codes, n_ref, ld_codes, L8, k, range, ref_offset, part_keys, th_init, nullptr);          \
     break;
     switch (KS) { SCAN2(4) SCAN2(8) SCAN2(12) SCAN2(16) SCAN2(20) }
 #undef SCAN2
@@ -799,13 +934,14 @@ extern "C" int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, 
   SNV_CHECK_ARG(idx && codes && W && pe && out, "null pointer");
   SNV_CHECK_ARG(D % 8 == 0 && n_sites + 2 <= L, "shape");
   if (nq == 0) return 0;
-  dim3 g((unsigned)cdiv(L, 64), (unsigned)nq);
+  SNV_CHECK_ARG(k >= 1 && k <= RM_KMAX, "k must be in [1, 128]");
+  dim3 g((unsigned)cdiv(L, RM_P), (unsigned)cdiv(nq, RM_Q));
   hipStream_t s = as_stream(stream);
   if (dtype_out == SNVRAG_BF16)
-    hipLaunchKernelGGL(rag_mean_kernel<bf16>, g, dim3(256), 0, s, (int)L, (int)D, k, idx, codes, (long)ld_codes,
+    hipLaunchKernelGGL(rag_mean_kernel<bf16>, g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes, (long)ld_codes,
                        n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (bf16*)out);
   else
-    hipLaunchKernelGGL(rag_mean_kernel<float>, g, dim3(256), 0, s, (int)L, (int)D, k, idx, codes, (long)ld_codes,
+    hipLaunchKernelGGL(rag_mean_kernel<float>, g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes, (long)ld_codes,
                        n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (float*)out);
   SNV_LAUNCH_CHECK();
   return 0;

@@ -11,6 +11,7 @@ Reference behaviour replaced (src/dataset/embedding_rag_dataset.py):
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -75,7 +76,7 @@ class PanelIndex:
     def scan_keys(self, lut: torch.Tensor, nq: int, limbs: int, k: int, presample: Optional[bool] = None) -> torch.Tensor:
         """Exact local top-k keys [nq, k] (uint64 in int64 storage) with global indices.
 
-        Large panels first scan a 1/32 prefix of the panel: its k-th best distance is an
+        Large panels first scan a 1/128 prefix of the panel: its k-th best distance is an
         upper bound on the panel's, so the full scan can start from it (strictly above it
         nothing can enter the top-k) and keeps far fewer candidates; the result is the
         same exact top-k."""
@@ -84,9 +85,11 @@ class PanelIndex:
             presample = n_ref >= self.SAMPLE_MIN
         th = None
         if presample:
-            m = max(16 * k, ((n_ref // 32) + 15) // 16 * 16)
+            div = int(os.environ.get("SNVRAG_SAMPLE_DIV", "128"))
+            rpp = int(os.environ.get("SNVRAG_SAMPLE_RPP", "64"))
+            m = max(16 * k, ((n_ref // div) + 15) // 16 * 16)
             sample = K.knn_scan(self.codes[:m], self.n_sites_pad, lut, nq, limbs, k, self.ref_offset,
-                                n_parts=max(1, min(256, m // 128)))
+                                n_parts=max(1, min(256, m // rpp)))
             th = K.knn_threshold(K.topk_merge(sample, k), k)
         parts = K.knn_scan(self.codes, self.n_sites_pad, lut, nq, limbs, k, self.ref_offset, th_init=th)
         return K.topk_merge(parts, k)

@@ -5,6 +5,7 @@ kernels against a plain torch fp32 (float64 where stated) reference of the same 
 """
 
 import math
+import os
 
 import numpy as np
 import pytest
@@ -128,7 +129,8 @@ def decode_lut(lut: torch.Tensor, nq: int, n_sites_pad: int, limbs: int) -> np.n
     """Inverse of the fragment layout [qt][limb][ks][lane][16] -> int32 dq[q, s]."""
     KS = n_sites_pad // 64
     nqt = (nq + 15) // 16
-    b = lut.cpu().numpy().view(np.int8).reshape(nqt, limbs, KS, 4, 16, 16)   # [qt][limb][ks][g][li][j]
+    b = lut.cpu().numpy().view(np.int8)[:nqt * limbs * KS * 1024]
+    b = b.reshape(nqt, limbs, KS, 4, 16, 16)                                   # [qt][limb][ks][g][li][j]
     b = b.transpose(0, 4, 1, 2, 3, 5).reshape(nqt * 16, limbs, n_sites_pad).astype(np.int32)
     dq = b[:, 0] * 128 + b[:, 1] if limbs == 2 else b[:, 0]
     return dq[:nq]
@@ -177,6 +179,18 @@ def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
     kk = keys.cpu().numpy().view(np.uint64)
     valid = oi >= 0
     np.testing.assert_array_equal(kk[valid], knn_np.pack_key(od, oi)[valid])
+    if limbs == 2:
+        # binary Delta (aligned masks) reduces to the one-limb scan; either way the keys
+        # equal the forced two-limb scan's
+        nqt, KS = (nq + 15) // 16, idx_t.n_sites_pad // 64
+        wide = lut.cpu().numpy().view(np.int8)[nqt * 3 * KS * 1024 + nqt * 64:][:4].view(np.int32)[0]
+        assert wide == (0 if tie else 1)
+        os.environ["SNVRAG_KNN_NO_REDUCE"] = "1"
+        try:
+            keys2 = idx_t.scan_keys(lut, nq, 2, k)
+        finally:
+            del os.environ["SNVRAG_KNN_NO_REDUCE"]
+        torch.testing.assert_close(keys2, keys, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("tie", [False, True])
@@ -223,26 +237,31 @@ def test_panel_synth_matches_hash_restatement():
     assert (codes[:, 300:] == 0).all()
 
 
-def test_rag_mean_vs_oracle():
-    from oracle import model_np
+@pytest.mark.parametrize("nq,k", [(6, 8), (37, 32)])
+def test_rag_mean_vs_oracle(nq, k):
     rng = np.random.default_rng(9)
-    D, L, n_sites, n_ref, k = 64, 1030, 500, 200, 8
+    D, L, n_sites, n_ref = 64, 1030, 500, 200
     W = rng.standard_normal((12, D)).astype(np.float32)
     pe = rng.standard_normal((L, D)).astype(np.float32)
     Ar = rng.standard_normal((L, D)).astype(np.float32)
     panel = rng.integers(0, 2, (n_ref, n_sites)).astype(np.uint8)
-    idx = rng.integers(0, n_ref, (6, k))
+    idx = rng.integers(0, n_ref, (nq, k))
     idx[5, 3:] = -1                                    # missing neighbours are skipped
+    idx[nq - 1, :] = -1                                # no neighbour at all: site rows are zero
     from src.retrieval import PanelIndex
     pi = PanelIndex.from_alleles(panel, np.zeros(L, np.float32), DEV)
     out = K().rag_mean(torch.from_numpy(idx).to(DEV), pi.codes, n_sites, torch.from_numpy(W).to(DEV),
                        torch.from_numpy(pe).to(DEV), torch.from_numpy(Ar).to(DEV), L, torch.float32)
     toks = np.zeros((n_ref, L), np.int64)
     toks[:, 0], toks[:, 1:1 + n_sites], toks[:, 1 + n_sites] = 2, 5 + panel, 3
-    ref = np.zeros((6, L, D), np.float32)
-    for q in range(6):
+    ref = np.zeros((nq, L, D), np.float32)
+    for q in range(nq):
         v = idx[q][idx[q] >= 0]
-        ref[q] = (W[toks[v]] + pe[None] + Ar[None]).mean(0)
+        if len(v):
+            ref[q] = (W[toks[v]] + pe[None] + Ar[None]).mean(0)
+        else:
+            ref[q] = W[toks[0]] + pe + Ar
+            ref[q, 1:1 + n_sites] = pe[1:1 + n_sites] + Ar[1:1 + n_sites]
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
 
 

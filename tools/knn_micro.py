@@ -57,6 +57,10 @@ def main():
         ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 1, 0))
         print(f"scan v2 k=1 {name}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
     os.environ.pop("SNVRAG_SCAN_MODE", None)
+    lut1, _, _ = index.lut(tok, W, smask, 1)
+    for k in (1, 32):
+        ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut1, nq, 1, k, 0))
+        print(f"scan v2 1-limb k={k}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
     ms = timeit(lambda: index.lut(tok, W, smask, 2))
     print(f"lut: {ms:7.3f} ms", flush=True)
     parts = K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 32, 0)
@@ -65,6 +69,12 @@ def main():
     for pre in (False, True):
         ms = timeit(lambda: index.scan_keys(lut, nq, 2, 32, presample=pre))
         print(f"scan_keys k=32 presample={pre}: {ms:7.3f} ms", flush=True)
+    for div in (32, 128):
+        for rpp in (64, 128):
+            os.environ["SNVRAG_SAMPLE_DIV"], os.environ["SNVRAG_SAMPLE_RPP"] = str(div), str(rpp)
+            ms = timeit(lambda: index.scan_keys(lut, nq, 2, 32, presample=True))
+            print(f"scan_keys k=32 presample div={div} rpp={rpp}: {ms:7.3f} ms", flush=True)
+    os.environ.pop("SNVRAG_SAMPLE_DIV"); os.environ.pop("SNVRAG_SAMPLE_RPP")
     ms = timeit(lambda: index.search(tok, W, smask, 32))
     print(f"search k=32 (lut+scan+merge+decode): {ms:7.3f} ms", flush=True)
 
