@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 6
+#define SNVRAG_ABI_VERSION 7
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -276,6 +276,42 @@ int snvrag_evlog_enable(int capacity);
 int snvrag_evlog_pause(int paused);
 int snvrag_evlog_reset(void);
 int snvrag_evlog_read(int* kinds, float* ms, double* work, int max);
+
+/* ---------------------------------------------------------------- training --
+ * Replaces the autograd backward of model/attention/attention.py:21-31 (via
+ * multi_head_attention.py:44-51) and the trainer step of
+ * main/pretrain_with_val_optimized.py:210-245 (FocalLoss optim_schedule.py:64-96,
+ * clip_grad_norm_, fused torch.optim.Adam, cal_pr optim_schedule.py:167-203).
+ *
+ * attention_train_fwd: bf16 qkv [nseq*L, ld_qkv] (q | k | v column blocks) -> out
+ *   [nseq*L, ld_out] and lse [nseq][heads][L] f32 (log2 domain: P = exp2(c s - lse),
+ *   c = scale*log2 e).  attention_bwd: dout [nseq*L, ld_dout] -> dqkv (same layout as
+ *   qkv, bf16); d_ws f32 [nseq*heads*L] scratch (rowsum(dO o O)).  dh in {32, 64}. */
+int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv, int64_t ld_qkv,
+                               void* out, int64_t ld_out, float* lse, float scale, void* stream);
+int snvrag_attention_bwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv, int64_t ld_qkv,
+                         const void* out, int64_t ld_out, const void* dout, int64_t ld_dout,
+                         const float* lse, float* d_ws, void* dqkv, int64_t ld_dqkv, float scale, void* stream);
+/* focal loss over rows with mask[m] != 0: probs [M, C] f32 (the heads' softmax output),
+ * labels int64 [M]; loss_sum += weight * sum_m FL_m (caller zeroes it); grad [M, C] =
+ * weight * dFL/dprobs (0 on unmasked rows). */
+int snvrag_focal_loss(int64_t M, int C, const float* probs, const int64_t* labels, const uint8_t* mask,
+                      float gamma, float weight, float* loss_sum, float* grad, void* stream);
+/* acc = sum x^2 (acc is zeroed on the stream first). x 16-byte aligned. */
+int snvrag_sqnorm(int64_t n, const float* x, float* acc, void* stream);
+typedef struct {
+  float lr, beta1, beta2, eps, weight_decay;
+  float grad_scale;     /* g <- g * grad_scale (1/world for summed DDP gradients) */
+  float max_norm;       /* > 0: clip the scaled gradient to this L2 norm using *sqnorm */
+  int step;             /* 1-based */
+} snvrag_adam_t;
+/* One Adam step over a flat f32 buffer; p_bf16 (nullable) receives bf16(p_new);
+ * sqnorm (nullable) = snvrag_sqnorm of g (unscaled). */
+int snvrag_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16,
+                     const float* sqnorm, const snvrag_adam_t* a, void* stream);
+/* counts [3][C] uint64 (tp, fp, fn) += over rows with mask[m] (and mask2[m] when given). */
+int snvrag_confusion(int64_t M, int C, const float* probs, const int64_t* labels, const uint8_t* mask,
+                     const uint8_t* mask2, uint64_t* counts, void* stream);
 
 /* self tests of MFMA operand/accumulator layouts used by the kernels (GPU only):
  * returns 0 when the i8 / bf16 / f32 MFMA maps match the CPU product. */

@@ -14,37 +14,14 @@
 // buffered with register prefetch of the next 64-key tile.
 //
 // f32 path: exact-f32 VALU online softmax, one thread per query (parity mode).
-#include "common.h"
+#include "attn_common.h"
 
 namespace snvrag {
-
-constexpr int AQ = 64;     // queries per workgroup
-constexpr int AK = 64;     // keys per tile
-
-template <int DH>
-struct AttnCfg {
-  static constexpr int KS = (DH + 31) / 32;        // 32-wide MFMA k-steps over head dim
-  static constexpr int DP = KS * 32;               // padded head dim in the K tile
-  static constexpr int KROWB = DP * 2;             // bytes per K-tile row
-  static constexpr int CPR = DP / 8;               // 16-B chunks per K row
-  static constexpr int RPC = 256 / KROWB;          // rows per 256-B bank cycle
-  static constexpr int ET = DH / 16;               // 16-wide output d tiles
-  static constexpr int VT_LD = AK + 8;             // V^T row stride (bf16), padded
-  static constexpr int KBYTES = AK * KROWB;
-  static constexpr int VBYTES = DP * VT_LD * 2;
-  static constexpr int STAGE = KBYTES + VBYTES;
-};
-
-template <int DH>
-__device__ __forceinline__ int k_off(int key, int chunk) {
-  using C = AttnCfg<DH>;
-  return key * C::KROWB + ((chunk ^ ((key / C::RPC) % C::CPR)) << 4);
-}
 
 template <int DH>
 __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, const bf16* __restrict__ qkv,
                                                      long ld, bf16* __restrict__ out, long ldo,
-                                                     float scale_log2e, int nqb) {
+                                                     float scale_log2e, int nqb, float* __restrict__ lse) {
   using C = AttnCfg<DH>;
   __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE];
 
@@ -187,6 +164,8 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, con
 
   if (q < L) {
     const float inv = 1.0f / l_run;
+    // training: per-row log2-sum-exp of the scaled scores, P = exp2(s*c - lse) in the backward
+    if (lse && lg == 0) lse[((long)seq * H + h) * L + q] = m_run + log2f(l_run);
     bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * DH;
 #pragma unroll
     for (int e = 0; e < C::ET; ++e) {
@@ -542,7 +521,7 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const long nb = (long)nqb * H * nseq;
     SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
     hipLaunchKernelGGL(attn_fwd_bf16<DH>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, H,
-                       (const bf16*)qkv, ld, (bf16*)out, ldo, scale * 1.4426950408889634f, nqb);
+                       (const bf16*)qkv, ld, (bf16*)out, ldo, scale * 1.4426950408889634f, nqb, nullptr);
   } else {
     hipLaunchKernelGGL(attn_fwd_f32<DH>, dim3(cdiv(L, 64), H, (unsigned)nseq), dim3(64), 0, s,
                        (int)nseq, (int)L, H, (const float*)qkv, ld, (float*)out, ldo, scale);
@@ -563,6 +542,35 @@ extern "C" int snvrag_attention_fallbacks(int reset) {
   SNV_HIP(hipMemcpy(&v, p, sizeof(int), hipMemcpyDeviceToHost));
   if (reset) SNV_HIP(hipMemset(p, 0, sizeof(int)));
   return v;
+}
+
+// Training forward: the generic bf16 kernel (online softmax) plus the per-row log2-sum-exp
+// the backward (attention_train.hip) rebuilds P from.
+extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv,
+                                          int64_t ld_qkv, void* out, int64_t ld_out, float* lse, float scale,
+                                          void* stream) {
+  SNV_CHECK_ARG(qkv && out && lse, "null pointer");
+  SNV_CHECK_ARG(nseq >= 0 && L > 0 && heads > 0, "bad shape");
+  SNV_CHECK_ARG(ld_qkv >= 3L * heads * dh && ld_out >= (long)heads * dh, "leading dims too small");
+  SNV_CHECK_ARG(ld_qkv % 8 == 0 && ld_out % 4 == 0, "bf16 alignment");
+  if (nseq == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const int nqb = cdiv(L, AQ);
+  const long nb = (long)nqb * heads * nseq;
+  SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
+  const float sl2 = scale * 1.4426950408889634f;
+  evlog_begin(s);
+  if (dh == 32)
+    hipLaunchKernelGGL(attn_fwd_bf16<32>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse);
+  else if (dh == 64)
+    hipLaunchKernelGGL(attn_fwd_bf16<64>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse);
+  else
+    return fail(__func__, "training attention supports head dims 32 and 64");
+  SNV_LAUNCH_CHECK();
+  evlog_end(s, EV_ATTN, 4.0 * nseq * heads * (double)L * L * dh);
+  return 0;
 }
 
 extern "C" int snvrag_attention(int dtype, int64_t nseq, int64_t L, int heads, int dh,

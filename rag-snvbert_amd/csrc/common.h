@@ -20,7 +20,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 void set_error(const std::string& msg);
 
 // ---- event log (bench.py live per-kernel timing; off by default) ----
-enum EvKind { EV_GEMM = 1, EV_ATTN = 2, EV_LN = 3, EV_KNN_SCAN = 4, EV_KNN_LUT = 5, EV_MERGE = 6, EV_OTHER = 7, EV_BLOCK = 8 };
+enum EvKind { EV_GEMM = 1, EV_ATTN = 2, EV_LN = 3, EV_KNN_SCAN = 4, EV_KNN_LUT = 5, EV_MERGE = 6, EV_OTHER = 7, EV_BLOCK = 8,
+              EV_ATTN_BWD = 10, EV_TRAIN = 11 };
 bool evlog_on();
 void evlog_begin(hipStream_t s);
 void evlog_end(hipStream_t s, int kind, double work);

@@ -1,0 +1,214 @@
+"""torch.autograd Functions over the libsnvrag training kernels.
+
+The training graph (``src/train_forward.py``) is ordinary autograd; its heavy nodes
+are these Functions, whose forward and backward run the HIP kernels:
+
+  hip_linear      Linear layers on the row-panel MFMA GEMM (bf16 in, f32 accumulate):
+                  forward  y = x W^T + b             (snvrag_linear)
+                  backward dx = dy W                 (snvrag_linear on W^T)
+                           dW = dy^T x               (hipBLASLt via torch.mm — a plain
+                                                      library GEMM, long-K reduction)
+  hip_attention   unmasked softmax attention: flash forward that keeps the row
+                  log-sum-exp, FlashAttention-2 style dq / dkv backward kernels.
+  focal_loss      FocalLoss(reduction='sum') over masked rows, forward and derivative
+                  fused in one kernel.
+  rag_mean_train  K-mean of the retrieved neighbours' complete-token embeddings
+                  (embedding_rag_dataset.py:404-438 re-encode WITH grad + bert.py:176-179
+                  mean): values from the rag_mean kernel; gradients into the token
+                  table (rows tok0/tok1/<sos>/<eos>, <pad> excluded as nn.Embedding's
+                  padding_idx) and into the panel AF embedding.
+
+Master parameters stay f32 ``nn.Parameter``s; their bf16 compute copies are cached per
+parameter version (the fused Adam kernel bumps the version in place).
+"""
+
+from __future__ import annotations
+
+import weakref
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import kernels as K
+
+_BF16: Dict[tuple, list] = {}
+_MIRROR: Dict[int, tuple] = {}              # id(param) -> (weakref(param), flat-buffer bf16 view)
+_EPOCH = [0]                                # bumped after every optimizer step
+
+
+def _base_key(p: torch.Tensor):
+    base = p._base if p._base is not None else p
+    return base, (id(base), p.storage_offset(), tuple(p.shape), tuple(p.stride()))
+
+
+def bf16_of(p: torch.Tensor, transposed: bool = False) -> torch.Tensor:
+    """bf16 copy (or transposed copy) of a master parameter (or a view of one).  Entries are
+    tied to the live base tensor (weakref identity, so a freed parameter's address reused by
+    another can never hit) and to (its version, the optimizer epoch).  Parameters held in a
+    FlatParams buffer read the optimizer's bf16 mirror directly."""
+    base, key = _base_key(p)
+    if not transposed and p._base is None:
+        mv = _MIRROR.get(id(p))
+        if mv is not None and mv[0]() is p:
+            return mv[1]
+    ent = _BF16.get(key)
+    ver = (base._version, _EPOCH[0])
+    if ent is None or ent[0]() is not base or ent[1] != ver:
+        mv = _MIRROR.get(id(p)) if p._base is None else None
+        val = mv[1] if (mv is not None and mv[0]() is p) else p.detach().to(torch.bfloat16).contiguous()
+        ent = [weakref.ref(base), ver, val, None]
+        _BF16[key] = ent
+    if not transposed:
+        return ent[2]
+    if ent[3] is None:
+        ent[3] = ent[2].t().contiguous()
+    return ent[3]
+
+
+def clear_weight_cache() -> None:
+    _BF16.clear()
+
+
+def weights_updated() -> None:
+    """Called after a parameter update done outside torch's version tracking (HIP kernels)."""
+    _EPOCH[0] += 1
+    _BF16.clear()
+
+
+def register_mirror(p: torch.Tensor, view: torch.Tensor) -> None:
+    _MIRROR[id(p)] = (weakref.ref(p), view)
+
+
+class _HipLinear(torch.autograd.Function):
+    """y = x [W_1; ..; W_n]^T + [b_1; ..; b_n]: one GEMM over weights concatenated along the
+    output dim (the q/k/v Linear layers of multi_head_attention.py:44 as one N = 3D GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, n, *wb):
+        ws, bs = wb[:n], wb[n:]
+        Kd = x.shape[-1]
+        x2 = x.reshape(-1, Kd)
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        x2 = x2.contiguous()
+        w = bf16_of(ws[0]) if n == 1 else torch.cat([bf16_of(t) for t in ws], 0)
+        has_b = bs[0] is not None
+        b = torch.cat([t.detach().float().reshape(-1) for t in bs]).contiguous() if has_b else None
+        y = K.linear(x2, w, b)
+        ctx.save_for_backward(x2, *ws)
+        ctx.n, ctx.has_bias = n, has_b
+        ctx.in_shape, ctx.in_dtype = x.shape, x.dtype
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, *ws = ctx.saved_tensors
+        sizes = [t.shape[0] for t in ws]
+        g2 = gy.reshape(-1, sum(sizes))
+        if g2.dtype != torch.bfloat16:
+            g2 = g2.to(torch.bfloat16)
+        g2 = g2.contiguous()
+        gx = None
+        gws = [None] * ctx.n
+        gbs = [None] * ctx.n
+        if ctx.needs_input_grad[0]:
+            wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else \
+                torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
+            gx = K.linear(g2, wt).reshape(ctx.in_shape).to(ctx.in_dtype)
+        if any(ctx.needs_input_grad[2:2 + ctx.n]):
+            gw = torch.mm(g2.t(), x2).float()
+            gws = list(torch.split(gw, sizes, 0))
+        if ctx.has_bias:
+            gbs = list(torch.split(g2.float().sum(0), sizes, 0))
+        return (gx, None, *gws, *gbs)
+
+
+def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
+    """nn.Linear on the MFMA kernels; bf16 activations in and out.  ``weight``/``bias`` may be
+    lists (layers sharing the input, fused along the output dim)."""
+    ws = list(weight) if isinstance(weight, (list, tuple)) else [weight]
+    bs = list(bias) if isinstance(bias, (list, tuple)) else [bias] * len(ws)
+    Kd, Nn = ws[0].shape[1], sum(t.shape[0] for t in ws)
+    if Kd % 8 or Nn % 8:
+        w = torch.cat(ws, 0).to(torch.bfloat16)
+        b = torch.cat(bs, 0).to(torch.bfloat16) if bs[0] is not None else None
+        return torch.nn.functional.linear(x.to(torch.bfloat16), w, b)
+    return _HipLinear.apply(x, len(ws), *ws, *bs)
+
+
+class _HipAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, nseq, L, heads, dh):
+        qkv = qkv.contiguous()
+        out, lse = K.attention_train_fwd(qkv, nseq, L, heads, dh)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.shape = (nseq, L, heads, dh)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        qkv, out, lse = ctx.saved_tensors
+        nseq, L, heads, dh = ctx.shape
+        g = gout.to(torch.bfloat16).contiguous()
+        return K.attention_bwd(qkv, out, g, lse, nseq, L, heads, dh), None, None, None, None
+
+
+def hip_attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int) -> torch.Tensor:
+    """softmax(q k^T / sqrt(dh)) v per (sequence, head); qkv [nseq*L, 3D] bf16 -> [nseq*L, D]."""
+    return _HipAttention.apply(qkv, nseq, L, heads, dh)
+
+
+class _FocalLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, probs, labels, mask, gamma, weight):
+        loss, grad = K.focal_loss(probs.detach(), labels, mask, gamma, weight)
+        ctx.save_for_backward(grad)
+        ctx.dtype = probs.dtype
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return (grad * g).to(ctx.dtype), None, None, None, None
+
+
+def focal_loss(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, gamma: float = 2.0,
+               weight: float = 1.0) -> torch.Tensor:
+    """weight * FocalLoss(gamma, reduction='sum')(probs[mask], labels[mask]) — main/optim_schedule.py:64-96."""
+    return _FocalLoss.apply(probs, labels, mask, gamma, weight)
+
+
+class _RagMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos):
+        out = K.rag_mean(idx, codes, n_sites, W.detach().float().contiguous(), pe, Ar.detach().float().contiguous(),
+                         L, torch.bfloat16, tok0=tok0, tok1=tok1, sos=sos, eos=eos)
+        valid = idx >= 0
+        nv = valid.sum(1)
+        al = codes[idx.clamp(min=0)][:, :, :n_sites].float() * valid[:, :, None]
+        frac = al.sum(1) / nv.clamp(min=1)[:, None]                         # [nq, n_sites]
+        ctx.save_for_backward(frac, (nv > 0).float())
+        ctx.meta = (n_sites, W.shape, tok0, tok1, sos, eos)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        frac, anyq = ctx.saved_tensors
+        n, wshape, tok0, tok1, sos, eos = ctx.meta
+        G = g.float()
+        gW = torch.zeros(wshape, device=g.device, dtype=torch.float32)
+        Gs = G[:, 1:1 + n]
+        gW[tok1] += torch.einsum("qs,qsd->d", frac, Gs)
+        gW[tok0] += torch.einsum("qs,qsd->d", anyq[:, None] * (1 - frac), Gs)
+        gW[sos] += G[:, 0].sum(0)
+        if n + 1 < G.shape[1]:
+            gW[eos] += G[:, n + 1].sum(0)
+        # <pad> positions: nn.Embedding(padding_idx=0) accumulates no gradient
+        gAr = G.sum(0)
+        return gW, gAr, None, None, None, None, None, None, None, None, None
+
+
+def rag_mean_train(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, codes: torch.Tensor, n_sites: int,
+                   pe: torch.Tensor, L: int, tok0: int = 5, tok1: int = 6, sos: int = 2, eos: int = 3) -> torch.Tensor:
+    """[nq, L, D] bf16 mean of the k neighbours' complete-token embeddings, differentiable in W and Ar."""
+    return _RagMean.apply(W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos)

@@ -161,7 +161,8 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     from ..engine import engine_for
     from .. import kernels as K
     eng = engine_for(embedding_layer)
-    P = eng.packed()
+    train = embedding_layer.training
+    P = eng.packed(allow_train=True)
     dev = torch.device(device)
     h1 = batch["hap_1"].to(dev, non_blocking=True).long()
     h2 = batch["hap_2"].to(dev, non_blocking=True).long()
@@ -171,8 +172,9 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     groups = defaultdict(list)
     for i, w in enumerate(batch["window_idx"]):
         groups[int(w)].append(i)
-    rag_mean = torch.empty(2 * B, L, D, device=dev, dtype=eng.dtype)
+    rag_mean = None if train else torch.empty(2 * B, L, D, device=dev, dtype=eng.dtype)
     rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
+    rag_groups = []
     for w, rows in groups.items():
         index = ds.panel_index(w, dev)
         rows_t = torch.tensor(rows, device=dev, dtype=torch.long)
@@ -184,19 +186,28 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         # windows built from one freq table); otherwise pass both AF embeddings (exact LUT form).
         afw = af[rows_t]
         same = bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw)))
-        Ar_emb = eng.af_embedding(ref_af.unsqueeze(0)).float()[0].contiguous() if P.af is not None else None
-        Aq = Ar = None
-        if not same and P.af is not None:
-            Aq = eng.af_embedding(afw).float().contiguous()
-            Ar = Ar_emb
-        idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
-        means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
+        with torch.no_grad():
+            Ar_emb = eng.af_embedding(ref_af.unsqueeze(0), True).float()[0].contiguous() \
+                if P.af is not None else None
+            Aq = Ar = None
+            if not same and P.af is not None:
+                Aq = eng.af_embedding(afw, True).float().contiguous()
+                Ar = Ar_emb
+            idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
         nb = len(rows)
-        rag_mean[rows_t] = means[:nb]
-        rag_mean[rows_t + B] = means[nb:]
+        if train:
+            # the model re-encodes the neighbours WITH grad (train_forward.neighbour_means)
+            rag_groups.append((rows_t, idx[:nb], idx[nb:], index))
+        else:
+            means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
+            rag_mean[rows_t] = means[:nb]
+            rag_mean[rows_t + B] = means[nb:]
         rag_idx[rows_t] = idx[:nb]
         rag_idx[rows_t + B] = idx[nb:]
     batch["rag_idx_h1"], batch["rag_idx_h2"] = rag_idx[:B], rag_idx[B:]
+    if train:
+        batch["rag_groups"] = rag_groups
+        return batch
     if dense:
         raise NotImplementedError("dense [B,k,L,D] neighbour embeddings: use rag_idx_* with "
                                   "BERTEmbedding on the retrieved complete tokens")

@@ -81,13 +81,17 @@ class Engine:
         raise TypeError(f"no native engine for {type(r).__name__}")
 
     def _param_key(self):
-        return tuple((p.data_ptr(), p._version) for p in self.root.parameters()) + \
+        from .autograd_ops import _EPOCH      # in-place HIP optimizer updates bump no torch version
+        return (_EPOCH[0],) + tuple((p.data_ptr(), p._version) for p in self.root.parameters()) + \
             tuple((b.data_ptr(), b._version) for b in self.root.buffers())
 
-    def packed(self) -> _Packed:
-        if self.root.training:
-            raise NotImplementedError("native engine runs eval semantics (dropout off); call model.eval() — "
-                                      "the training kernels (backward) are not part of this round")
+    def packed(self, allow_train: bool = False) -> _Packed:
+        """Packed weights for the eval kernels.  ``allow_train``: eval semantics are wanted even
+        though the module is in train mode (retrieval search / index, which the reference also
+        runs without dropout — embedding_rag_dataset.py:358-371)."""
+        if self.root.training and not allow_train:
+            raise NotImplementedError("the native engine runs eval semantics (dropout off); train-mode "
+                                      "forwards go through src/train_forward.py (BERTFoundationModel.forward)")
         key = self._param_key()
         if self._packed is None or key != self._key:
             self._packed = self._pack()
@@ -192,9 +196,9 @@ class Engine:
         return P
 
     # ---------------------------------------------------------- sub-forwards --
-    def af_embedding(self, af: torch.Tensor) -> torch.Tensor:
+    def af_embedding(self, af: torch.Tensor, allow_train: bool = False) -> torch.Tensor:
         """AFEmbedding forward (af_embedding.py:79-91) -> [..., D] in compute dtype."""
-        P = self.packed()
+        P = self.packed(allow_train)
         a = P.af
         N.require_gpu(af)
         af = af.float().contiguous()

@@ -327,3 +327,78 @@ def encoder_ws_bytes(dtype: torch.dtype, nseq: int, L: int, D: int, heads: int) 
 
 def selftest_mfma() -> int:
     return int(N.lib().snvrag_selftest_mfma(stream_ptr()))
+
+
+# ---------------------------------------------------------------- training --
+def attention_train_fwd(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int):
+    """bf16 attention forward that also returns lse [nseq, heads, L] (log2 domain) for the backward."""
+    N.require_gpu(qkv)
+    assert qkv.dtype == torch.bfloat16
+    D = heads * dh
+    out = torch.empty(nseq * L, D, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(nseq, heads, L, device=qkv.device, dtype=torch.float32)
+    check(N.lib().snvrag_attention_train_fwd(nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1], ptr(out), D,
+                                             ptr(lse), 1.0 / float(dh) ** 0.5, stream_ptr()), "attention_train_fwd")
+    return out, lse
+
+
+def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, nseq: int, L: int,
+                  heads: int, dh: int) -> torch.Tensor:
+    """d(qkv) [nseq*L, 3D] bf16 of the unmasked softmax attention (csrc/attention_train.hip)."""
+    N.require_gpu(qkv, out, dout, lse)
+    D = heads * dh
+    dqkv = torch.empty(nseq * L, 3 * D, device=qkv.device, dtype=torch.bfloat16)
+    ws = torch.empty(nseq * heads * L, device=qkv.device, dtype=torch.float32)
+    check(N.lib().snvrag_attention_bwd(nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1], ptr(_c(out)), out.shape[-1],
+                                       ptr(_c(dout)), dout.shape[-1], ptr(_c(lse)), ptr(ws), ptr(dqkv), 3 * D,
+                                       1.0 / float(dh) ** 0.5, stream_ptr()), "attention_bwd")
+    return dqkv
+
+
+def focal_loss(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, gamma: float, weight: float,
+               loss_acc: Optional[torch.Tensor] = None):
+    """(loss_sum [1] f32 (accumulated into loss_acc when given), d(weight*loss)/dprobs)."""
+    N.require_gpu(probs)
+    Cc = probs.shape[-1]
+    M = probs.numel() // Cc
+    p = _c(probs.float().contiguous())
+    lab = labels.reshape(-1).long().contiguous()
+    msk = mask.reshape(-1).to(torch.uint8).contiguous()
+    if loss_acc is None:
+        loss_acc = torch.zeros(1, device=probs.device, dtype=torch.float32)
+    grad = torch.empty_like(p)
+    check(N.lib().snvrag_focal_loss(M, Cc, ptr(p), ptr(lab), ptr(msk), float(gamma), float(weight), ptr(loss_acc),
+                                    ptr(grad), stream_ptr()), "focal_loss")
+    return loss_acc, grad
+
+
+def sqnorm(x: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+    N.require_gpu(x)
+    assert x.dtype == torch.float32
+    if acc is None:
+        acc = torch.empty(1, device=x.device, dtype=torch.float32)
+    check(N.lib().snvrag_sqnorm(x.numel(), ptr(_c(x)), ptr(acc), stream_ptr()), "sqnorm")
+    return acc
+
+
+def adam_step(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, *, lr: float, betas=(0.9, 0.999),
+              eps: float = 1e-8, weight_decay: float = 0.0, step: int, grad_scale: float = 1.0,
+              max_norm: float = 0.0, sq: Optional[torch.Tensor] = None, p_bf16: Optional[torch.Tensor] = None):
+    N.require_gpu(p, g, m, v)
+    a = N.AdamS(lr, betas[0], betas[1], eps, weight_decay, grad_scale, max_norm, step)
+    check(N.lib().snvrag_adam_step(p.numel(), ptr(_c(p)), ptr(_c(g)), ptr(_c(m)), ptr(_c(v)), ptr(p_bf16), ptr(sq),
+                                   C.byref(a), stream_ptr()), "adam_step")
+
+
+def confusion(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, counts: torch.Tensor,
+              mask2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """counts int64 [3, C] (tp, fp, fn) += cal_pr over the masked rows, on the device."""
+    N.require_gpu(probs)
+    Cc = probs.shape[-1]
+    M = probs.numel() // Cc
+    p = probs.float().contiguous()
+    m2 = mask2.reshape(-1).to(torch.uint8).contiguous() if mask2 is not None else None
+    check(N.lib().snvrag_confusion(M, Cc, ptr(p), ptr(labels.reshape(-1).long().contiguous()),
+                                   ptr(mask.reshape(-1).to(torch.uint8).contiguous()), ptr(m2), ptr(_c(counts)),
+                                   stream_ptr()), "confusion")
+    return counts

@@ -44,6 +44,10 @@ class BERTFoundationModel(nn.Module):
         self.gt_classifier = GenotypeClassifier(2, 4)
 
     def forward(self, x):
+        if self.training:
+            # autograd graph over the HIP training kernels (src/train_forward.py)
+            from ..train_forward import forward_train
+            return forward_train(self, x)
         from ..engine import engine_for
         o = engine_for(self).forward(x)
         return [o["probs_h1"], o["probs_h2"], o["gt"], o["h1_before"], o["h2_before"],

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -60,6 +60,11 @@ class AfGateW(C.Structure):
 class GtW(C.Structure):
     _fields_ = [(n, vp) for n in ("f_w", "f_b", "n_w", "n_b", "w1", "b1", "ln_w", "ln_b",
                                   "w2", "b2", "c_w", "c_b")]
+
+
+class AdamS(C.Structure):
+    _fields_ = [("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32),
+                ("grad_scale", f32), ("max_norm", f32), ("step", C.c_int)]
 
 
 class LayerW(C.Structure):
@@ -104,6 +109,13 @@ _SIGS = {
     "snvrag_ffn_pack_bytes": ([C.c_int], sz),
     "snvrag_ffn_pack": ([C.c_int, vp, vp, vp, vp], C.c_int),
     "snvrag_ffn_forward": ([i64, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
+    "snvrag_attention_train_fwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, f32, vp], C.c_int),
+    "snvrag_attention_bwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, i64, vp, vp, vp, i64, f32, vp],
+                             C.c_int),
+    "snvrag_focal_loss": ([i64, C.c_int, vp, vp, vp, f32, f32, vp, vp, vp], C.c_int),
+    "snvrag_sqnorm": ([i64, vp, vp, vp], C.c_int),
+    "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),
+    "snvrag_confusion": ([i64, C.c_int, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

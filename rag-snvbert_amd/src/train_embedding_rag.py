@@ -1,0 +1,142 @@
+"""v18 embedding-RAG training entry point (reference: src/train_embedding_rag.py:23-420).
+
+Same command-line surface as the reference (dataset/panel/freq/window/type/pop/pos paths,
+model and optimiser hyper-parameters, rag_k, resume, output) plus:
+  --synthetic N_SAMPLES   build the data in memory (src/dataset/synthetic.py) — this image
+                          has no 1000-Genomes files and no h5py/allel to read them;
+  --max_steps N           stop an epoch after N batches (smoke runs).
+Multi-GPU: launch one process per GPU with torch.distributed.run; ranks walk the windows
+in lock-step (DistributedWindowSampler) and average gradients with bucketed RCCL
+all-reduces (src/main/optimizer.py).
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="v18 embedding-RAG SNV imputation training (MI355X)")
+    for name in ("train_dataset", "train_panel", "val_dataset", "val_panel", "refpanel_path", "freq_path",
+                 "window_path", "type_path", "pop_path", "pos_path"):
+        p.add_argument(f"--{name}", type=str, default=None)
+    p.add_argument("--dims", type=int, default=384)
+    p.add_argument("--layers", type=int, default=12)
+    p.add_argument("--attn_heads", type=int, default=12)
+    p.add_argument("--epochs", type=int, default=20)
+    p.add_argument("--train_batch_size", type=int, default=24)
+    p.add_argument("--val_batch_size", type=int, default=48)
+    p.add_argument("--lr", type=float, default=7.5e-5)
+    p.add_argument("--warmup_steps", type=int, default=15000)
+    p.add_argument("--grad_accum_steps", type=int, default=2)
+    p.add_argument("--focal_gamma", type=float, default=2.0)
+    p.add_argument("--use_recon_loss", type=str, default="false")
+    p.add_argument("--patience", type=int, default=5)
+    p.add_argument("--val_metric", type=str, default="f1")
+    p.add_argument("--min_delta", type=float, default=0.001)
+    p.add_argument("--rag_k", type=int, default=1)
+    p.add_argument("--cuda_devices", type=int, default=0)
+    p.add_argument("--num_workers", type=int, default=0)
+    p.add_argument("--resume_path", type=str, default=None)
+    p.add_argument("--resume_epoch", type=int, default=0)
+    p.add_argument("--output_path", type=str, default="output/rag_bert.model")
+    p.add_argument("--log_freq", type=int, default=500)
+    p.add_argument("--rare_threshold", type=float, default=0.05)
+    p.add_argument("--metrics_csv", type=str, default=None)
+    p.add_argument("--weight_decay", type=float, default=0.01)
+    p.add_argument("--synthetic", type=int, default=0, help="samples of in-memory synthetic data (0 = files)")
+    p.add_argument("--synthetic_sites", type=int, default=1020)
+    p.add_argument("--synthetic_windows", type=int, default=2)
+    p.add_argument("--synthetic_ref", type=int, default=256, help="panel samples (2 haplotypes each)")
+    p.add_argument("--max_steps", type=int, default=0)
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args(argv)
+
+
+def build_data(args, rank: int, world: int):
+    from .dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from .dataset.sampler import DistributedWindowSampler, WindowGroupedSampler
+    if args.synthetic:
+        from .dataset.synthetic import make_rag_dataset
+        train, vocab = make_rag_dataset(args.synthetic, args.synthetic_sites, args.synthetic_windows,
+                                        args.synthetic_ref, seed=args.seed, name="train")
+        val, _ = make_rag_dataset(max(2, args.synthetic // 4), args.synthetic_sites, args.synthetic_windows,
+                                  args.synthetic_ref, seed=args.seed + 1, name="val")
+    else:
+        raise SystemExit("reading the reference's H5/VCF inputs needs h5py and scikit-allel, which this image "
+                         "does not have; run with --synthetic N (in-memory data with the same file contract)")
+    mk = lambda ds, sampler, bs: torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler,
+                                                             num_workers=args.num_workers,
+                                                             collate_fn=embedding_rag_collate_fn)
+    if world > 1:
+        ts = DistributedWindowSampler(train, rank, world)
+        vs = DistributedWindowSampler(val, rank, world)
+    else:
+        ts, vs = WindowGroupedSampler(train, shuffle=True, seed=args.seed), WindowGroupedSampler(val, shuffle=False)
+    return mk(train, ts, args.train_batch_size), mk(val, vs, args.val_batch_size), vocab
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(args.cuda_devices)))
+    if not torch.cuda.is_available():
+        raise SystemExit("training runs on the MI355X kernels only (no CPU fallback)")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    torch.manual_seed(args.seed + rank)
+    train_loader, val_loader, vocab = build_data(args, rank, world)
+    from .main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
+    from .model import build_model
+    model = build_model(len(vocab), args.dims, args.layers, args.attn_heads).to(dev)
+    if world > 1:   # identical initial weights on every rank
+        import torch.distributed as dist
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, 0)
+    trainer = BERTTrainerWithValidationOptimized(
+        model, train_loader, val_loader, vocab, lr=args.lr, weight_decay=args.weight_decay,
+        warmup_steps=args.warmup_steps, log_freq=args.log_freq, grad_accum_steps=args.grad_accum_steps,
+        focal_gamma=args.focal_gamma, use_recon_loss=args.use_recon_loss.lower() == "true",
+        patience=args.patience, val_metric=args.val_metric, min_delta=args.min_delta,
+        rare_threshold=args.rare_threshold, output_csv=args.metrics_csv if rank == 0 else None)
+    trainer.rag_k = args.rag_k
+    start = 0
+    if args.resume_path:
+        start = trainer.load(args.resume_path) + 1 if not args.resume_epoch else args.resume_epoch
+    if args.max_steps:
+        import itertools
+
+        class _Cap:
+            def __init__(self, dl, n):
+                self.dl, self.n, self.dataset = dl, n, dl.dataset
+
+            def __iter__(self):
+                return itertools.islice(iter(self.dl), self.n)
+
+        trainer.train_data = _Cap(train_loader, args.max_steps)
+        trainer.val_data = _Cap(val_loader, args.max_steps)
+    for epoch in range(start, args.epochs):
+        ds = train_loader.dataset
+        if epoch > 0 and hasattr(ds, "regenerate_masks"):
+            ds.current_epoch = epoch
+            ds.regenerate_masks(seed=epoch)
+        trainer.train(epoch)
+        res = trainer.validate(epoch)
+        trainer.save(epoch, args.output_path)
+        if epoch % 2 == 1 and hasattr(ds, "add_level"):
+            ds.add_level()
+        if trainer.should_stop_early(res):
+            break
+    return trainer
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

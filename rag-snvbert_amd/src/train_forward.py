@@ -1,0 +1,208 @@
+"""Training-mode forward of the v18 model as an autograd graph over the HIP kernels.
+
+Semantics follow the reference in train mode (dropout active, BatchNorm batch
+statistics with running-stat updates), call stack model/foundation_model.py:25-33 ->
+model/bert.py:148-219:
+
+  BERTEmbedding (embedding/bert.py:53-75)      W[tok] + pe + AFEmbedding(af) -> dropout
+  neighbour K-mean (bert.py:171-183)           rag_mean_train (autograd_ops) or a given
+                                               rag_emb_h1/h2 [B, K, L, D] averaged over K
+  EmbeddingFusionModule x4 (fusion.py:336-369) one [4B, L, D] GEMM + rank-2 pos/af terms
+  EnhancedRareVariantFusion x2 (fusion.py:131-162)
+  12 TransformerBlocks (transformer.py:32-35) h1 and h2 batched into one 2B dimension
+  EnhancedHaplotypeClassifier, GenotypeClassifier (foundation_model.py:64-80, :156-176)
+
+Heavy nodes (every Linear with K, N multiples of 8, attention) run on libsnvrag through
+``autograd_ops``; the small per-site MLPs, LayerNorm, activations and dropout are torch
+elementwise kernels.  Differences from the reference, all in the stochastic parts:
+  * the attention-probability dropout (attention.py:28-29) is not applied;
+  * EnhancedRareVariantFusion's AF gate (af_adapter) is computed once per sample and
+    shared by the h1 and h2 calls (the reference computes it twice with independent
+    dropout masks; without dropout the two are identical);
+  * the neighbour mean is taken over the k complete-token embeddings before dropout
+    (the reference drops each neighbour's embedding independently, then averages).
+With dropout p = 0 the graph computes the reference's train-mode function exactly
+(up to bf16 rounding) — the gradient parity tests run it that way.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .autograd_ops import hip_attention, hip_linear, rag_mean_train
+
+T = torch.bfloat16
+
+
+def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
+    return F.dropout(x, p, training) if (training and p > 0) else x
+
+
+def af_embedding(afm, af: torch.Tensor) -> torch.Tensor:
+    """AFEmbedding.forward (af_embedding.py:70-91) -> [..., D] bf16."""
+    x = af.float().unsqueeze(-1) * afm.basis_freqs
+    feat = torch.cat([torch.sin(2 * math.pi * x), torch.cos(2 * math.pi * x)], -1)
+    pr = afm.projection
+    h = hip_linear(feat, pr[0].weight, pr[0].bias)
+    h = F.gelu(_ln(h, pr[1])).to(T)
+    return hip_linear(h, pr[3].weight, pr[3].bias)
+
+
+def pos_feat(pfm, pos: torch.Tensor) -> torch.Tensor:
+    """PositionFeatModule.forward (fusion.py:317-332), f32, BatchNorm in the module's mode."""
+    out = pos.float().unsqueeze(1)
+    out = pfm.norm1(F.leaky_relu(pfm.conv1(out), 0.05))
+    out = pfm.norm2(F.leaky_relu(pfm.conv2(out), 0.05))
+    return F.leaky_relu(pfm.conv3(out), 0.05).squeeze(1)
+
+
+def _linear_cat2(x: torch.Tensor, lin, c1: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
+    """Linear(cat([x, c1, c2], -1)) with the two extra input columns as rank-1 terms (f32)."""
+    D = x.shape[-1]
+    W = lin.weight
+    y = hip_linear(x, W[:, :D], lin.bias).float()
+    return y + c1.unsqueeze(-1) * W[:, D] + c2.unsqueeze(-1) * W[:, D + 1]
+
+
+def _ln(x: torch.Tensor, m) -> torch.Tensor:
+    """LayerNorm in f32 (statistics and affine), f32 out."""
+    return F.layer_norm(x.float(), (x.shape[-1],), m.weight, m.bias, m.eps)
+
+
+def emb_fusion(ef, embs: torch.Tensor, pos: torch.Tensor, af: torch.Tensor, n_calls: int) -> torch.Tensor:
+    """EmbeddingFusionModule.forward (fusion.py:351-369) for n_calls stacked [B, L, D] inputs.
+    pos_feat runs once per reference call (its BatchNorm running statistics update each time;
+    the batch-statistics output is identical)."""
+    pf = pos_feat(ef.pos_feat, pos)
+    if ef.pos_feat.training:
+        with torch.no_grad():
+            for _ in range(n_calls - 1):
+                pos_feat(ef.pos_feat, pos)
+    rep = lambda t: t.repeat(n_calls, 1)
+    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1)
+    return _ln(embs.float() + y, ef.norm).to(T)
+
+
+def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p: torch.Tensor, p: float,
+               training: bool) -> torch.Tensor:
+    """EnhancedRareVariantFusion.forward (fusion.py:131-162) for h1 and h2 stacked as [2B, L, D]
+    (K = 1 after the neighbour mean, so the pooling softmax weight is exactly 1)."""
+    ai = rf.af_interaction
+    comb = torch.stack([af, af_p], -1)
+    gate = torch.sigmoid(F.linear(F.gelu(F.linear(comb, ai.gate_net[0].weight, ai.gate_net[0].bias)),
+                                  ai.gate_net[2].weight, ai.gate_net[2].bias))
+    enc = F.gelu(_ln(F.linear(comb, ai.joint_encoder[0].weight, ai.joint_encoder[0].bias), ai.joint_encoder[1]))
+    fused_af = af.unsqueeze(-1) + ai.res_scale * (gate * enc)
+    ad = rf.af_adapter
+    w = _drop(F.gelu(hip_linear(fused_af, ad[0].weight, ad[0].bias)), p, training)
+    w = torch.sigmoid(hip_linear(w, ad[3].weight, ad[3].bias).float())            # [B, L, D]
+    w2 = w.repeat(2, 1, 1)
+    pooled = (rag.float() * w2).to(T)
+    fu = rf.fusion
+    h = _drop(F.gelu(hip_linear(torch.cat([orig, pooled], -1), fu[0].weight, fu[0].bias)), p, training)
+    h = _ln(hip_linear(h, fu[3].weight, fu[3].bias), fu[4]).float()
+    af2 = af.repeat(2, 1)
+    maf = torch.minimum(af2, 1 - af2).unsqueeze(-1)
+    mw = torch.log1p(1.0 / (maf + 1e-6)).clamp(max=3.0)
+    return (orig.float() + rf.res_scale * (h * mw)).to(T)
+
+
+def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, training: bool) -> torch.Tensor:
+    """TransformerBlock.forward (transformer.py:32-35), eval-identical except dropout."""
+    a = blk.attention
+    D = x.shape[-1]
+    ll = a.linear_layers
+    qkv = hip_linear(x.reshape(-1, D), [ll[0].weight, ll[1].weight, ll[2].weight],
+                     [ll[0].bias, ll[1].bias, ll[2].bias])
+    att = hip_attention(qkv, nseq, L, a.heads, a.dims)
+    o = hip_linear(att, a.output_layer.weight, a.output_layer.bias).reshape(x.shape)
+    x = _drop(_ln(x + o, blk.input_sublayer.norm).to(T), p, training)
+    ff = blk.feed_forward
+    h = F.leaky_relu(hip_linear(x, ff.w_1.weight, ff.w_1.bias), 0.1)
+    f = _drop(F.leaky_relu(hip_linear(_ln(h, ff.norm).to(T), ff.w_2.weight, ff.w_2.bias), 0.1), p, training)
+    x = _drop(_ln(x + f, blk.output_sublayer.norm).to(T), p, training)
+    return _drop(x, p, training)
+
+
+def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
+    """[2B, L, D] bf16: given dense rag embeddings (mean over K) or retrieved indices + panels."""
+    if "rag_emb_h1" in x:
+        out = []
+        for key in ("rag_emb_h1", "rag_emb_h2"):
+            r = x[key]
+            r = r.mean(1) if r.dim() == 4 else r
+            out.append(r.to(T))
+        return torch.cat(out, 0)
+    groups = x.get("rag_groups")
+    if not groups:
+        return None
+    emb = bert.embedding
+    D = emb.embed_size
+    pe = emb.position.pe[0, :L].float().contiguous()
+    rows_out: List[torch.Tensor] = []
+    vals: List[torch.Tensor] = []
+    for rows, idx_h1, idx_h2, index in groups:
+        Ar = af_embedding(emb.af_embedding, index.ref_af.view(1, -1))[0].float() if emb.use_af else \
+            torch.zeros(L, D, device=pe.device)
+        idx = torch.cat([idx_h1, idx_h2], 0)
+        m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L)
+        nb = rows.numel()
+        rows_out += [rows, rows + B]
+        vals += [m[:nb], m[nb:]]
+    order = torch.cat(rows_out)
+    stacked = torch.cat(vals, 0)
+    out = torch.empty_like(stacked)
+    out[order] = stacked
+    return out
+
+
+def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
+    """BERTFoundationModel.forward in train mode -> the reference's 7-element output list."""
+    bert = fm.bert
+    training = fm.training
+    p = bert.embedding.dropout.p
+    h1, h2 = x["hap_1"].long(), x["hap_2"].long()
+    B, L = h1.shape
+    dev = h1.device
+    g = lambda k: x[k].to(dev, torch.float32)
+    af, pos = g("af"), g("pos")
+    af_p = g("af_p") if "af_p" in x else af
+    emb = bert.embedding
+    D = emb.embed_size
+    # 1. query embeddings (embedding/bert.py:63-75); h1 and h2 stacked
+    tok = torch.cat([h1, h2], 0)
+    e = F.embedding(tok, emb.tokenizer.weight, padding_idx=0) + emb.position.pe[:, :L]
+    if emb.use_af:
+        e = e + af_embedding(emb.af_embedding, af).float().repeat(2, 1, 1)
+    h_raw = _drop(e.to(T), p, training)                                          # [2B, L, D]
+    rag = neighbour_means(bert, x, B, L)
+    if rag is not None:
+        rag = _drop(rag, p, training)
+        fused = emb_fusion(bert.emb_fusion, torch.cat([h_raw, rag], 0), pos, af, 4)
+        hx = rag_fusion(bert.rag_fusion, fused[:2 * B], fused[2 * B:], af, af_p, p, training)
+    else:
+        hx = emb_fusion(bert.emb_fusion, h_raw, pos, af, 2)
+    # 2. encoder (bert.py:213-217), both haplotypes in one batch
+    for blk in bert.transformer_blocks:
+        hx = transformer_block(blk, hx, 2 * B, L, p, training)
+    # 3. heads (foundation_model.py:25-33)
+    hc = fm.hap_classifier
+    af2, afp2 = af.repeat(2, 1), af_p.repeat(2, 1)
+    hh = F.gelu(_linear_cat2(hx, hc.af_fusion[0], af2, afp2).to(T))
+    hh = _ln(hip_linear(hh, hc.af_fusion[2].weight, hc.af_fusion[2].bias), hc.af_fusion[3]).to(T)
+    hh = F.gelu(hip_linear(hh, hc.net[0].weight, hc.net[0].bias))
+    logits = F.linear(hh.float(), hc.net[2].weight, hc.net[2].bias)
+    probs = torch.softmax(logits, -1)
+    p1, p2 = probs[:B], probs[B:]
+    gc = fm.gt_classifier
+    gf = torch.cat([p1, p2, g("ref").unsqueeze(-1), g("het").unsqueeze(-1), g("hom").unsqueeze(-1)], -1)
+    gf = _ln(F.leaky_relu(gc.gf_fusion(gf), 0.01), gc.gf_norm)
+    ff = gc.layer
+    gf = F.leaky_relu(ff.w_1(gf), 0.1)
+    gf = _drop(F.leaky_relu(ff.w_2(_ln(gf, ff.norm)), 0.1), ff.dropout.p, training)
+    gt = torch.softmax(gc.classifier(gf), -1)
+    return [p1, p2, gt, h_raw[:B], h_raw[B:], hx[:B], hx[B:]]
