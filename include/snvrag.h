@@ -313,6 +313,12 @@ int snvrag_adam_step(int64_t n, float* p, const float* g, float* m, float* v, vo
 int snvrag_confusion(int64_t M, int C, const float* probs, const int64_t* labels, const uint8_t* mask,
                      const uint8_t* mask2, uint64_t* counts, void* stream);
 
+/* Inference post-processing (replaces infer_embedding_rag.py:145-152): probs_h1/h2 [M, 2]
+ * f32 head probabilities -> p1, p2 [M] = softmax(probs)[..., 1] (the reference's second
+ * softmax) and gt [M, 4] = (p00, p01, p10, p11).  gt 16-byte aligned. */
+int snvrag_infer_post(int64_t M, const float* probs_h1, const float* probs_h2, float* p1, float* p2,
+                      float* gt, void* stream);
+
 /* self tests of MFMA operand/accumulator layouts used by the kernels (GPU only):
  * returns 0 when the i8 / bf16 / f32 MFMA maps match the CPU product. */
 int snvrag_selftest_mfma(void* stream);

@@ -370,3 +370,36 @@ extern "C" int snvrag_gt_head(int64_t M, const float* p1, const float* p2, const
   SNV_LAUNCH_CHECK();
   return 0;
 }
+
+// --------------------------------------------------------- infer post-process --
+// infer_embedding_rag.py:145-152: the heads' probabilities go through softmax AGAIN,
+// p = softmax(probs)[..., 1]; gt = [(1-p1)(1-p2), (1-p1)p2, p1(1-p2), p1 p2].
+__global__ __launch_bounds__(256) void infer_post_kernel(long M, const float* __restrict__ ph1,
+                                                         const float* __restrict__ ph2, float* __restrict__ p1o,
+                                                         float* __restrict__ p2o, float* __restrict__ gt) {
+  const long m = (long)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  auto p_alt = [](float a, float b) {          // softmax([a, b])[1]
+    const float mx = fmaxf(a, b), ea = expf(a - mx), eb = expf(b - mx);
+    return eb / (ea + eb);
+  };
+  const float p1 = p_alt(ph1[2 * m], ph1[2 * m + 1]), p2 = p_alt(ph2[2 * m], ph2[2 * m + 1]);
+  p1o[m] = p1;
+  p2o[m] = p2;
+  f32x4 g;
+  g[0] = (1.f - p1) * (1.f - p2);
+  g[1] = (1.f - p1) * p2;
+  g[2] = p1 * (1.f - p2);
+  g[3] = p1 * p2;
+  reinterpret_cast<f32x4*>(gt)[m] = g;
+}
+
+extern "C" int snvrag_infer_post(int64_t M, const float* probs_h1, const float* probs_h2, float* p1, float* p2,
+                                 float* gt, void* stream) {
+  SNV_CHECK_ARG(probs_h1 && probs_h2 && p1 && p2 && gt && ((uintptr_t)gt % 16) == 0, "null or misaligned pointer");
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(infer_post_kernel, dim3(cdiv(M, 256)), dim3(256), 0, as_stream(stream), (long)M, probs_h1,
+                     probs_h2, p1, p2, gt);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}

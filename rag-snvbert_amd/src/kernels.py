@@ -402,3 +402,15 @@ def confusion(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, cou
                                    ptr(mask.reshape(-1).to(torch.uint8).contiguous()), ptr(m2), ptr(_c(counts)),
                                    stream_ptr()), "confusion")
     return counts
+
+
+def infer_post(probs_h1: torch.Tensor, probs_h2: torch.Tensor):
+    """(p1, p2 [...], gt [..., 4]) of infer_embedding_rag.py:145-152 (second softmax included)."""
+    N.require_gpu(probs_h1, probs_h2)
+    a, b = probs_h1.float().contiguous(), probs_h2.float().contiguous()
+    M = a.numel() // 2
+    p1 = torch.empty(a.shape[:-1], device=a.device, dtype=torch.float32)
+    p2 = torch.empty_like(p1)
+    gt = torch.empty(*a.shape[:-1], 4, device=a.device, dtype=torch.float32)
+    check(N.lib().snvrag_infer_post(M, ptr(a), ptr(b), ptr(p1), ptr(p2), ptr(gt), stream_ptr()), "infer_post")
+    return p1, p2, gt

@@ -116,6 +116,7 @@ _SIGS = {
     "snvrag_sqnorm": ([i64, vp, vp, vp], C.c_int),
     "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),
     "snvrag_confusion": ([i64, C.c_int, vp, vp, vp, vp, vp, vp], C.c_int),
+    "snvrag_infer_post": ([i64, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

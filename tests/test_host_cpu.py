@@ -91,3 +91,17 @@ def test_state_dict_keys_match_reference_fixture():
         sd = synthetic.synth_state_dict(model_state_shapes(cfg["vocab"], cfg["d"], cfg["layers"], cfg["heads"]),
                                         cfg["seed"])
         assert synthetic.state_dict_digest(sd) == cfg["sd_digest"]
+
+
+def test_infer_geometry_matches_oracle():
+    from src.infer_embedding_rag import geometry
+    from oracle import data_np
+    rng = np.random.default_rng(1)
+    W, S, L = 3, 4, 1030
+    h1, h2 = rng.random((W * S, L)), rng.random((W * S, L))
+    gt, mask = rng.random((W * S, L, 4)), rng.integers(0, 2, (W * S, L))
+    for n_var in (2000, 3500):
+        got = geometry(h1, h2, gt, mask, W, n_var, 1020)
+        exp = data_np.infer_geometry(h1, h2, gt, mask, W, n_var, 1020)
+        for a, b in zip(got, exp):
+            np.testing.assert_array_equal(a, b)
