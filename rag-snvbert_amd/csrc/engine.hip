@@ -24,11 +24,14 @@ static int64_t chunk_seqs(int64_t nseq, int64_t L, int D, int esz) {
   }
   // The row-panel GEMMs tile M by 128 rows with whole output rows per tile, so a chunk
   // must hold >= ~4 tiles per CU (1024 tiles = 131k rows) to fill 256 CUs; cap the
-  // per-chunk workspace (10 D / token) at ~4 GB of the 288 GB HBM.
+  // per-chunk workspace (10 D / token) at ~16 GB of the 288 GB HBM; chunks are balanced
+  // (a 505 + 7 split would run the 7-sequence chunk at a fraction of the chip).
   const double per_seq = (double)L * D * 10.0 * esz;
-  int64_t c = (int64_t)(4.0e9 / per_seq);
+  int64_t c = (int64_t)(16.0e9 / per_seq);
   if (c < 1) c = 1;
-  return std::min<int64_t>(c, nseq);
+  if (c >= nseq) return nseq;
+  const int64_t nchunks = (nseq + c - 1) / c;
+  return (nseq + nchunks - 1) / nchunks;
 }
 
 }  // namespace snvrag

@@ -527,7 +527,7 @@ template <int KS, int LIMBS, int QTW, int MODE>
 __device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict__ codes, long n_ref, long ld,
                                            const int8_t* __restrict__ lut, const int* __restrict__ mult, int nq,
                                            int k, long range, long ref_offset, uint64_t* __restrict__ parts,
-                                           const int* __restrict__ th_init) {
+                                           const int* __restrict__ th_init, int part, int group) {
   constexpr int ROWB = KS * 64;                        // staged row bytes
   constexpr int STAGE = S2_R * ROWB;
   constexpr int PPW = STAGE / 1024 / 8;                // glds pieces per wave per stage
@@ -538,9 +538,8 @@ __device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int nqt = (nq + 15) >> 4;
-  const int qt0 = blockIdx.y * 8 + wave * QTW;
+  const int qt0 = group * 8 + wave * QTW;
   const bool active = wave * QTW < 8 && qt0 < nqt;     // wave-uniform; every wave still loads + syncs
-  const int part = blockIdx.x;
   const long r_begin = (long)part * range;
   const long r_end = min(n_ref, r_begin + range);
   const int nstage = r_end > r_begin ? (int)((r_end - r_begin + S2_R - 1) / S2_R) : 0;
@@ -713,18 +712,27 @@ template <int KS, int LIMBS, int MODE = 0>
 __global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ codes, long n_ref, long ld,
                                                     const int8_t* __restrict__ lut, int nq, int k, long range,
                                                     long ref_offset, uint64_t* __restrict__ parts,
-                                                    const int* __restrict__ th_init, const int* __restrict__ wide) {
+                                                    const int* __restrict__ th_init, const int* __restrict__ wide,
+                                                    int n_parts, int n_groups) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // XCD co-scheduling: the G query groups of one panel range get consecutive dispatch
+  // slots 8 apart (same XCD, same round), so the range streams from HBM once and the
+  // other G-1 workgroups read it from that XCD's L2 (one pass over the panel per launch)
+  const int i = blockIdx.x, G = n_groups;
+  const int slot = i / 8, group = slot % G, part = (slot / G) * 8 + i % 8;
+  if (part >= n_parts) return;                        // whole workgroup, before any barrier
   if constexpr (LIMBS == 2 && KS <= 16) {   // (KS = 20: two tiles of A would spill)
     if (wide && *wide == 0) {
       const long nqt = (nq + 15) >> 4;
       const int8_t* lut1 = lut + nqt * 2 * KS * 1024;
       const int* mult = reinterpret_cast<const int*>(lut1 + nqt * KS * 1024);
-      scan2_body<KS, 1, S2_QTW1, MODE>(smem, codes, n_ref, ld, lut1, mult, nq, k, range, ref_offset, parts, th_init);
+      scan2_body<KS, 1, S2_QTW1, MODE>(smem, codes, n_ref, ld, lut1, mult, nq, k, range, ref_offset, parts, th_init,
+                                       part, group);
       return;
     }
   }
-  scan2_body<KS, LIMBS, 1, MODE>(smem, codes, n_ref, ld, lut, nullptr, nq, k, range, ref_offset, parts, th_init);
+  scan2_body<KS, LIMBS, 1, MODE>(smem, codes, n_ref, ld, lut, nullptr, nq, k, range, ref_offset, parts, th_init,
+                                 part, group);
 }
 
 template <int KS, int LB>
@@ -741,8 +749,10 @@ static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* code
     if (m && m[0] == '2') kern = scan2_kernel<KS, LB, 2>;
   }
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  dim3 g((unsigned)n_parts, (unsigned)(((nq + 15) / 16 + 7) / 8));
-  hipLaunchKernelGGL(kern, g, dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th, wide);
+  const int G = ((nq + 15) / 16 + 7) / 8;
+  const long nwg = (long)((n_parts + 7) / 8) * 8 * G;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th,
+                     wide, n_parts, G);
 }
 
 static int scan_parts(long n_ref) {
