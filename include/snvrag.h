@@ -313,6 +313,19 @@ int snvrag_adam_step(int64_t n, float* p, const float* g, float* m, float* v, vo
 int snvrag_confusion(int64_t M, int C, const float* probs, const int64_t* labels, const uint8_t* mask,
                      const uint8_t* mask2, uint64_t* counts, void* stream);
 
+/* Training LayerNorm (sublayer.py:15-16, feed_forward.py:20, nn.LayerNorm under autograd):
+ * y = LN(x + r) g + b, bf16 [M, N] in/out (r nullable), f32 statistics; writes s = bf16(x + r)
+ * (when r is given) and stats [M] = (mean, rstd) for the backward, which returns
+ * ds (= dx = dr, bf16), dg, db (f32 [N]).  N % 8 == 0, N <= 2048. */
+int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
+                        float eps, void* y, void* s_out, float* stats, void* stream);
+size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N);
+int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
+                  void* ds, float* dg, float* db, void* ws, size_t ws_bytes, void* stream);
+/* out[n] = sum_m x[m, n] for a bf16 [M, N] matrix (Linear bias gradients), f32 out. */
+size_t snvrag_colsum_ws_bytes(int64_t M, int N);
+int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, size_t ws_bytes, void* stream);
+
 /* Inference post-processing (replaces infer_embedding_rag.py:145-152): probs_h1/h2 [M, 2]
  * f32 head probabilities -> p1, p2 [M] = softmax(probs)[..., 1] (the reference's second
  * softmax) and gt [M, 4] = (p00, p01, p10, p11).  gt 16-byte aligned. */

@@ -174,3 +174,252 @@ extern "C" int snvrag_confusion(int64_t M, int C, const float* probs, const int6
   SNV_LAUNCH_CHECK();
   return 0;
 }
+
+// ------------------------------------------------------- LayerNorm (training) --
+// y = LN(x + r) * g + b over rows of N (sublayer.py:15-16 / nn.LayerNorm), bf16 in/out,
+// f32 statistics.  Forward keeps s = x + r (bf16, only when r is given) and (mean, rstd)
+// per row for the backward:
+//   xh = (s - mean) * rstd,  gy = dy * g
+//   ds = rstd * (gy - mean_n(gy) - xh * mean_n(gy * xh))       (= dx = dr)
+//   dg = sum_rows dy * xh,  db = sum_rows dy                   (per-block partials)
+// One wave per row, lanes over 8-column chunks.
+namespace snvrag {
+constexpr int LN_MAXC = 4;   // 8-col chunks per lane: N <= 64 * 8 * 4 = 2048
+
+__device__ __forceinline__ void ld8bf(const bf16* p, float* v) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(a[e] << 16);
+    v[2 * e + 1] = __uint_as_float(a[e] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8bf(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = (bf16)v[e];
+  *reinterpret_cast<bf16x8*>(p) = a;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ r, const float* __restrict__ g,
+                                                           const float* __restrict__ b, float eps,
+                                                           bf16* __restrict__ y, bf16* __restrict__ s_out,
+                                                           float2* __restrict__ stats) {
+  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  const int nc = N / 8;
+  float v[LN_MAXC][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c) {
+    const int cc = lane + 64 * c;
+    if (cc < nc) {
+      ld8bf(x + m * N + 8 * cc, v[c]);
+      if (r) {
+        float t[8];
+        ld8bf(r + m * N + 8 * cc, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)(v[c][j] + t[j]);   // s is kept in bf16
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[c][j];
+    }
+  }
+  const float mean = wave_sum(sum) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c)
+    if (lane + 64 * c < nc)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; q += d * d; }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / N + eps);
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c) {
+    const int cc = lane + 64 * c;
+    if (cc < nc) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * g[8 * cc + j] + b[8 * cc + j];
+      st8bf(y + m * N + 8 * cc, o);
+      if (s_out) st8bf(s_out + m * N + 8 * cc, v[c]);
+    }
+  }
+  if (lane == 0) stats[m] = make_float2(mean, rstd);
+}
+
+// RPB rows per block (one wave each, looping): the block's dg/db partials go to
+// part[blockIdx.x][2][N]
+__global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per_wave, const bf16* __restrict__ dy,
+                                                     const bf16* __restrict__ s, const float2* __restrict__ stats,
+                                                     const float* __restrict__ g, bf16* __restrict__ ds,
+                                                     float* __restrict__ part) {
+  extern __shared__ float red[];                      // [4 waves][2][N]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = N / 8;
+  float dgp[LN_MAXC][8], dbp[LN_MAXC][8];
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dgp[c][j] = dbp[c][j] = 0.f;
+  const long r0 = ((long)blockIdx.x * 4 + wave) * rows_per_wave;
+  for (int i = 0; i < rows_per_wave; ++i) {
+    const long m = r0 + i;
+    if (m >= M) break;
+    const float2 st = stats[m];
+    float xh[LN_MAXC][8], gy[LN_MAXC][8];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+      const int cc = lane + 64 * c;
+      if (cc < nc) {
+        float dv[8];
+        ld8bf(s + m * N + 8 * cc, xh[c]);
+        ld8bf(dy + m * N + 8 * cc, dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xh[c][j] - st.x) * st.y;
+          gy[c][j] = dv[j] * g[8 * cc + j];
+          a1 += gy[c][j];
+          a2 += gy[c][j] * xh[c][j];
+          dgp[c][j] += dv[j] * xh[c][j];
+          dbp[c][j] += dv[j];
+        }
+      }
+    }
+    a1 = wave_sum(a1) / N;
+    a2 = wave_sum(a2) / N;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+      const int cc = lane + 64 * c;
+      if (cc < nc) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = st.y * (gy[c][j] - a1 - xh[c][j] * a2);
+        st8bf(ds + m * N + 8 * cc, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c) {
+    const int cc = lane + 64 * c;
+    if (cc < nc)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * 2 + 0) * N + 8 * cc + j] = dgp[c][j];
+        red[(wave * 2 + 1) * N + 8 * cc + j] = dbp[c][j];
+      }
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < 2 * N; n += 256) {
+    const int which = n / N, col = n % N;
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc += red[(w * 2 + which) * N + col];
+    part[(long)blockIdx.x * 2 * N + n] = acc;
+  }
+}
+
+// out[n] (+)= sum over rows r of x[r, n] (f32 partials [R, N] -> N, or bf16 [M, N] -> N)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(long R, int N, const T* __restrict__ x, float* __restrict__ out,
+                                                     int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (long r = 0; r < R; ++r) acc += to_f32(x[r * N + n]);
+  out[n] = accumulate ? out[n] + acc : acc;
+}
+
+// column sums of a bf16 [M, N] matrix (bias gradients): per-block partials over row slabs
+__global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, int rows_per_block, const bf16* __restrict__ x,
+                                                          float* __restrict__ part) {
+  const int nc = N / 8;
+  const int per = 256 / nc;                         // row lanes per block (>= 1)
+  const int c = threadIdx.x % nc, rl = threadIdx.x / nc;
+  extern __shared__ float red2[];                   // [per][N]
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rl < per) {
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(M, r0 + rows_per_block);
+    for (long m = r0 + rl; m < r1; m += per) {
+      float v[8];
+      ld8bf(x + m * N + 8 * c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red2[rl * N + 8 * c + j] = acc[j];
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float s = 0.f;
+    for (int w = 0; w < per; ++w) s += red2[w * N + n];
+    part[(long)blockIdx.x * N + n] = s;
+  }
+}
+}  // namespace snvrag
+
+extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
+                                   float eps, void* y, void* s_out, float* stats, void* stream) {
+  SNV_CHECK_ARG(x && g && b && y && stats, "null pointer");
+  SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
+  SNV_CHECK_ARG(!r || s_out, "a residual needs s_out");
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(ln_fwd_train_kernel, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N,
+                     (const bf16*)x, (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N) {
+  const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
+  return (size_t)nblk * 2 * N * sizeof(float);
+}
+
+extern "C" int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
+                             void* ds, float* dg, float* db, void* ws, size_t ws_bytes, void* stream) {
+  SNV_CHECK_ARG(dy && s && stats && g && ds && dg && db && ws, "null pointer");
+  SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
+  SNV_CHECK_ARG(ws_bytes >= snvrag_ln_bwd_ws_bytes(M, N), "workspace too small");
+  if (M == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
+  const int rpw = (int)((M + nblk * 4 - 1) / (nblk * 4));
+  float* part = (float*)ws;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nblk), dim3(256), 4 * 2 * N * sizeof(float), st, (long)M, N, rpw,
+                     (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, part);
+  SNV_LAUNCH_CHECK();
+  // reduce the [nblk][2][N] partials: dg = part[:, 0, :], db = part[:, 1, :]
+  hipLaunchKernelGGL(colsum_kernel<float>, dim3(cdiv(2 * N, 256)), dim3(256), 0, st, (long)nblk, 2 * N,
+                     (const float*)part, part, 0);   // rows of 2N: in-place into row 0 (read-before-write per column)
+  SNV_LAUNCH_CHECK();
+  SNV_HIP(hipMemcpyAsync(dg, part, N * sizeof(float), hipMemcpyDeviceToDevice, st));
+  SNV_HIP(hipMemcpyAsync(db, part + N, N * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+extern "C" size_t snvrag_colsum_ws_bytes(int64_t M, int N) {
+  const long nblk = std::min<long>(cdiv(M, 256), 1024);
+  return (size_t)nblk * N * sizeof(float);
+}
+
+extern "C" int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  SNV_CHECK_ARG(x && out && ws, "null pointer");
+  SNV_CHECK_ARG(N % 8 == 0 && N / 8 <= 256, "N must be a multiple of 8, <= 2048");
+  SNV_CHECK_ARG(ws_bytes >= snvrag_colsum_ws_bytes(M, N), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  if (M == 0) return (int)hipMemsetAsync(out, 0, N * sizeof(float), st);
+  const long nblk = std::min<long>(cdiv(M, 256), 1024);
+  const int rpb = (int)((M + nblk - 1) / nblk);
+  const int per = 256 / (N / 8);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)nblk), dim3(256), per * N * sizeof(float), st, (long)M, N,
+                     rpb, (const bf16*)x, (float*)ws);
+  SNV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_kernel<float>, dim3(cdiv(N, 256)), dim3(256), 0, st, (long)nblk, N, (const float*)ws,
+                     out, 0);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}

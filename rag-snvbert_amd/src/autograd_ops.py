@@ -119,7 +119,8 @@ class _HipLinear(torch.autograd.Function):
             gw = torch.mm(g2.t(), x2).float()
             gws = list(torch.split(gw, sizes, 0))
         if ctx.has_bias:
-            gbs = list(torch.split(g2.float().sum(0), sizes, 0))
+            gb = K.colsum(g2) if g2.shape[-1] % 8 == 0 and g2.shape[-1] <= 2048 else g2.float().sum(0)
+            gbs = list(torch.split(gb, sizes, 0))
         return (gx, None, *gws, *gbs)
 
 
@@ -134,6 +135,32 @@ def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
         b = torch.cat(bs, 0).to(torch.bfloat16) if bs[0] is not None else None
         return torch.nn.functional.linear(x.to(torch.bfloat16), w, b)
     return _HipLinear.apply(x, len(ws), *ws, *bs)
+
+
+class _HipAddLayerNorm(torch.autograd.Function):
+    """y = LayerNorm(x + r) (r optional) in bf16 with f32 statistics (snvrag_ln_fwd_train /
+    snvrag_ln_bwd): one pass each way instead of torch's f32 conversion + LN + grad kernels."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps):
+        x = x.to(torch.bfloat16).contiguous()
+        r = r.to(torch.bfloat16).contiguous() if r is not None else None
+        y, s, stats = K.ln_fwd_train(x, r, weight.detach().float().contiguous(),
+                                     bias.detach().float().contiguous(), eps)
+        ctx.save_for_backward(s, stats, weight)
+        ctx.has_r = r is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        s, stats, weight = ctx.saved_tensors
+        ds, dg, db = K.ln_bwd(gy.to(torch.bfloat16).contiguous(), s, stats, weight.detach().float().contiguous())
+        return ds, (ds if ctx.has_r else None), dg, db, None
+
+
+def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln) -> torch.Tensor:
+    """bf16 LayerNorm(x + r) with the parameters of nn.LayerNorm ``ln`` (N % 8 == 0, N <= 2048)."""
+    return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps)
 
 
 class _HipAttention(torch.autograd.Function):

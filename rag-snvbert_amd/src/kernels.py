@@ -414,3 +414,42 @@ def infer_post(probs_h1: torch.Tensor, probs_h2: torch.Tensor):
     gt = torch.empty(*a.shape[:-1], 4, device=a.device, dtype=torch.float32)
     check(N.lib().snvrag_infer_post(M, ptr(a), ptr(b), ptr(p1), ptr(p2), ptr(gt), stream_ptr()), "infer_post")
     return p1, p2, gt
+
+
+def ln_fwd_train(x: torch.Tensor, r: Optional[torch.Tensor], g: torch.Tensor, b: torch.Tensor, eps: float):
+    """(y bf16, s bf16 = x + r (x itself when r is None), stats f32 [M, 2])."""
+    N.require_gpu(x)
+    Nn = x.shape[-1]
+    M = x.numel() // Nn
+    y = torch.empty_like(x)
+    s = torch.empty_like(x) if r is not None else x
+    stats = torch.empty(M, 2, device=x.device, dtype=torch.float32)
+    check(N.lib().snvrag_ln_fwd_train(M, Nn, ptr(_c(x)), ptr(_c(r)) if r is not None else None,
+                                      ptr(_c(g)), ptr(_c(b)), eps, ptr(y), ptr(s) if r is not None else None,
+                                      ptr(stats), stream_ptr()), "ln_fwd_train")
+    return y, s, stats
+
+
+def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tensor):
+    """(ds bf16, dg f32 [N], db f32 [N]) of y = LN(s) g + b."""
+    Nn = s.shape[-1]
+    M = s.numel() // Nn
+    ds = torch.empty_like(s)
+    dg = torch.empty(Nn, device=s.device, dtype=torch.float32)
+    db = torch.empty_like(dg)
+    wsb = N.lib().snvrag_ln_bwd_ws_bytes(M, Nn)
+    ws = torch.empty(wsb, device=s.device, dtype=torch.uint8)
+    check(N.lib().snvrag_ln_bwd(M, Nn, ptr(_c(dy)), ptr(_c(s)), ptr(_c(stats)), ptr(_c(g)), ptr(ds), ptr(dg),
+                                ptr(db), ptr(ws), wsb, stream_ptr()), "ln_bwd")
+    return ds, dg, db
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """f32 column sums of a bf16 matrix [..., N] (bias gradients)."""
+    Nn = x.shape[-1]
+    M = x.numel() // Nn
+    out = torch.empty(Nn, device=x.device, dtype=torch.float32)
+    wsb = N.lib().snvrag_colsum_ws_bytes(M, Nn)
+    ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
+    check(N.lib().snvrag_colsum_bf16(M, Nn, ptr(_c(x)), ptr(out), ptr(ws), wsb, stream_ptr()), "colsum")
+    return out

@@ -117,6 +117,11 @@ _SIGS = {
     "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),
     "snvrag_confusion": ([i64, C.c_int, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_infer_post": ([i64, vp, vp, vp, vp, vp, vp], C.c_int),
+    "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, vp], C.c_int),
+    "snvrag_ln_bwd_ws_bytes": ([i64, C.c_int], sz),
+    "snvrag_ln_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
+    "snvrag_colsum_ws_bytes": ([i64, C.c_int], sz),
+    "snvrag_colsum_bf16": ([i64, C.c_int, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

@@ -33,7 +33,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import hip_attention, hip_linear, rag_mean_train
+from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train
 
 T = torch.bfloat16
 
@@ -48,7 +48,7 @@ def af_embedding(afm, af: torch.Tensor) -> torch.Tensor:
     feat = torch.cat([torch.sin(2 * math.pi * x), torch.cos(2 * math.pi * x)], -1)
     pr = afm.projection
     h = hip_linear(feat, pr[0].weight, pr[0].bias)
-    h = F.gelu(_ln(h, pr[1])).to(T)
+    h = F.gelu(hip_add_layernorm(h, None, pr[1]))
     return hip_linear(h, pr[3].weight, pr[3].bias)
 
 
@@ -83,8 +83,8 @@ def emb_fusion(ef, embs: torch.Tensor, pos: torch.Tensor, af: torch.Tensor, n_ca
             for _ in range(n_calls - 1):
                 pos_feat(ef.pos_feat, pos)
     rep = lambda t: t.repeat(n_calls, 1)
-    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1)
-    return _ln(embs.float() + y, ef.norm).to(T)
+    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1).to(T)
+    return hip_add_layernorm(embs, y, ef.norm)
 
 
 def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p: torch.Tensor, p: float,
@@ -104,7 +104,7 @@ def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p
     pooled = (rag.float() * w2).to(T)
     fu = rf.fusion
     h = _drop(F.gelu(hip_linear(torch.cat([orig, pooled], -1), fu[0].weight, fu[0].bias)), p, training)
-    h = _ln(hip_linear(h, fu[3].weight, fu[3].bias), fu[4]).float()
+    h = hip_add_layernorm(hip_linear(h, fu[3].weight, fu[3].bias), None, fu[4]).float()
     af2 = af.repeat(2, 1)
     maf = torch.minimum(af2, 1 - af2).unsqueeze(-1)
     mw = torch.log1p(1.0 / (maf + 1e-6)).clamp(max=3.0)
@@ -120,11 +120,12 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
                      [ll[0].bias, ll[1].bias, ll[2].bias])
     att = hip_attention(qkv, nseq, L, a.heads, a.dims)
     o = hip_linear(att, a.output_layer.weight, a.output_layer.bias).reshape(x.shape)
-    x = _drop(_ln(x + o, blk.input_sublayer.norm).to(T), p, training)
+    x = _drop(hip_add_layernorm(x, o, blk.input_sublayer.norm), p, training)
     ff = blk.feed_forward
     h = F.leaky_relu(hip_linear(x, ff.w_1.weight, ff.w_1.bias), 0.1)
-    f = _drop(F.leaky_relu(hip_linear(_ln(h, ff.norm).to(T), ff.w_2.weight, ff.w_2.bias), 0.1), p, training)
-    x = _drop(_ln(x + f, blk.output_sublayer.norm).to(T), p, training)
+    f = _drop(F.leaky_relu(hip_linear(hip_add_layernorm(h, None, ff.norm), ff.w_2.weight, ff.w_2.bias), 0.1),
+              p, training)
+    x = _drop(hip_add_layernorm(x, f, blk.output_sublayer.norm), p, training)
     return _drop(x, p, training)
 
 
@@ -193,7 +194,7 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     hc = fm.hap_classifier
     af2, afp2 = af.repeat(2, 1), af_p.repeat(2, 1)
     hh = F.gelu(_linear_cat2(hx, hc.af_fusion[0], af2, afp2).to(T))
-    hh = _ln(hip_linear(hh, hc.af_fusion[2].weight, hc.af_fusion[2].bias), hc.af_fusion[3]).to(T)
+    hh = hip_add_layernorm(hip_linear(hh, hc.af_fusion[2].weight, hc.af_fusion[2].bias), None, hc.af_fusion[3])
     hh = F.gelu(hip_linear(hh, hc.net[0].weight, hc.net[0].bias))
     logits = F.linear(hh.float(), hc.net[2].weight, hc.net[2].bias)
     probs = torch.softmax(logits, -1)

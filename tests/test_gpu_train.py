@@ -96,6 +96,33 @@ def test_hip_linear_backward(M, K_, N, multi):
         assert rel(b.grad, r.grad) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,resid", [(1000, 384, True), (517, 1536, False), (64, 64, True)])
+def test_hip_add_layernorm_fwd_bwd(M, N, resid):
+    from src.autograd_ops import hip_add_layernorm
+    g = torch.Generator(device="cpu").manual_seed(N)
+    ln = torch.nn.LayerNorm(N).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(N, generator=g) * 0.5 + 1)
+        ln.bias.copy_(torch.randn(N, generator=g) * 0.1)
+    x = (torch.randn(M, N, generator=g) * 3 + 1).to(DEV, torch.bfloat16).requires_grad_(True)
+    r = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16).requires_grad_(True) if resid else None
+    gy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    y = hip_add_layernorm(x, r, ln)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if resid else None
+    s = (xr + rr).bfloat16().float() if resid else xr          # the kernel keeps x + r in bf16
+    wr, br = ln.weight.detach().clone().requires_grad_(True), ln.bias.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(s, (N,), wr, br, ln.eps)
+    yr.backward(gy.float())
+    rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()
+    assert rel(y, yr.detach()) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    if resid:
+        assert rel(r.grad, rr.grad) < 1e-2
+    assert rel(ln.weight.grad, wr.grad) < 1e-3 and rel(ln.bias.grad, br.grad) < 1e-3
+
+
 def test_focal_loss_kernel_vs_oracle_and_reference():
     from src import kernels as K
     z = load_golden("focal")
