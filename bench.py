@@ -219,7 +219,7 @@ def main():
     name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
     roofline = dict(bound="mfma", kernel=name,
                     achieved=round(dom["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",
-                    frac=round(dom["rate"] / 1e12 / peak_f, 4), traffic=None,
+                    frac=round(dom["rate"] / 1e12 / peak_f, 4), traffic=pmc_traffic(name),
                     avg_launch_ms=round(dom["avg_ms"], 4),
                     algorithmic_per_launch=f"{dom['work_per_launch']:.4g} FLOP ({per})")
     extra = {
@@ -308,6 +308,24 @@ def train_bench(args, world, rank, dev):
             "n_gpus": world, "loss": round(float(loss), 3),
             "note": "DDP: bucketed async all-reduce of the flat f32 gradient buffer over RCCL; "
                     "reference banner: 115 ms/batch at B=24 on an unstated GPU (BASELINE.md)"}
+
+
+def pmc_traffic(kernel_name):
+    """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes run by tools/pmc.sh
+    on this bench, committed as profiles/pmc_traffic.json), launch-weighted over the kernel class."""
+    f = REPO / "profiles" / "pmc_traffic.json"
+    cls = {"rows_gemm_kernel": "gemm", "ffn_kernel": "ffn", "attn32_bf16": "attention"}
+    key = next((v for k, v in cls.items() if kernel_name.startswith(k)), None)
+    if key is None or not f.exists():
+        return None
+    ent = json.loads(f.read_text())["kernels"].get(key)
+    if not ent:
+        return None
+    n = sum(e["launches"] for e in ent)
+    fetch = sum(e["fetch_bytes"] * e["launches"] for e in ent) / n
+    write = sum((e["write_bytes"] or 0) * e["launches"] for e in ent) / n
+    return {"bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
+            "source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH x2 on gfx950)"}
 
 
 def cpu_baseline(args, model, vocab, af_np, ref_af, raw_mask, x, dev):

@@ -417,6 +417,9 @@ static int dispatch_nw(int nw, long M, long N, long K, const void* A, long lda, 
 
 // tile width for an N: prefer 384 (6), then 256, 128, 64; 0 = unsupported
 int rows_pick_nw(long N, bool need_full_row) {
+  static const int force = getenv("SNVRAG_GEMM_NW") ? atoi(getenv("SNVRAG_GEMM_NW")) : 0;
+  if (force && !need_full_row && N % (64L * force) == 0 && (force == 1 || force == 2 || force == 4 || force == 6))
+    return force;
   const int cands[4] = {6, 4, 2, 1};
   for (int c : cands) {
     const long bn = 64L * c;

@@ -67,7 +67,10 @@ def main():
     ffn_out = torch.empty_like(x)
     cases["ffn fused (W1+W2, 2 GEMMs)"] = (lambda: K.ffn_forward(x, ffn_ws, ffn_v, out=ffn_out), M, 8 * D, D, -2)
     variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
+    only = os.environ.get("GM_CASE")
     for name, (fn, m, n, k, extra) in cases.items():
+        if only and only not in name:
+            continue
         flop = 2.0 * m * n * k
         byts = 2.0 * (m * k + n * k + m * n * (1 + extra)) if extra >= 0 else 2.0 * 2 * m * k
         for vn, env in variants:
@@ -83,6 +86,8 @@ def main():
         for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
             os.environ.pop(kk, None)
         if not os.environ.get("GM_TORCH"):
+            continue
+        if (n, k) not in w:
             continue
         a = h if k == 4 * D else x
         ww = w[(n, k)]
