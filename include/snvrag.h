@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 7
+#define SNVRAG_ABI_VERSION 8
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -242,6 +242,9 @@ typedef struct {
   /* optional (bf16, D in {128,256,384}): fused FFN weight stream from snvrag_ffn_pack
    * and its vector table (see snvrag_ffn_forward); NULL = unfused GEMM path */
   const void* ffn_w; const float* ffn_v;
+  /* optional (bf16): snvrag_wsg_pack of w_qkv -> the QKV projection runs on the
+   * weight-streaming GEMM */
+  const void* qkv_ws;
 } snvrag_layer_t;
 
 /* ------------------------------------------------------------------------
@@ -262,6 +265,17 @@ size_t snvrag_ffn_pack_bytes(int D);
 int snvrag_ffn_pack(int D, const void* w1, const void* w2g, void* out, void* stream);
 int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
                        const float* vec, float eps, void* stream);
+
+/* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
+ * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either
+ * act(.) (ln_g == NULL) or LN(. + resid) * ln_g + ln_b (N == K, resid [M, ld_resid]).
+ * A [M, K] contiguous; W packed once by snvrag_wsg_pack (wsg_pack_bytes(N, K) bytes).
+ * K in {128, 256, 384}, N % 64 == 0 (N / 64 in {2,4,6,8,12,16,18,24} without LN). */
+size_t snvrag_wsg_pack_bytes(int64_t N, int64_t K);
+int snvrag_wsg_pack(int64_t N, int64_t K, const void* w, void* out, void* stream);
+int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
+                       int act, float slope, const void* resid, int64_t ld_resid, const float* ln_g,
+                       const float* ln_b, float eps, void* out, int64_t ldo, void* stream);
 
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);
 int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,

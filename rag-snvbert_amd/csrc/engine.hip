@@ -80,7 +80,11 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       snvrag_epilogue_t e{};
       int rc;
       e.bias = ly.b_qkv;
-      rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
+      if (dtype == SNVRAG_BF16 && ly.qkv_ws && !getenv("SNVRAG_NO_WSG"))
+        rc = snvrag_wsg_forward(M, 3 * D, D, xc, ly.qkv_ws, ly.b_qkv, SNVRAG_ACT_NONE, 0.f, nullptr, 0, nullptr,
+                                nullptr, 0.f, qkv, 3 * D, stream);
+      else
+        rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
       if (rc) return rc;
       // q rows may carry a folded factor (the bf16 engine folds log2(e)/sqrt(dh))
       const float sc = ly.q_scale > 0.f ? scale / ly.q_scale : scale;

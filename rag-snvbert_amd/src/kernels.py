@@ -453,3 +453,31 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     ws = torch.empty(wsb, device=x.device, dtype=torch.uint8)
     check(N.lib().snvrag_colsum_bf16(M, Nn, ptr(_c(x)), ptr(out), ptr(ws), wsb, stream_ptr()), "colsum")
     return out
+
+
+def wsg_pack(w: torch.Tensor) -> torch.Tensor:
+    """Fragment-ordered bf16 weight stream of the weight-streaming GEMM (csrc/wsgemm.hip)."""
+    Nn, Kk = w.shape
+    nbytes = int(N.lib().snvrag_wsg_pack_bytes(Nn, Kk))
+    if nbytes == 0:
+        raise ValueError(f"weight-streaming GEMM needs N % 64 == 0 and K in (128, 256, 384), got {tuple(w.shape)}")
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    check(N.lib().snvrag_wsg_pack(Nn, Kk, ptr(_c(w.to(torch.bfloat16).contiguous())), ptr(out), stream_ptr()),
+          "wsg_pack")
+    return out
+
+
+def wsg_linear(x: torch.Tensor, wstream: torch.Tensor, n_out: int, bias: torch.Tensor, *, act: int = N.ACT_NONE,
+               slope: float = 0.0, resid: Optional[torch.Tensor] = None,
+               ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, eps: float = 1e-5,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    N.require_gpu(x)
+    Kk = x.shape[-1]
+    M = x.numel() // Kk
+    if out is None:
+        out = torch.empty(*x.shape[:-1], n_out, device=x.device, dtype=torch.bfloat16)
+    check(N.lib().snvrag_wsg_forward(M, n_out, Kk, ptr(_c(x)), ptr(wstream), ptr(_c(bias)), act, slope,
+                                     ptr(resid), n_out if resid is not None else 0,
+                                     ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, eps,
+                                     ptr(out), n_out, stream_ptr()), "wsg_linear")
+    return out

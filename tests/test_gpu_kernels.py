@@ -398,3 +398,30 @@ def test_attention_dh32_overflow_takes_exact_fallback():
     assert torch.isfinite(out.float()).all()
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
     assert K().attention_fallbacks(True) > 0
+
+
+@pytest.mark.parametrize("M,N,Kd,mode", [(1000, 1152, 384, "plain"), (517, 1536, 384, "gelu"), (333, 384, 384, "ln"),
+                                        (130, 256, 256, "ln"), (77, 512, 128, "lrelu")])
+def test_weight_streaming_gemm(M, N, Kd, mode):
+    """snvrag_wsg_forward vs torch fp32 on the same bf16 operands (bf16 output: 1e-2 rel)."""
+    from src import native as NN
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    x = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    ws = K().wsg_pack(w)
+    ref = x.float() @ w.float().t() + b
+    kw = {}
+    if mode == "gelu":
+        kw = dict(act=NN.ACT_GELU)
+        ref = torch.nn.functional.gelu(ref)
+    elif mode == "lrelu":
+        kw = dict(act=NN.ACT_LRELU, slope=0.1)
+        ref = torch.nn.functional.leaky_relu(ref, 0.1)
+    elif mode == "ln":
+        r = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+        gm, bt = torch.rand(N, generator=g).to(DEV) + 0.5, torch.randn(N, generator=g).to(DEV)
+        kw = dict(resid=r, ln=(gm, bt))
+        ref = torch.nn.functional.layer_norm(ref + r.float(), (N,), gm, bt, 1e-5)
+    out = K().wsg_linear(x, ws, N, b, **kw)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
