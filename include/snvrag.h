@@ -277,6 +277,13 @@ int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const voi
                        int act, float slope, const void* resid, int64_t ld_resid, const float* ln_g,
                        const float* ln_b, float eps, void* out, int64_t ldo, void* stream);
 
+/* Hap-classifier tail in one pass (foundation_model.py:77-80): probs[M, 2] =
+ * softmax(act(A W^T + bias) w_out^T + b_out), logits (nullable) before the softmax;
+ * the [M, N] hidden stays in registers.  (K, N) in {(384,1536), (256,1024), (128,512)}. */
+int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
+                     int act, float slope, const float* w_out, const float* b_out, float* logits, float* probs,
+                     void* stream);
+
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);
 int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,
                            const snvrag_layer_t* layers, void* x, void* ws, size_t ws_bytes,

@@ -58,6 +58,9 @@ struct WsEpi {
   const bf16* resid;       // EPI 1: [M, ldr]
   long ld_resid;
   const float* ln_g; const float* ln_b; float eps;
+  // EPI 2 (hap head, foundation_model.py:77-80): logits = act(.) w_out^T + b_out (2 outputs),
+  // probs = softmax(logits); the 4D hidden never leaves the registers
+  const float* w_out; const float* b_out; float* logits; float* probs;
 };
 
 template <int K, int NCH, int EPI>
@@ -103,6 +106,7 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
   const long row = rbase + li;
   const bool rv = row < M;
   float keep[EPI == 1 ? NCH : 1][16];
+  float po0 = 0.f, po1 = 0.f;                     // EPI 2 partial logits
   int slab = 0;
 #pragma unroll (EPI == 1 ? NCH : 1)
   for (int c0 = 0; c0 < NCH; ++c0) {
@@ -134,7 +138,23 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
       v[4 * t + 2] = h[t][2] + bb.z;
       v[4 * t + 3] = h[t][3] + bb.w;
     }
-    if constexpr (EPI == 0) {
+    if constexpr (EPI == 2) {
+      if (e.act == SNVRAG_ACT_LRELU) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * e.slope;
+      } else if (e.act) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = apply_act(e.act, v[j], e.slope);
+      }
+      const int col = c * 64 + 16 * lg;
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float4 w0 = *reinterpret_cast<const float4*>(e.w_out + col + 4 * j4);
+        const float4 w1 = *reinterpret_cast<const float4*>(e.w_out + NCH * 64 + col + 4 * j4);
+        po0 += v[4 * j4] * w0.x + v[4 * j4 + 1] * w0.y + v[4 * j4 + 2] * w0.z + v[4 * j4 + 3] * w0.w;
+        po1 += v[4 * j4] * w1.x + v[4 * j4 + 1] * w1.y + v[4 * j4 + 2] * w1.z + v[4 * j4 + 3] * w1.w;
+      }
+    } else if constexpr (EPI == 0) {
       if (e.act == SNVRAG_ACT_LRELU) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * e.slope;
@@ -150,6 +170,18 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
     } else {
 #pragma unroll
       for (int j = 0; j < 16; ++j) keep[c0][j] = v[j];
+    }
+  }
+  if constexpr (EPI == 2) {
+    po0 += __shfl_xor(po0, 16, 64);
+    po0 += __shfl_xor(po0, 32, 64);
+    po1 += __shfl_xor(po1, 16, 64);
+    po1 += __shfl_xor(po1, 32, 64);
+    if (rv && lg == 0) {
+      const float l0 = po0 + e.b_out[0], l1 = po1 + e.b_out[1];
+      if (e.logits) reinterpret_cast<float2*>(e.logits)[row] = make_float2(l0, l1);
+      const float mx = fmaxf(l0, l1), e0 = expf(l0 - mx), e1 = expf(l1 - mx), inv = 1.0f / (e0 + e1);
+      reinterpret_cast<float2*>(e.probs)[row] = make_float2(e0 * inv, e1 * inv);
     }
   }
   if constexpr (EPI == 1) {
@@ -230,6 +262,28 @@ static int launch_wsg(int64_t M, const void* A, const void* ws, void* out, long 
 }  // namespace snvrag
 
 using namespace snvrag;
+
+// hap head (foundation_model.py:77-80): probs = softmax(act(A W^T + b) w_out^T + b_out),
+// A [M, K], W packed by snvrag_wsg_pack (N hidden), w_out [2, N] f32
+extern "C" int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream,
+                                const float* bias, int act, float slope, const float* w_out, const float* b_out,
+                                float* logits, float* probs, void* stream) {
+  SNV_CHECK_ARG(A && wstream && bias && w_out && b_out && probs, "null pointer");
+  SNV_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)w_out % 16) == 0 && ((uintptr_t)bias % 16) == 0,
+                "A/w_out/bias must be 16-byte aligned");
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  WsEpi e{bias, act, slope, nullptr, 0, nullptr, nullptr, 0.f, w_out, b_out, logits, probs};
+  int rc = -1;
+  evlog_begin(s);
+  if (K == 384 && N == 1536) rc = launch_wsg<384, 24, 2>(M, A, wstream, nullptr, 0, e, s);
+  else if (K == 256 && N == 1024) rc = launch_wsg<256, 16, 2>(M, A, wstream, nullptr, 0, e, s);
+  else if (K == 128 && N == 512) rc = launch_wsg<128, 8, 2>(M, A, wstream, nullptr, 0, e, s);
+  if (rc < 0) return fail(__func__, "unsupported (N, K) for the fused head");
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)N * (K + 2));
+  return 0;
+}
 
 extern "C" size_t snvrag_wsg_pack_bytes(int64_t N, int64_t K) {
   if (N % 64 || (K != 128 && K != 256 && K != 384)) return 0;

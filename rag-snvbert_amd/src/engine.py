@@ -22,6 +22,7 @@ import weakref
 from typing import Dict, Optional
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -188,6 +189,10 @@ class Engine:
                     g=f32(hc.af_fusion[3].weight), bb=f32(hc.af_fusion[3].bias),
                     n0=cvt(hc.net[0].weight), n0b=f32(hc.net[0].bias),
                     n2=f32(hc.net[2].weight), n2b=f32(hc.net[2].bias))
+        if T == torch.bfloat16 and D in (128, 256, 384) and P.hh["n2"].shape[0] == 2 \
+                and os.environ.get("SNVRAG_NO_WSG") is None:
+            # fused net[0] + GELU + net[2] + softmax (csrc/wsgemm.hip, EPI 2)
+            P.hh["n0_ws"] = K.wsg_pack(P.hh["n0"])
         gc = fm.gt_classifier
         P.gt_t = [f32(t) for t in (gc.gf_fusion.weight, gc.gf_fusion.bias, gc.gf_norm.weight, gc.gf_norm.bias,
                                    gc.layer.w_1.weight, gc.layer.w_1.bias, gc.layer.norm.weight,
@@ -284,8 +289,12 @@ class Engine:
         h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
                      row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
         h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
-        h = K.linear(h, hh["n0"], hh["n0b"], act=N.ACT_GELU)
-        logits, probs = K.hap_head_out(h, hh["n2"], hh["n2b"], want_logits=want_logits)
+        if "n0_ws" in hh:
+            logits, probs = K.wsg_head2(h, hh["n0_ws"], hh["n0"].shape[0], hh["n0b"], hh["n2"], hh["n2b"],
+                                        act=N.ACT_GELU, want_logits=want_logits)
+        else:
+            h = K.linear(h, hh["n0"], hh["n0b"], act=N.ACT_GELU)
+            logits, probs = K.hap_head_out(h, hh["n2"], hh["n2b"], want_logits=want_logits)
         dev = probs.device
         g = lambda k: x[k].to(dev, torch.float32).contiguous()
         gt = K.gt_head(probs[:B], probs[B:], g("ref"), g("het"), g("hom"), BL, P.gt)

@@ -481,3 +481,17 @@ def wsg_linear(x: torch.Tensor, wstream: torch.Tensor, n_out: int, bias: torch.T
                                      ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, eps,
                                      ptr(out), n_out, stream_ptr()), "wsg_linear")
     return out
+
+
+def wsg_head2(x: torch.Tensor, wstream: torch.Tensor, n_hidden: int, bias: torch.Tensor, w_out: torch.Tensor,
+              b_out: torch.Tensor, act: int = N.ACT_GELU, want_logits: bool = False):
+    """(logits or None, probs) [..., 2] of softmax(act(x W^T + b) w_out^T + b_out) in one launch."""
+    N.require_gpu(x)
+    Kk = x.shape[-1]
+    M = x.numel() // Kk
+    probs = torch.empty(*x.shape[:-1], 2, device=x.device, dtype=torch.float32)
+    logits = torch.empty_like(probs) if want_logits else None
+    check(N.lib().snvrag_wsg_head2(M, n_hidden, Kk, ptr(_c(x)), ptr(wstream), ptr(_c(bias)), act, 0.0,
+                                   ptr(_c(w_out)), ptr(_c(b_out)), ptr(logits), ptr(probs), stream_ptr()),
+          "wsg_head2")
+    return logits, probs

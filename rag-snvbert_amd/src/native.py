@@ -119,6 +119,7 @@ _SIGS = {
     "snvrag_infer_post": ([i64, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_wsg_pack_bytes": ([i64, i64], sz),
     "snvrag_wsg_pack": ([i64, i64, vp, vp, vp], C.c_int),
+    "snvrag_wsg_head2": ([i64, i64, i64, vp, vp, vp, C.c_int, f32, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_wsg_forward": ([i64, i64, i64, vp, vp, vp, C.c_int, f32, vp, i64, vp, vp, f32, vp, i64, vp], C.c_int),
     "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, vp], C.c_int),
     "snvrag_ln_bwd_ws_bytes": ([i64, C.c_int], sz),

@@ -425,3 +425,21 @@ def test_weight_streaming_gemm(M, N, Kd, mode):
         ref = torch.nn.functional.layer_norm(ref + r.float(), (N,), gm, bt, 1e-5)
     out = K().wsg_linear(x, ws, N, b, **kw)
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,Kd", [(1, 384), (300, 384), (4111, 256), (129, 128)])
+def test_weight_streaming_head2(M, Kd):
+    """snvrag_wsg_head2 (net[0] + GELU + net[2] + softmax) vs torch fp32 on the same bf16 operands."""
+    g = torch.Generator(device="cpu").manual_seed(M + Kd)
+    N = 4 * Kd
+    x = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    w2 = (torch.randn(2, N, generator=g) / math.sqrt(N)).to(DEV)
+    b2 = torch.randn(2, generator=g).to(DEV)
+    h = torch.nn.functional.gelu(x.float() @ w.float().t() + b)
+    ref_l = h @ w2.t() + b2
+    logits, probs = K().wsg_head2(x, K().wsg_pack(w), N, b, w2, b2, want_logits=True)
+    torch.testing.assert_close(logits, ref_l, rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(probs, torch.softmax(ref_l, -1), rtol=1e-3, atol=1e-3)
