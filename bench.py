@@ -214,7 +214,7 @@ def main():
     peak_f = BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_PEAK_TFLOPS
     # roofline object = the MFMA kernel class with the most time per step
     mf = [("rows_gemm_kernel (encoder QKV/out-proj + fusion/head GEMMs)", gemm, "2*M*N*K averaged over launches"),
-          ("ffn_kernel (fused FFN sublayer, 12 launches)", ffn, "2*M*D*8D = 16*M*D^2 per launch"),
+          ("ffn_kernel (block tail: out-projection + LN1 + FFN + LN2, 12 launches)", ffn, "2*M*D*9D = 18*M*D^2 per launch"),
           ("attn32_bf16 (attention)", attn, "4*L^2*dh*H*nseq per launch")]
     name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
     roofline = dict(bound="mfma", kernel=name,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 8
+#define SNVRAG_ABI_VERSION 9
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -245,6 +245,9 @@ typedef struct {
   /* optional (bf16): snvrag_wsg_pack of w_qkv -> the QKV projection runs on the
    * weight-streaming GEMM */
   const void* qkv_ws;
+  /* optional (bf16, with ffn_w/ffn_v): snvrag_ffn_pre_pack of w_o -> the attention
+   * output projection + LN1 run inside the fused FFN launch (snvrag_block_tail_forward) */
+  const void* o_ws;
 } snvrag_layer_t;
 
 /* ------------------------------------------------------------------------
@@ -265,6 +268,18 @@ size_t snvrag_ffn_pack_bytes(int D);
 int snvrag_ffn_pack(int D, const void* w1, const void* w2g, void* out, void* stream);
 int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
                        const float* vec, float eps, void* stream);
+
+/* Whole block tail in ONE launch (multi_head_attention.py:51 output projection,
+ * sublayer.py:15-16 x2, feed_forward.py:18-21), bf16, eval, in place on x:
+ *   x1 = LN1(x + att W_o^T + b_o);  x = LN2(x1 + FFN(x1))
+ * x1 stays in LDS.  wo_stream from snvrag_ffn_pre_pack (snvrag_ffn_pre_pack_bytes(D)
+ * bytes), ffn_stream / ffn_vec as for snvrag_ffn_forward.  att, x [M, D] bf16, must
+ * not alias; all pointers 16-byte aligned; D in {128, 256, 384}. */
+size_t snvrag_ffn_pre_pack_bytes(int D);
+int snvrag_ffn_pre_pack(int D, const void* w_o, void* out, void* stream);
+int snvrag_block_tail_forward(int64_t M, int D, const void* att, void* x, const void* wo_stream,
+                              const float* b_o, const float* ln1_g, const float* ln1_b,
+                              const void* ffn_stream, const float* ffn_vec, float eps, void* stream);
 
 /* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
  * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either

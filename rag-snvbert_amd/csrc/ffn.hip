@@ -19,6 +19,11 @@
 // W2' rows are permuted so lane (li, lg) holds output columns 32s + 8lg + j (j < 8):
 // residual, LayerNorm and the 16-byte stores work on whole 8-column runs of one
 // row, and the row reductions are two lane shuffles.
+//
+// PRE variant (snvrag_block_tail_forward): the attention output projection runs in
+// the same workgroup first, x1 = LN1(x + att W_o^T + b_o), from att rows staged in
+// the x1 LDS tile and a W_o' stream (18 slabs at D = 384, phase-2 format) ahead of
+// the FFN stream; x1 is written over att in LDS and never reaches HBM.
 #include "common.h"
 
 namespace snvrag {
@@ -74,12 +79,19 @@ __device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const
 
 // RT 16-row tiles per wave, NWV waves: RT = 2, NWV = 4 (one wave per SIMD, 512 registers)
 // or RT = 1, NWV = 8 (two waves per SIMD, 256 registers each); 128 rows either way.
-template <int D, int RT, int NWV, int DBG>
+struct FfnPre {            // PRE: x1 = LN1(resid + att W_o^T + b_o)
+  const bf16* resid; const char* wo; const float* b_o; const float* g1; const float* be1;
+};
+
+template <int D, int RT, int NWV, int DBG, bool PRE = false>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV / 4, NWV / 4)))
-void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* __restrict__ out, const char* __restrict__ ws,
-                const float* __restrict__ vec, float eps) {
+void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __restrict__ ws,
+                const float* __restrict__ vec, float eps, FfnPre pre) {
   using S = FfnShape<D>;
-  constexpr int KS = S::KS, NT = S::NT, NB = S::NB, NSLAB = S::NSLAB;
+  constexpr int KS = S::KS, NT = S::NT, NB = S::NB;
+  constexpr int NCHP = PRE ? D / 64 : 0;           // W_o' chunks (64 k each) ahead of the FFN stream
+  constexpr int NPRE = NCHP * NB;
+  constexpr int NSLAB = NPRE + S::NSLAB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -102,11 +114,20 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* __restrict__ out, cons
   // order is the same sum): concurrent CUs of an XCD then read different slabs
   // instead of all hitting the same L2 channels with the same 16 KiB.
   const int rot = (int)(blockIdx.x % S::NCH);
+  const int rotp = PRE ? (int)(blockIdx.x % (NCHP > 0 ? NCHP : 1)) : 0;
   auto issue = [&](int i) {
     if (DBG != 1 && i < NSLAB) {
-      int cc = i / S::SPC + rot;
-      cc = cc >= S::NCH ? cc - S::NCH : cc;
-      const char* src = ws + ((long)cc * S::SPC + i % S::SPC) * FF_SLAB + wave * BPW * 1024 + lane * 16;
+      const char* src;
+      if (PRE && i < NPRE) {
+        int cc = i / NB + rotp;
+        cc = cc >= NCHP ? cc - NCHP : cc;
+        src = pre.wo + ((long)cc * NB + i % NB) * FF_SLAB + wave * BPW * 1024 + lane * 16;
+      } else {
+        const int k = i - NPRE;
+        int cc = k / S::SPC + rot;
+        cc = cc >= S::NCH ? cc - S::NCH : cc;
+        src = ws + ((long)cc * S::SPC + k % S::SPC) * FF_SLAB + wave * BPW * 1024 + lane * 16;
+      }
       char* dst = ring + (i % FF_NSLOT) * FF_SLAB + wave * BPW * 1024;
 #pragma unroll
       for (int j = 0; j < BPW; ++j) ff_glds16(src + j * 1024, dst + j * 1024);
@@ -131,10 +152,74 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* __restrict__ out, cons
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  int slab = 0;
+  if constexpr (PRE) {
+    // ---- acc = att W_o'^T (att rows are this wave's LDS tile, k order of the x1 layout)
+#pragma unroll 1
+    for (int c0 = 0; c0 < NCHP; ++c0) {
+      const int c = c0 + rotp >= NCHP ? c0 + rotp - NCHP : c0 + rotp;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const char* sl = step(slab++);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          u32x4 a[8], b[RT];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 2 + s2) * 1024);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + 2 * c + s2) * 1024);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) acc[rt][nb * 8 + t] = mfma_bf16(a[t], b[rt], acc[rt][nb * 8 + t]);
+        }
+      }
+    }
+    // ---- x1 = LN1(resid + acc + b_o) -> this wave's LDS tile (over att), acc reset
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const long r = min(rbase + rt * 16 + li, (long)M - 1);
+      float sum = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const u32x4 xr = *reinterpret_cast<const u32x4*>(pre.resid + r * D + 32 * s + 8 * lg);
+        const float* bo = pre.b_o + 32 * s + 8 * lg;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = acc[rt][2 * s + (j >> 2)][j & 3] + bo[j] + bfx(xr, j);
+          acc[rt][2 * s + (j >> 2)][j & 3] = v;
+          sum += v;
+        }
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      const float mean = sum * (1.0f / D);
+      float q = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const float d = acc[rt][t][i] - mean; q = fmaf(d, d, q); }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float rstd = 1.0f / sqrtf(q * (1.0f / D) + eps);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float* g = pre.g1 + 32 * s + 8 * lg;
+        const float* b = pre.be1 + 32 * s + 8 * lg;
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (acc[rt][2 * s + (j >> 2)][j & 3] - mean) * rstd * g[j] + b[j];
+        *reinterpret_cast<u32x4*>(xt + (rt * KS + s) * 1024 + lane * 16) =
+            u32x4{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
   float st1[RT], st2[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) st1[rt] = st2[rt] = 0.f;
-  int slab = 0;
 #pragma unroll 1
   for (int c0 = 0; c0 < S::NCH; ++c0) {
     const int c = c0 + rot >= S::NCH ? c0 + rot - S::NCH : c0 + rot;
@@ -287,7 +372,33 @@ __global__ void ffn_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w
   for (int j = 0; j < 8; ++j) out[p * 8 + j] = v[j];
 }
 
+// W_o' stream of the PRE variant: per 64-k chunk c, NB slabs; block t*2+s2 of slab
+// (c, nb): W_o[perm(8nb+t, li)][64c + 32s2 + 8lg + j]
+__global__ void ffn_pre_pack_kernel(int D, long n_pieces, const bf16* __restrict__ wo, bf16* __restrict__ out) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pieces) return;
+  const int NB = D / 128;
+  const long slab = p / 1024;
+  const int b = (int)((p / 64) % 16), L = (int)(p % 64), li = L & 15, lg = L >> 4;
+  const int c = (int)(slab / NB), nb = (int)(slab % NB), t = b / 2, s2 = b % 2;
+  const int n = ffn_perm(nb * 8 + t, li);
+  const long k0 = (long)c * 64 + 32 * s2 + 8 * lg;
+  for (int j = 0; j < 8; ++j) out[p * 8 + j] = wo[(long)n * D + k0 + j];
+}
+
 static bool ffn_d_ok(int D) { return D == 128 || D == 256 || D == 384; }
+
+template <int D>
+static int launch_ffn_pre(int64_t M, const void* att, void* x, const void* ws, const float* vec, float eps,
+                          const FfnPre& pre, hipStream_t s) {
+  constexpr size_t lds = FfnShape<D>::LDS;
+  auto kern = ffn_kernel<D, 1, 8, 0, true>;
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(512), lds, s, (int)M, (const bf16*)att, (bf16*)x,
+                     (const char*)ws, vec, eps, pre);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
 
 template <int D>
 static int launch_ffn(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps, hipStream_t s) {
@@ -299,7 +410,7 @@ static int launch_ffn(int64_t M, const void* x1, void* out, const void* ws, cons
   const int nthr = one ? 256 : 512;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(nthr), lds, s, (int)M, (const bf16*)x1, (bf16*)out,
-                     (const char*)ws, vec, eps);
+                     (const char*)ws, vec, eps, FfnPre{});
   SNV_LAUNCH_CHECK();
   return 0;
 }
@@ -347,5 +458,45 @@ extern "C" int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, c
   }
   if (rc) return rc;
   evlog_end(s, EV_BLOCK, 2.0 * M * (double)D * D * 8);
+  return 0;
+}
+
+extern "C" size_t snvrag_ffn_pre_pack_bytes(int D) {
+  return ffn_d_ok(D) ? (size_t)(D / 64) * (D / 128) * FF_SLAB : 0;
+}
+
+extern "C" int snvrag_ffn_pre_pack(int D, const void* w_o, void* out, void* stream) {
+  SNV_CHECK_ARG(ffn_d_ok(D), "fused block tail needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(w_o && out, "null pointer");
+  const long pieces = (long)(snvrag_ffn_pre_pack_bytes(D) / 16);
+  hipLaunchKernelGGL(ffn_pre_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D,
+                     pieces, (const bf16*)w_o, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_block_tail_forward(int64_t M, int D, const void* att, void* x, const void* wo_stream,
+                                         const float* b_o, const float* ln1_g, const float* ln1_b,
+                                         const void* ffn_stream, const float* ffn_vec, float eps, void* stream) {
+  SNV_CHECK_ARG(ffn_d_ok(D), "fused block tail needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(att && x && wo_stream && b_o && ln1_g && ln1_b && ffn_stream && ffn_vec, "null pointer");
+  SNV_CHECK_ARG(att != x, "att and x must not alias");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)att % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)wo_stream % 16) == 0 &&
+                    ((uintptr_t)ffn_stream % 16) == 0 && ((uintptr_t)ffn_vec % 16) == 0 && ((uintptr_t)b_o % 16) == 0 &&
+                    ((uintptr_t)ln1_g % 16) == 0 && ((uintptr_t)ln1_b % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const FfnPre pre{(const bf16*)x, (const char*)wo_stream, b_o, ln1_g, ln1_b};
+  evlog_begin(s);
+  int rc;
+  switch (D) {
+    case 128: rc = launch_ffn_pre<128>(M, att, x, ffn_stream, ffn_vec, eps, pre, s); break;
+    case 256: rc = launch_ffn_pre<256>(M, att, x, ffn_stream, ffn_vec, eps, pre, s); break;
+    default: rc = launch_ffn_pre<384>(M, att, x, ffn_stream, ffn_vec, eps, pre, s); break;
+  }
+  if (rc) return rc;
+  evlog_end(s, EV_BLOCK, 2.0 * M * (double)D * D * 9);
   return 0;
 }

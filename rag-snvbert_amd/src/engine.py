@@ -178,6 +178,7 @@ class Engine:
                 t["ffn_w"] = K.ffn_pack(t["w1"], w2g)
                 t["ffn_v"] = K.ffn_vec(t["b1"], b2g, w2g, t["ln2_g"], t["ln2_b"])
                 t["qkv_ws"] = K.wsg_pack(t["w_qkv"])
+                t["o_ws"] = K.ffn_pre_pack(t["w_o"])
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:

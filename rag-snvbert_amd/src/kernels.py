@@ -117,6 +117,33 @@ def ffn_forward(x1: torch.Tensor, wstream: torch.Tensor, vec: torch.Tensor, eps:
     return out
 
 
+def ffn_pre_pack(w_o: torch.Tensor) -> torch.Tensor:
+    """W_o stream of the fused block tail (csrc/ffn.hip, PRE variant)."""
+    D = w_o.shape[1]
+    nbytes = int(N.lib().snvrag_ffn_pre_pack_bytes(D))
+    if nbytes == 0:
+        raise ValueError(f"fused block tail needs D in (128, 256, 384), got {D}")
+    out = torch.empty(nbytes, device=w_o.device, dtype=torch.uint8)
+    w = _c(w_o.to(torch.bfloat16))
+    assert tuple(w.shape) == (D, D)
+    check(N.lib().snvrag_ffn_pre_pack(D, ptr(w), ptr(out), stream_ptr()), "ffn_pre_pack")
+    return out
+
+
+def block_tail_forward(att: torch.Tensor, x: torch.Tensor, wo_stream: torch.Tensor, b_o, ln1_g, ln1_b,
+                       ffn_stream: torch.Tensor, ffn_vec: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """x <- LN2(x1 + FFN(x1)), x1 = LN1(x + att W_o^T + b_o), in place, one launch (bf16)."""
+    N.require_gpu(att, x)
+    assert att.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and x.is_contiguous()
+    D = x.shape[-1]
+    M = x.numel() // D
+    f = [_c(t.float()) for t in (b_o, ln1_g, ln1_b)]
+    check(N.lib().snvrag_block_tail_forward(M, D, ptr(_c(att)), ptr(x), ptr(wo_stream), ptr(f[0]), ptr(f[1]),
+                                            ptr(f[2]), ptr(ffn_stream), ptr(ffn_vec), eps, stream_ptr()),
+          "block_tail_forward")
+    return x
+
+
 def stat_tiles(n: int) -> int:
     """Column tiles of the row-panel GEMM for an N (the stats_out leading dim)."""
     for bn in (384, 256, 128, 64):

@@ -340,6 +340,45 @@ def test_ffn_fused_kernel(D, M):
     assert (out.double() - ref).abs().mean() < 1e-2
 
 
+@pytest.mark.parametrize("D,M", [(384, 777), (384, 128 * 3), (128, 300), (256, 1), (384, 4 * 1030 + 5)])
+def test_block_tail_fused_kernel(D, M):
+    """One-launch block tail (csrc/ffn.hip PRE): x1 = LN1(x + att W_o^T + b_o), x = LN2(x1 + FFN(x1))
+    (multi_head_attention.py:51, sublayer.py:15-16, feed_forward.py:18-21) vs float64 torch on the
+    same bf16 operands, and vs the two-launch bf16 path (row-panel GEMM with LN epilogue + fused FFN)."""
+    g = torch.Generator(device="cpu").manual_seed(3 * D + M)
+    bf = torch.bfloat16
+    x = torch.randn(M, D, generator=g).to(DEV, bf)
+    att = (0.5 * torch.randn(M, D, generator=g)).to(DEV, bf)
+    w_o = (torch.randn(D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    b_o = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    g1, be1 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w1 = (torch.randn(4 * D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    w2 = (torch.randn(D, 4 * D, generator=g) / math.sqrt(4 * D)).to(DEV)
+    b1, b2 = torch.randn(4 * D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    gf, bff = (1 + 0.2 * torch.randn(4 * D, generator=g)).to(DEV), (0.1 * torch.randn(4 * D, generator=g)).to(DEV)
+    g2, be2 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w2g, b2g, _ = K().fold_layernorm(w2, b2, gf, bff, bf)
+    ws = K().ffn_pack(w1, w2g)
+    vec = K().ffn_vec(b1, b2g, w2g, g2, be2)
+    wo_s = K().ffn_pre_pack(w_o)
+    # two-launch path first (x is updated in place by the fused one)
+    x1_2 = K().linear(att, w_o, b_o, resid=x, ln=(g1, be1))
+    two = K().ffn_forward(x1_2, ws, vec)
+    xd = x.double()
+    x1 = torch.nn.functional.layer_norm(xd + att.double() @ w_o.double().T + b_o.double(), (D,), g1.double(),
+                                        be1.double(), 1e-5)
+    h = torch.nn.functional.leaky_relu(x1 @ w1.double().T + b1.double(), 0.1)
+    hn = torch.nn.functional.layer_norm(h, (4 * D,), gf.double(), bff.double(), 1e-5)
+    f = torch.nn.functional.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
+    ref = torch.nn.functional.layer_norm(x1 + f, (D,), g2.double(), be2.double(), 1e-5)
+    out = K().block_tail_forward(att, x, wo_s, b_o, g1, be1, ws, vec)
+    assert out.data_ptr() == x.data_ptr()
+    torch.testing.assert_close(out.double(), ref, rtol=5e-2, atol=5e-2)
+    assert (out.double() - ref).abs().mean() < 1e-2
+    torch.testing.assert_close(out.double(), two.double(), rtol=5e-2, atol=5e-2)
+    assert (out.double() - two.double()).abs().mean() < 5e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_encoder_fused_equals_unfused(dt, monkeypatch):
     """Encoder stack with LN fused into GEMM epilogues/prologues == the 8-launch unfused stack."""

@@ -54,6 +54,7 @@ def main():
         "oproj N384 K384 +resid": (lambda: K.linear(x, w[(D, D)], bias[D], resid=x), M, D, D, 1),
         "oproj N384 K384 +LN": (lambda: K.linear(x, w[(D, D)], bias[D], ln=(lg, lb)), M, D, D, 0),
         "ffn1 N1536 K384 plain": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D]), M, 4 * D, D, 0),
+        "ffn1 N1536 K384 +gelu": (lambda: K.linear(x, w[(4 * D, D)], bias[4 * D], act=N.ACT_GELU), M, 4 * D, D, 0),
         "ffn2 N384 K1536 +rownorm+resid+LN": (lambda: K.linear(h, w[(D, 4 * D)], bias[D], act=N.ACT_LRELU, slope=0.1,
                                                                resid=x, ln=(lg, lb),
                                                                rownorm=(stats, K.stat_tiles(4 * D), 4 * D, c1)),
@@ -66,6 +67,11 @@ def main():
     ffn_v = K.ffn_vec(bias[4 * D], b2g, w2g, lg, lb)
     ffn_out = torch.empty_like(x)
     cases["ffn fused (W1+W2, 2 GEMMs)"] = (lambda: K.ffn_forward(x, ffn_ws, ffn_v, out=ffn_out), M, 8 * D, D, -2)
+    wo_s = K.ffn_pre_pack(w[(D, D)])
+    xt = x.clone()
+    cases["block tail (Wo+LN1+FFN)"] = (lambda: K.block_tail_forward(x, xt, wo_s,
+                                                                      bias[D], lg, lb, ffn_ws, ffn_v),
+                                        M, 9 * D, D, -2)
     qkv_ws = K.wsg_pack(w[(3 * D, D)])
     o_ws = K.wsg_pack(w[(D, D)])
     f1_ws = K.wsg_pack(w[(4 * D, D)])
