@@ -83,7 +83,7 @@ struct FfnPre {            // PRE: x1 = LN1(resid + att W_o^T + b_o)
   const bf16* resid; const char* wo; const float* b_o; const float* g1; const float* be1;
 };
 
-template <int D, int RT, int NWV, int DBG, bool PRE = false>
+template <int D, int RT, int NWV, int DBG, bool PRE = false, bool PRIO = false, bool PAIR = false>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV / 4, NWV / 4)))
 void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __restrict__ ws,
                 const float* __restrict__ vec, float eps, FfnPre pre) {
@@ -135,16 +135,29 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
   };
   // slab i landed for every wave (and, at i = 0, this wave's x1 rows), slab i-1's slot
   // free; then keep FF_PD slabs in flight
+  // PAIR: one wait + barrier per two slabs (slabs i, i+1 landed; i+2, i+3 go into the
+  // slots of i-2, i-1), so a wave's LDS reads of the second slab overlap the MFMAs of
+  // the first; two slabs in flight instead of three.
   auto step = [&](int i) -> const char* {
-    if (DBG != 1) {
-      ff_wait<BPW>(min(FF_PD - 1, NSLAB - 1 - i));
-      __builtin_amdgcn_s_barrier();
+    if constexpr (PAIR) {
+      if ((i & 1) == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(i + 2);
+        issue(i + 3);
+      }
+    } else {
+      if (DBG != 1) {
+        ff_wait<BPW>(min(FF_PD - 1, NSLAB - 1 - i));
+        __builtin_amdgcn_s_barrier();
+      }
+      issue(i + FF_PD);
     }
-    issue(i + FF_PD);
     return ring + (i % FF_NSLOT) * FF_SLAB + lane * 16;
   };
+  static_assert(!PAIR || NSLAB % 2 == 0, "PAIR needs an even slab count");
 #pragma unroll
-  for (int i = 0; i < FF_PD; ++i) issue(i);
+  for (int i = 0; i < (PAIR ? 2 : FF_PD); ++i) issue(i);
 
   f32x4 acc[RT][NT];
 #pragma unroll
@@ -168,10 +181,12 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
           for (int t = 0; t < 8; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 2 + s2) * 1024);
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + 2 * c + s2) * 1024);
+          if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int t = 0; t < 8; ++t)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) acc[rt][nb * 8 + t] = mfma_bf16(a[t], b[rt], acc[rt][nb * 8 + t]);
+          if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         }
       }
     }
@@ -241,6 +256,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
         for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 4 + s) * 1024);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + kb * 4 + s) * 1024);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -248,6 +264,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
             if (DBG == 2) h[rt][t][0] += __builtin_bit_cast(float, a[t][0] ^ b[rt][0]);
             else h[rt][t] = mfma_bf16(a[t], b[rt], h[rt][t]);
           }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       }
     }
     // bias + LeakyReLU(0.1) + LN_f running sums; pack h^T as phase-2 B operands
@@ -281,6 +298,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
         u32x4 a[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 2 + s2) * 1024);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -288,6 +306,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
             if (DBG == 2) acc[rt][nb * 8 + t][0] += __builtin_bit_cast(float, a[t][0] ^ hf[rt][s2][0]);
             else acc[rt][nb * 8 + t] = mfma_bf16(a[t], hf[rt][s2], acc[rt][nb * 8 + t]);
           }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       }
     }
   }
@@ -392,7 +411,10 @@ template <int D>
 static int launch_ffn_pre(int64_t M, const void* att, void* x, const void* ws, const float* vec, float eps,
                           const FfnPre& pre, hipStream_t s) {
   constexpr size_t lds = FfnShape<D>::LDS;
-  auto kern = ffn_kernel<D, 1, 8, 0, true>;
+  static const bool prio = getenv("SNVRAG_FFN_NOPRIO") == nullptr;
+  static const bool pair = getenv("SNVRAG_FFN_NOPAIR") == nullptr;
+  auto kern = pair ? ffn_kernel<D, 1, 8, 0, true, true, true>
+              : prio ? ffn_kernel<D, 1, 8, 0, true, true> : ffn_kernel<D, 1, 8, 0, true>;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(512), lds, s, (int)M, (const bf16*)att, (bf16*)x,
                      (const char*)ws, vec, eps, pre);
@@ -405,8 +427,12 @@ static int launch_ffn(int64_t M, const void* x1, void* out, const void* ws, cons
   constexpr size_t lds = FfnShape<D>::LDS;
   static const int dbg = getenv("SNVRAG_FFN_DBG") ? atoi(getenv("SNVRAG_FFN_DBG")) : 0;
   static const bool one = getenv("SNVRAG_FFN_1W") != nullptr;   // one wave per SIMD variant
+  static const bool prio = getenv("SNVRAG_FFN_NOPRIO") == nullptr;
+  static const bool pair = getenv("SNVRAG_FFN_NOPAIR") == nullptr;
   auto kern = one ? (dbg == 1 ? ffn_kernel<D, 2, 4, 1> : dbg == 2 ? ffn_kernel<D, 2, 4, 2> : ffn_kernel<D, 2, 4, 0>)
-                  : (dbg == 1 ? ffn_kernel<D, 1, 8, 1> : dbg == 2 ? ffn_kernel<D, 1, 8, 2> : ffn_kernel<D, 1, 8, 0>);
+                  : (dbg == 1 ? ffn_kernel<D, 1, 8, 1> : dbg == 2 ? ffn_kernel<D, 1, 8, 2>
+                     : pair ? ffn_kernel<D, 1, 8, 0, false, true, true>
+                     : prio ? ffn_kernel<D, 1, 8, 0, false, true> : ffn_kernel<D, 1, 8, 0>);
   const int nthr = one ? 256 : 512;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(nthr), lds, s, (int)M, (const bf16*)x1, (bf16*)out,

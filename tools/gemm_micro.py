@@ -83,7 +83,7 @@ def main():
     variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
     only = os.environ.get("GM_CASE")
     for name, (fn, m, n, k, extra) in cases.items():
-        if only and only not in name:
+        if only and not any(o in name for o in only.split(",")):
             continue
         flop = 2.0 * m * n * k
         byts = 2.0 * (m * k + n * k + m * n * (1 + extra)) if extra >= 0 else 2.0 * 2 * m * k
