@@ -31,7 +31,6 @@ namespace snvrag {
 constexpr int FF_SLAB = 16384;   // bytes per weight slab = 16 fragment blocks of 1 KiB
 constexpr int FF_NSLOT = 4;      // LDS ring slots
 constexpr int FF_PD = 3;         // slabs in flight (<= NSLOT - 1)
-constexpr int FF_ROWS = 128;     // token rows per workgroup (4 waves x 32)
 
 // vector table (f32) offsets, in units of D: b1[4D] b2' c1 g2 be2
 enum { FV_B1 = 0, FV_B2 = 4, FV_C1 = 5, FV_G2 = 6, FV_BE2 = 7, FV_N = 8 };
@@ -53,6 +52,11 @@ template <int D> struct FfnShape {
 __device__ __forceinline__ void ff_glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+// streaming (read-once) rows: non-temporal, so they do not push the weight stream out of L2
+__device__ __forceinline__ void ff_glds16_nt(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
 }
 
 template <int BPW> __device__ __forceinline__ void ff_wait(int younger) {
@@ -83,8 +87,13 @@ struct FfnPre {            // PRE: x1 = LN1(resid + att W_o^T + b_o)
   const bf16* resid; const char* wo; const float* b_o; const float* g1; const float* be1;
 };
 
-template <int D, int RT, int NWV, int DBG, bool PRE = false, bool PRIO = false, bool PAIR = false>
-__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV / 4, NWV / 4)))
+// G: slabs per wait+barrier (1: three slabs in flight, slab-wise; 2, 4: G landed, G in flight).
+// XREG: this wave's x1 (and, PRE, att) rows live in VGPRs instead of LDS; the whole LDS is ring.
+// SLOTS: ring slots for G = 1 (SLOTS - 1 slabs in flight); WPE: waves per SIMD the register
+// budget is sized for (2 with NWV = 4 means two workgroups per CU).
+template <int D, int RT, int NWV, int DBG, bool PRE = false, bool PRIO = false, int G = 1, bool XREG = false,
+          bool NTS = false, int SLOTS = FF_NSLOT, int WPE = NWV / 4>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __restrict__ ws,
                 const float* __restrict__ vec, float eps, FfnPre pre) {
   using S = FfnShape<D>;
@@ -96,25 +105,37 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   constexpr int BPW = 16 / NWV;                    // 1-KiB blocks of a slab loaded per wave
-  static_assert(RT * 16 * NWV == FF_ROWS, "tile rows");
-  const long rbase = (long)blockIdx.x * FF_ROWS + wave * 16 * RT;
+  constexpr int ROWS = RT * 16 * NWV;
+  constexpr int PD = SLOTS - 1;
+  const long rbase = (long)blockIdx.x * ROWS + wave * 16 * RT;
   // this wave's x1 rows, B-operand fragment blocks [rt][s], lane-linear 16 B each
   char* xt = smem + wave * (RT * KS * 1024);
   const char* xtl = xt + lane * 16;
-  char* ring = smem + S::XT;
+  char* ring = smem + (XREG ? 0 : NWV * RT * KS * 1024);
+  constexpr int NSLOT = G == 1 ? SLOTS : 2 * G;
+  u32x4 xr[XREG ? RT : 1][XREG ? KS : 1];
+  // B operand block idx (32 k) of row tile rt: registers or the LDS tile
+  auto xb = [&](int rt, int idx) -> u32x4 {
+    if constexpr (XREG) return xr[rt][idx];
+    else return *reinterpret_cast<const u32x4*>(xtl + (rt * KS + idx) * 1024);
+  };
 
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const long r = min(rbase + rt * 16 + li, (long)M - 1);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) ff_glds16(x1 + r * D + 32 * s + 8 * lg, xt + (rt * KS + s) * 1024);
+    for (int s = 0; s < KS; ++s) {
+      if constexpr (XREG) xr[rt][s] = *reinterpret_cast<const u32x4*>(x1 + r * D + 32 * s + 8 * lg);
+      else if constexpr (NTS) ff_glds16_nt(x1 + r * D + 32 * s + 8 * lg, xt + (rt * KS + s) * 1024);
+      else ff_glds16(x1 + r * D + 32 * s + 8 * lg, xt + (rt * KS + s) * 1024);
+    }
   }
 
   // Workgroups start at different hidden chunks (the FFN sums over chunks, so any
   // order is the same sum): concurrent CUs of an XCD then read different slabs
   // instead of all hitting the same L2 channels with the same 16 KiB.
   const int rot = (int)(blockIdx.x % S::NCH);
-  const int rotp = PRE ? (int)(blockIdx.x % (NCHP > 0 ? NCHP : 1)) : 0;
+  const int rotp = (PRE && !XREG) ? (int)(blockIdx.x % (NCHP > 0 ? NCHP : 1)) : 0;
   auto issue = [&](int i) {
     if (DBG != 1 && i < NSLAB) {
       const char* src;
@@ -128,7 +149,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
         cc = cc >= S::NCH ? cc - S::NCH : cc;
         src = ws + ((long)cc * S::SPC + k % S::SPC) * FF_SLAB + wave * BPW * 1024 + lane * 16;
       }
-      char* dst = ring + (i % FF_NSLOT) * FF_SLAB + wave * BPW * 1024;
+      char* dst = ring + (i % NSLOT) * FF_SLAB + wave * BPW * 1024;
 #pragma unroll
       for (int j = 0; j < BPW; ++j) ff_glds16(src + j * 1024, dst + j * 1024);
     }
@@ -139,25 +160,24 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
   // slots of i-2, i-1), so a wave's LDS reads of the second slab overlap the MFMAs of
   // the first; two slabs in flight instead of three.
   auto step = [&](int i) -> const char* {
-    if constexpr (PAIR) {
-      if ((i & 1) == 0) {
+    if constexpr (G > 1) {
+      if (i % G == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        issue(i + 2);
-        issue(i + 3);
+#pragma unroll
+        for (int g = 0; g < G; ++g) issue(i + G + g);
       }
     } else {
       if (DBG != 1) {
-        ff_wait<BPW>(min(FF_PD - 1, NSLAB - 1 - i));
+        ff_wait<BPW>(min(PD - 1, NSLAB - 1 - i));
         __builtin_amdgcn_s_barrier();
       }
-      issue(i + FF_PD);
+      issue(i + PD);
     }
-    return ring + (i % FF_NSLOT) * FF_SLAB + lane * 16;
+    return ring + (i % NSLOT) * FF_SLAB + lane * 16;
   };
-  static_assert(!PAIR || NSLAB % 2 == 0, "PAIR needs an even slab count");
 #pragma unroll
-  for (int i = 0; i < (PAIR ? 2 : FF_PD); ++i) issue(i);
+  for (int i = 0; i < (G > 1 ? G : PD); ++i) issue(i);
 
   f32x4 acc[RT][NT];
 #pragma unroll
@@ -168,7 +188,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
   int slab = 0;
   if constexpr (PRE) {
     // ---- acc = att W_o'^T (att rows are this wave's LDS tile, k order of the x1 layout)
-#pragma unroll 1
+#pragma unroll
     for (int c0 = 0; c0 < NCHP; ++c0) {
       const int c = c0 + rotp >= NCHP ? c0 + rotp - NCHP : c0 + rotp;
 #pragma unroll
@@ -180,7 +200,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
 #pragma unroll
           for (int t = 0; t < 8; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 2 + s2) * 1024);
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + 2 * c + s2) * 1024);
+          for (int rt = 0; rt < RT; ++rt) b[rt] = xb(rt, 2 * c + s2);
           if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int t = 0; t < 8; ++t)
@@ -197,11 +217,11 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
       float sum = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const u32x4 xr = *reinterpret_cast<const u32x4*>(pre.resid + r * D + 32 * s + 8 * lg);
+        const u32x4 rv = *reinterpret_cast<const u32x4*>(pre.resid + r * D + 32 * s + 8 * lg);
         const float* bo = pre.b_o + 32 * s + 8 * lg;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = acc[rt][2 * s + (j >> 2)][j & 3] + bo[j] + bfx(xr, j);
+          const float v = acc[rt][2 * s + (j >> 2)][j & 3] + bo[j] + bfx(rv, j);
           acc[rt][2 * s + (j >> 2)][j & 3] = v;
           sum += v;
         }
@@ -224,8 +244,9 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
         float y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (acc[rt][2 * s + (j >> 2)][j & 3] - mean) * rstd * g[j] + b[j];
-        *reinterpret_cast<u32x4*>(xt + (rt * KS + s) * 1024 + lane * 16) =
-            u32x4{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+        const u32x4 xv{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+        if constexpr (XREG) xr[rt][s] = xv;
+        else *reinterpret_cast<u32x4*>(xt + (rt * KS + s) * 1024 + lane * 16) = xv;
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -255,7 +276,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
 #pragma unroll
         for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const u32x4*>(sl + (t * 4 + s) * 1024);
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) b[rt] = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + kb * 4 + s) * 1024);
+        for (int rt = 0; rt < RT; ++rt) b[rt] = xb(rt, kb * 4 + s);
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -324,14 +345,14 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
     float sum = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const u32x4 xr = *reinterpret_cast<const u32x4*>(xtl + (rt * KS + s) * 1024);
+      const u32x4 xrs = xb(rt, s);
       const float* c1 = vec + FV_C1 * D + 32 * s + 8 * lg;
       const float* b2 = vec + FV_B2 * D + 32 * s + 8 * lg;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float u = hr * acc[rt][2 * s + (j >> 2)][j & 3] - hr * hm * c1[j] + b2[j];
         u = u >= 0.f ? u : 0.1f * u;
-        const float v = u + bfx(xr, j);
+        const float v = u + bfx(xrs, j);
         acc[rt][2 * s + (j >> 2)][j & 3] = v;
         sum += v;
       }
@@ -356,8 +377,9 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
         float y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (acc[rt][2 * s + (j >> 2)][j & 3] - mean) * rstd * g[j] + b[j];
-        *reinterpret_cast<u32x4*>(out + r * D + 32 * s + 8 * lg) =
-            u32x4{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+        const u32x4 ov{pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]), pack_bf2(y[4], y[5]), pack_bf2(y[6], y[7])};
+        if constexpr (NTS) __builtin_nontemporal_store(ov, reinterpret_cast<u32x4*>(out + r * D + 32 * s + 8 * lg));
+        else *reinterpret_cast<u32x4*>(out + r * D + 32 * s + 8 * lg) = ov;
       }
     }
   }
@@ -407,38 +429,49 @@ __global__ void ffn_pre_pack_kernel(int D, long n_pieces, const bf16* __restrict
 
 static bool ffn_d_ok(int D) { return D == 128 || D == 256 || D == 384; }
 
-template <int D>
-static int launch_ffn_pre(int64_t M, const void* att, void* x, const void* ws, const float* vec, float eps,
-                          const FfnPre& pre, hipStream_t s) {
-  constexpr size_t lds = FfnShape<D>::LDS;
-  static const bool prio = getenv("SNVRAG_FFN_NOPRIO") == nullptr;
-  static const bool pair = getenv("SNVRAG_FFN_NOPAIR") == nullptr;
-  auto kern = pair ? ffn_kernel<D, 1, 8, 0, true, true, true>
-              : prio ? ffn_kernel<D, 1, 8, 0, true, true> : ffn_kernel<D, 1, 8, 0, true>;
+// variant (SNVRAG_FFN_VARIANT): 0 = slab-wise ring (3 in flight), x1 in LDS; 1 = slab pairs, x1 in
+// LDS (default); 2 = 4-slab groups, x1 in VGPRs; 4 = 4 waves x 16 rows, two workgroups per CU
+static int ffn_variant() {
+  static const int v = getenv("SNVRAG_FFN_VARIANT") ? atoi(getenv("SNVRAG_FFN_VARIANT")) : 1;
+  return v;
+}
+
+template <int D, bool PRE, int NWV, int G, bool XREG, bool NTS, int SLOTS, int WPE>
+static int launch_ffn_k(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps,
+                        const FfnPre& pre, hipStream_t s) {
+  auto kern = ffn_kernel<D, 1, NWV, 0, PRE, true, G, XREG, NTS, SLOTS, WPE>;
+  constexpr int KS = D / 32;
+  const size_t lds = XREG ? (size_t)2 * G * FF_SLAB
+                          : (size_t)NWV * KS * 1024 + (size_t)(G == 1 ? SLOTS : 2 * G) * FF_SLAB;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(512), lds, s, (int)M, (const bf16*)att, (bf16*)x,
-                     (const char*)ws, vec, eps, pre);
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, 16 * NWV)), dim3(64 * NWV), lds, s, (int)M, (const bf16*)x1,
+                     (bf16*)out, (const char*)ws, vec, eps, pre);
   SNV_LAUNCH_CHECK();
   return 0;
 }
 
+template <int D, bool PRE>
+static int launch_ffn_v(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps,
+                        const FfnPre& pre, hipStream_t s) {
+  switch (ffn_variant()) {
+    case 0: return launch_ffn_k<D, PRE, 8, 1, false, false, 4, 2>(M, x1, out, ws, vec, eps, pre, s);
+    // measured slower at D = 384, M = 527 360 (tools/gemm_micro.py): x1 in VGPRs with 4-slab groups (+3 %),
+    // 64-row workgroups two per CU (+4 %: the weight stream is read twice as often)
+    case 2: return launch_ffn_k<D, PRE, 8, 4, true, false, 4, 2>(M, x1, out, ws, vec, eps, pre, s);
+    case 4: return launch_ffn_k<D, PRE, 4, 1, false, false, 2, 2>(M, x1, out, ws, vec, eps, pre, s);
+    default: return launch_ffn_k<D, PRE, 8, 2, false, false, 4, 2>(M, x1, out, ws, vec, eps, pre, s);
+  }
+}
+
 template <int D>
 static int launch_ffn(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps, hipStream_t s) {
-  constexpr size_t lds = FfnShape<D>::LDS;
-  static const int dbg = getenv("SNVRAG_FFN_DBG") ? atoi(getenv("SNVRAG_FFN_DBG")) : 0;
-  static const bool one = getenv("SNVRAG_FFN_1W") != nullptr;   // one wave per SIMD variant
-  static const bool prio = getenv("SNVRAG_FFN_NOPRIO") == nullptr;
-  static const bool pair = getenv("SNVRAG_FFN_NOPAIR") == nullptr;
-  auto kern = one ? (dbg == 1 ? ffn_kernel<D, 2, 4, 1> : dbg == 2 ? ffn_kernel<D, 2, 4, 2> : ffn_kernel<D, 2, 4, 0>)
-                  : (dbg == 1 ? ffn_kernel<D, 1, 8, 1> : dbg == 2 ? ffn_kernel<D, 1, 8, 2>
-                     : pair ? ffn_kernel<D, 1, 8, 0, false, true, true>
-                     : prio ? ffn_kernel<D, 1, 8, 0, false, true> : ffn_kernel<D, 1, 8, 0>);
-  const int nthr = one ? 256 : 512;
-  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, FF_ROWS)), dim3(nthr), lds, s, (int)M, (const bf16*)x1, (bf16*)out,
-                     (const char*)ws, vec, eps, FfnPre{});
-  SNV_LAUNCH_CHECK();
-  return 0;
+  return launch_ffn_v<D, false>(M, x1, out, ws, vec, eps, FfnPre{}, s);
+}
+
+template <int D>
+static int launch_ffn_pre(int64_t M, const void* att, void* x, const void* ws, const float* vec, float eps,
+                          const FfnPre& pre, hipStream_t s) {
+  return launch_ffn_v<D, true>(M, att, x, ws, vec, eps, pre, s);
 }
 
 }  // namespace snvrag
