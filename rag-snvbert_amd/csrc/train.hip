@@ -321,15 +321,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
   }
 }
 
-// out[n] (+)= sum over rows r of x[r, n] (f32 partials [R, N] -> N, or bf16 [M, N] -> N)
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(long R, int N, const T* __restrict__ x, float* __restrict__ out,
-                                                     int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float acc = 0.f;
-  for (long r = 0; r < R; ++r) acc += to_f32(x[r * N + n]);
-  out[n] = accumulate ? out[n] + acc : acc;
+// out[n] (+)= sum over the R rows of f32 partials x[R, N]: 16 columns x 16 row groups per
+// block (64-B row segments), four independent loads in flight per thread, fixed-order
+// reduction of the groups (deterministic).  In-place use (out == x, row 0) is safe: a
+// block writes only its own columns, after all of its reads.
+__global__ __launch_bounds__(256) void colsum_f32_kernel(long R, int N, const float* x, float* out,
+                                                         int accumulate) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < N) {
+    long r = g;
+    for (; r + 48 < R; r += 64) {
+      a0 += x[r * N + c];
+      a1 += x[(r + 16) * N + c];
+      a2 += x[(r + 32) * N + c];
+      a3 += x[(r + 48) * N + c];
+    }
+    for (; r < R; r += 16) a0 += x[r * N + c];
+  }
+  red[g][cl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (g == 0 && c < N) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum += red[i][cl];
+    out[c] = accumulate ? out[c] + sum : sum;
+  }
 }
 
 // column sums of a bf16 [M, N] matrix (bias gradients): per-block partials over row slabs
@@ -392,8 +411,8 @@ extern "C" int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, co
                      (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, part);
   SNV_LAUNCH_CHECK();
   // reduce the [nblk][2][N] partials: dg = part[:, 0, :], db = part[:, 1, :]
-  hipLaunchKernelGGL(colsum_kernel<float>, dim3(cdiv(2 * N, 256)), dim3(256), 0, st, (long)nblk, 2 * N,
-                     (const float*)part, part, 0);   // rows of 2N: in-place into row 0 (read-before-write per column)
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, 2 * N,
+                     (const float*)part, part, 0);   // rows of 2N: in place into row 0
   SNV_LAUNCH_CHECK();
   SNV_HIP(hipMemcpyAsync(dg, part, N * sizeof(float), hipMemcpyDeviceToDevice, st));
   SNV_HIP(hipMemcpyAsync(db, part + N, N * sizeof(float), hipMemcpyDeviceToDevice, st));
@@ -418,8 +437,8 @@ extern "C" int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, v
   hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)nblk), dim3(256), per * N * sizeof(float), st, (long)M, N,
                      rpb, (const bf16*)x, (float*)ws);
   SNV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_kernel<float>, dim3(cdiv(N, 256)), dim3(256), 0, st, (long)nblk, N, (const float*)ws,
-                     out, 0);
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)ws, out,
+                     0);
   SNV_LAUNCH_CHECK();
   return 0;
 }

@@ -52,12 +52,26 @@ def af_embedding(afm, af: torch.Tensor) -> torch.Tensor:
     return hip_linear(h, pr[3].weight, pr[3].bias)
 
 
+def _conv1d(x: torch.Tensor, conv) -> torch.Tensor:
+    """nn.Conv1d (stride 1, zero padding) as one batched [Cout, Cin*k] x [Cin*k, L] product over
+    the k shifted copies of x.  At these channel counts (1-4, k = 9) the library's convolution
+    weight-gradient kernels take milliseconds per call; this form's backward is two small GEMMs
+    and a few slices (f32 throughout, as the reference runs it with autocast off)."""
+    assert conv.stride == (1,) and conv.dilation == (1,) and conv.groups == 1
+    w = conv.weight
+    k, p, L = w.shape[-1], conv.padding[0], x.shape[-1]
+    xp = F.pad(x, (p, p))
+    cols = torch.stack([xp[..., j:j + L] for j in range(k)], 2)          # [B, Cin, k, L]
+    out = torch.matmul(w.reshape(w.shape[0], -1), cols.reshape(x.shape[0], -1, L))
+    return out + conv.bias[:, None]
+
+
 def pos_feat(pfm, pos: torch.Tensor) -> torch.Tensor:
     """PositionFeatModule.forward (fusion.py:317-332), f32, BatchNorm in the module's mode."""
     out = pos.float().unsqueeze(1)
-    out = pfm.norm1(F.leaky_relu(pfm.conv1(out), 0.05))
-    out = pfm.norm2(F.leaky_relu(pfm.conv2(out), 0.05))
-    return F.leaky_relu(pfm.conv3(out), 0.05).squeeze(1)
+    out = pfm.norm1(F.leaky_relu(_conv1d(out, pfm.conv1), 0.05))
+    out = pfm.norm2(F.leaky_relu(_conv1d(out, pfm.conv2), 0.05))
+    return F.leaky_relu(_conv1d(out, pfm.conv3), 0.05).squeeze(1)
 
 
 def _linear_cat2(x: torch.Tensor, lin, c1: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
