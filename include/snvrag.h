@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 9
+#define SNVRAG_ABI_VERSION 10
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -283,14 +283,18 @@ int snvrag_block_tail_forward(int64_t M, int D, const void* att, void* x, const 
 
 /* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
  * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either
- * act(.) (ln_g == NULL) or LN(. + resid) * ln_g + ln_b (N == K, resid [M, ld_resid]).
+ * act(.) (ln_g == NULL) or LN(act(.) + resid) * ln_g + ln_b (N == K, resid [M, ld_resid]).
+ * Optional rank-1 terms row1[m'] * col1[n] + row2[m'] * col2[n] join the bias before the
+ * activation (m' = m % row_period when row_period > 0): the cat(x, af, af_p) Linear inputs of
+ * fusion.py:355-360 and foundation_model.py:25-33 without widening K.
  * A [M, K] contiguous; W packed once by snvrag_wsg_pack (wsg_pack_bytes(N, K) bytes).
  * K in {128, 256, 384}, N % 64 == 0 (N / 64 in {2,4,6,8,12,16,18,24} without LN). */
 size_t snvrag_wsg_pack_bytes(int64_t N, int64_t K);
 int snvrag_wsg_pack(int64_t N, int64_t K, const void* w, void* out, void* stream);
 int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
                        int act, float slope, const void* resid, int64_t ld_resid, const float* ln_g,
-                       const float* ln_b, float eps, void* out, int64_t ldo, void* stream);
+                       const float* ln_b, float eps, const float* row1, const float* col1, const float* row2,
+                       const float* col2, int64_t row_period, void* out, int64_t ldo, void* stream);
 
 /* Hap-classifier tail in one pass (foundation_model.py:77-80): probs[M, 2] =
  * softmax(act(A W^T + bias) w_out^T + b_out), logits (nullable) before the softmax;

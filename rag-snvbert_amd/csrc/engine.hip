@@ -82,7 +82,7 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       e.bias = ly.b_qkv;
       if (dtype == SNVRAG_BF16 && ly.qkv_ws && !getenv("SNVRAG_NO_WSG"))
         rc = snvrag_wsg_forward(M, 3 * D, D, xc, ly.qkv_ws, ly.b_qkv, SNVRAG_ACT_NONE, 0.f, nullptr, 0, nullptr,
-                                nullptr, 0.f, qkv, 3 * D, stream);
+                                nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, 0, qkv, 3 * D, stream);
       else
         rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
       if (rc) return rc;

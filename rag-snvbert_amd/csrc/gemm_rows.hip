@@ -308,7 +308,7 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
           for (int e = 0; e < 8; ++e) v[j][e] = v[j][e] >= 0.f ? v[j][e] : v[j][e] * epi.slope;
         } else if (epi.act) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[j][e] = apply_act(epi.act, v[j][e], epi.slope);
+          for (int e = 0; e < 8; ++e) v[j][e] = apply_act_t<TO>(epi.act, v[j][e], epi.slope);
         }
         if (epi.resid) {
 #pragma unroll

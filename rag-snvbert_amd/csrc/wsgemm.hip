@@ -61,6 +61,10 @@ struct WsEpi {
   // EPI 2 (hap head, foundation_model.py:77-80): logits = act(.) w_out^T + b_out (2 outputs),
   // probs = softmax(logits); the 4D hidden never leaves the registers
   const float* w_out; const float* b_out; float* logits; float* probs;
+  // EPI 0 / 1: rank-1 row x column terms added before the activation (the cat(x, af, af_p)
+  // columns of fusion.py:355-360 / foundation_model.py:25-33 as rank updates); row index
+  // taken modulo row_period when > 0
+  const float* row1; const float* col1; const float* row2; const float* col2; long row_period;
 };
 
 template <int K, int NCH, int EPI>
@@ -105,6 +109,12 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
 
   const long row = rbase + li;
   const bool rv = row < M;
+  float rk1 = 0.f, rk2 = 0.f;
+  if constexpr (EPI != 2) {
+    const long rr = e.row_period > 0 ? (rv ? row : 0) % e.row_period : (rv ? row : 0);
+    if (e.row1) rk1 = e.row1[rr];
+    if (e.row2) rk2 = e.row2[rr];
+  }
   float keep[EPI == 1 ? NCH : 1][16];
   float po0 = 0.f, po1 = 0.f;                     // EPI 2 partial logits
   int slab = 0;
@@ -138,13 +148,35 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
       v[4 * t + 2] = h[t][2] + bb.z;
       v[4 * t + 3] = h[t][3] + bb.w;
     }
+    if constexpr (EPI != 2) {
+      if (e.row1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float4 cc = *reinterpret_cast<const float4*>(e.col1 + c * 64 + 16 * lg + 4 * t);
+          v[4 * t + 0] = fmaf(rk1, cc.x, v[4 * t + 0]);
+          v[4 * t + 1] = fmaf(rk1, cc.y, v[4 * t + 1]);
+          v[4 * t + 2] = fmaf(rk1, cc.z, v[4 * t + 2]);
+          v[4 * t + 3] = fmaf(rk1, cc.w, v[4 * t + 3]);
+        }
+      }
+      if (e.row2) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float4 cc = *reinterpret_cast<const float4*>(e.col2 + c * 64 + 16 * lg + 4 * t);
+          v[4 * t + 0] = fmaf(rk2, cc.x, v[4 * t + 0]);
+          v[4 * t + 1] = fmaf(rk2, cc.y, v[4 * t + 1]);
+          v[4 * t + 2] = fmaf(rk2, cc.z, v[4 * t + 2]);
+          v[4 * t + 3] = fmaf(rk2, cc.w, v[4 * t + 3]);
+        }
+      }
+    }
     if constexpr (EPI == 2) {
       if (e.act == SNVRAG_ACT_LRELU) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * e.slope;
       } else if (e.act) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = apply_act(e.act, v[j], e.slope);
+        for (int j = 0; j < 16; ++j) v[j] = apply_act_t<bf16>(e.act, v[j], e.slope);
       }
       const int col = c * 64 + 16 * lg;
 #pragma unroll
@@ -160,7 +192,7 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
         for (int j = 0; j < 16; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * e.slope;
       } else if (e.act) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = apply_act(e.act, v[j], e.slope);
+        for (int j = 0; j < 16; ++j) v[j] = apply_act_t<bf16>(e.act, v[j], e.slope);
       }
       if (rv) {
         u32x4* op = reinterpret_cast<u32x4*>(out + row * ldo + c * 64 + 16 * lg);
@@ -168,6 +200,13 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
         op[1] = u32x4{ws_pack2(v[8], v[9]), ws_pack2(v[10], v[11]), ws_pack2(v[12], v[13]), ws_pack2(v[14], v[15])};
       }
     } else {
+      if (e.act == SNVRAG_ACT_LRELU) {   // act(.) + residual, then the LayerNorm
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * e.slope;
+      } else if (e.act) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = apply_act_t<bf16>(e.act, v[j], e.slope);
+      }
 #pragma unroll
       for (int j = 0; j < 16; ++j) keep[c0][j] = v[j];
     }
@@ -273,7 +312,8 @@ extern "C" int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, 
                 "A/w_out/bias must be 16-byte aligned");
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
-  WsEpi e{bias, act, slope, nullptr, 0, nullptr, nullptr, 0.f, w_out, b_out, logits, probs};
+  WsEpi e{bias, act, slope, nullptr, 0, nullptr, nullptr, 0.f, w_out, b_out, logits, probs,
+          nullptr, nullptr, nullptr, nullptr, 0};
   int rc = -1;
   evlog_begin(s);
   if (K == 384 && N == 1536) rc = launch_wsg<384, 24, 2>(M, A, wstream, nullptr, 0, e, s);
@@ -303,8 +343,9 @@ extern "C" int snvrag_wsg_pack(int64_t N, int64_t K, const void* w, void* out, v
 
 extern "C" int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream,
                                   const float* bias, int act, float slope, const void* resid, int64_t ld_resid,
-                                  const float* ln_g, const float* ln_b, float eps, void* out, int64_t ldo,
-                                  void* stream) {
+                                  const float* ln_g, const float* ln_b, float eps, const float* row1,
+                                  const float* col1, const float* row2, const float* col2, int64_t row_period,
+                                  void* out, int64_t ldo, void* stream) {
   SNV_CHECK_ARG(A && wstream && bias && out, "null pointer");
   SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
   SNV_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wstream % 16) == 0 &&
@@ -312,7 +353,10 @@ extern "C" int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A
                 "A/out/wstream/bias must be 16-byte aligned, ldo % 8 == 0");
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
-  WsEpi e{bias, act, slope, (const bf16*)resid, (long)ld_resid, ln_g, ln_b, eps};
+  SNV_CHECK_ARG((!row1 || (col1 && ((uintptr_t)col1 % 16) == 0)) && (!row2 || (col2 && ((uintptr_t)col2 % 16) == 0)),
+                "row terms need 16-byte aligned column vectors");
+  WsEpi e{bias, act, slope, (const bf16*)resid, (long)ld_resid, ln_g, ln_b, eps, nullptr, nullptr, nullptr, nullptr,
+          row1, col1, row2, col2, (long)row_period};
   const bool ln = ln_g != nullptr;
   SNV_CHECK_ARG(!ln || (ln_b && resid && ld_resid % 8 == 0), "LayerNorm epilogue needs ln_b and a residual");
   evlog_begin(s);

@@ -110,6 +110,8 @@ class Engine:
         f32 = lambda t: t.detach().to(dev, torch.float32).contiguous()
         cvt = lambda t: t.detach().to(dev, T).contiguous()
         P.keep = []
+        # weight-streaming GEMM (csrc/wsgemm.hip) for the K = D projections at bf16
+        use_ws = T == torch.bfloat16 and os.environ.get("SNVRAG_NO_WSG") is None
 
         def afmlp(a):
             return dict(freqs=f32(a.basis_freqs), w0=cvt(a.projection[0].weight), b0=f32(a.projection[0].bias),
@@ -133,6 +135,9 @@ class Engine:
         fw = f32(ef.fusion.weight)
         P.ef = dict(w=cvt(fw[:, :D]), c_pos=fw[:, D].contiguous(), c_af=fw[:, D + 1].contiguous(),
                     b=f32(ef.fusion.bias), g=f32(ef.norm.weight), bb=f32(ef.norm.bias))
+        ws_ok = use_ws and D in (128, 256, 384)
+        # (emb_fusion stays on the row-panel GEMM: at N = K = D over 4B*L rows the
+        #  weight-streaming LN epilogue measured 4 % slower)
         pf = ef.pos_feat
         P.pf_t = [f32(t) for t in (pf.conv1.weight, pf.conv1.bias, pf.conv2.weight, pf.conv2.bias,
                                    pf.conv3.weight, pf.conv3.bias, pf.norm1.weight, pf.norm1.bias,
@@ -152,6 +157,8 @@ class Engine:
                     f3=cvt(rf.fusion[3].weight), f3b=f32(rf.fusion[3].bias),
                     g=f32(rf.fusion[4].weight), bb=f32(rf.fusion[4].bias),
                     rs=float(rf.res_scale.detach().float().item()))
+        if ws_ok and P.rf["a0"].shape == (4 * D, D):
+            P.rf["a0_ws"] = K.wsg_pack(P.rf["a0"])
         # encoder
         P.layers_t, P.layers = [], []
         for blk in bert.transformer_blocks:
@@ -190,8 +197,9 @@ class Engine:
                     g=f32(hc.af_fusion[3].weight), bb=f32(hc.af_fusion[3].bias),
                     n0=cvt(hc.net[0].weight), n0b=f32(hc.net[0].bias),
                     n2=f32(hc.net[2].weight), n2b=f32(hc.net[2].bias))
-        if T == torch.bfloat16 and D in (128, 256, 384) and P.hh["n2"].shape[0] == 2 \
-                and os.environ.get("SNVRAG_NO_WSG") is None:
+        if ws_ok and P.hh["w0"].shape == (4 * D, D):
+            P.hh["w0_ws"] = K.wsg_pack(P.hh["w0"])
+        if ws_ok and P.hh["n2"].shape[0] == 2:
             # fused net[0] + GELU + net[2] + softmax (csrc/wsgemm.hip, EPI 2)
             P.hh["n0_ws"] = K.wsg_pack(P.hh["n0"])
         gc = fm.gt_classifier
@@ -261,12 +269,19 @@ class Engine:
             hm[2 * B:].copy_(rag)
         pf = K.posfeat(pos, P.pf)                                     # [B, L]
         ef = P.ef
-        fused = K.linear(hm, ef["w"], ef["b"], row1=(pf, 1, ef["c_pos"]), row2=(af, 1, ef["c_af"]),
-                         row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm, ln=(ef["g"], ef["bb"]))
+        if "w_ws" in ef:
+            fused = K.wsg_linear(hm, ef["w_ws"], D, ef["b"], act=N.ACT_LRELU, slope=0.1, resid=hm,
+                                 ln=(ef["g"], ef["bb"]), row1=(pf, ef["c_pos"]), row2=(af, ef["c_af"]), row_period=BL)
+        else:
+            fused = K.linear(hm, ef["w"], ef["b"], row1=(pf, 1, ef["c_pos"]), row2=(af, 1, ef["c_af"]),
+                             row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm, ln=(ef["g"], ef["bb"]))
         if rag is not None:
             rf = P.rf
             fa = K.af_gate(af, af_p, P.ag, D, T)                      # [B, L, D]
-            t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
+            if "a0_ws" in rf:
+                t = K.wsg_linear(fa, rf["a0_ws"], rf["a0"].shape[0], rf["a0b"], act=N.ACT_GELU)
+            else:
+                t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
             aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
             cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
             h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
@@ -287,8 +302,12 @@ class Engine:
         B, L = o["B"], o["L"]
         BL = B * L
         hh = P.hh
-        h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
-                     row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
+        if "w0_ws" in hh:
+            h = K.wsg_linear(o["x_all"], hh["w0_ws"], hh["w0"].shape[0], hh["b0"], act=N.ACT_GELU,
+                             row1=(o["af"], hh["c_af"]), row2=(o["af_p"], hh["c_afp"]), row_period=BL)
+        else:
+            h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
+                         row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
         h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
         if "n0_ws" in hh:
             logits, probs = K.wsg_head2(h, hh["n0_ws"], hh["n0"].shape[0], hh["n0b"], hh["n2"], hh["n2b"],

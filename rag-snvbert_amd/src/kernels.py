@@ -497,16 +497,29 @@ def wsg_pack(w: torch.Tensor) -> torch.Tensor:
 def wsg_linear(x: torch.Tensor, wstream: torch.Tensor, n_out: int, bias: torch.Tensor, *, act: int = N.ACT_NONE,
                slope: float = 0.0, resid: Optional[torch.Tensor] = None,
                ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, eps: float = 1e-5,
+               row1: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+               row2: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, row_period: int = 0,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = act(x W^T + bias + row1[m] col1 + row2[m] col2), or LN(act(.) + resid) with ``ln``;
+    ``row1 = (row_vector f32, col_vector f32 [n_out])``, row index modulo ``row_period``."""
     N.require_gpu(x)
     Kk = x.shape[-1]
     M = x.numel() // Kk
     if out is None:
         out = torch.empty(*x.shape[:-1], n_out, device=x.device, dtype=torch.bfloat16)
+    rows = []
+    for rc in (row1, row2):
+        if rc is None:
+            rows += [None, None]
+        else:
+            assert rc[0].dtype == torch.float32 and rc[1].dtype == torch.float32 and rc[1].numel() == n_out
+            assert rc[0].numel() >= (row_period if row_period > 0 else M)
+            rows += [_c(rc[0]), _c(rc[1])]
     check(N.lib().snvrag_wsg_forward(M, n_out, Kk, ptr(_c(x)), ptr(wstream), ptr(_c(bias)), act, slope,
                                      ptr(resid), n_out if resid is not None else 0,
                                      ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, eps,
-                                     ptr(out), n_out, stream_ptr()), "wsg_linear")
+                                     *[ptr(t) for t in rows], row_period, ptr(out), n_out, stream_ptr()),
+          "wsg_linear")
     return out
 
 

@@ -440,7 +440,9 @@ def test_attention_dh32_overflow_takes_exact_fallback():
 
 
 @pytest.mark.parametrize("M,N,Kd,mode", [(1000, 1152, 384, "plain"), (517, 1536, 384, "gelu"), (333, 384, 384, "ln"),
-                                        (130, 256, 256, "ln"), (77, 512, 128, "lrelu")])
+                                        (130, 256, 256, "ln"), (77, 512, 128, "lrelu"),
+                                        (900, 1536, 384, "rank_gelu"), (1203, 384, 384, "rank_lrelu_ln"),
+                                        (260, 128, 128, "rank_lrelu_ln")])
 def test_weight_streaming_gemm(M, N, Kd, mode):
     """snvrag_wsg_forward vs torch fp32 on the same bf16 operands (bf16 output: 1e-2 rel)."""
     from src import native as NN
@@ -462,6 +464,23 @@ def test_weight_streaming_gemm(M, N, Kd, mode):
         gm, bt = torch.rand(N, generator=g).to(DEV) + 0.5, torch.randn(N, generator=g).to(DEV)
         kw = dict(resid=r, ln=(gm, bt))
         ref = torch.nn.functional.layer_norm(ref + r.float(), (N,), gm, bt, 1e-5)
+    elif mode.startswith("rank"):
+        # rank-1 row x column terms with a row period (the cat(x, af, af_p) columns)
+        period = (M + 2) // 3
+        r1, r2 = torch.rand(period, generator=g).to(DEV), torch.rand(period, generator=g).to(DEV)
+        c1, c2 = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+        ri = torch.arange(M, device=DEV) % period
+        ref = ref + r1[ri, None] * c1[None] + r2[ri, None] * c2[None]
+        kw = dict(row1=(r1, c1), row2=(r2, c2), row_period=period)
+        if mode == "rank_gelu":
+            kw["act"] = NN.ACT_GELU
+            ref = torch.nn.functional.gelu(ref)
+        else:
+            r = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+            gm, bt = torch.rand(N, generator=g).to(DEV) + 0.5, torch.randn(N, generator=g).to(DEV)
+            kw.update(act=NN.ACT_LRELU, slope=0.1, resid=r, ln=(gm, bt))
+            ref = torch.nn.functional.layer_norm(torch.nn.functional.leaky_relu(ref, 0.1) + r.float(), (N,), gm, bt,
+                                                 1e-5)
     out = K().wsg_linear(x, ws, N, b, **kw)
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
 
