@@ -499,9 +499,33 @@ __global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long
 // codes itself (8x the L2->CU traffic).  Rows are n_sites_pad bytes (multiple of
 // 256); the 16-B chunk c of row r sits at c ^ (r & 15) so the 16 rows of a
 // ds_read_b128 B fragment hit 16 different bank groups.
-constexpr int S2_R = 32;                  // haplotypes per LDS stage
-constexpr int S2_CAP = 64;                // candidate slots per query (k <= 32 plus 16+ of slack)
-constexpr int S2_TH = S2_CAP - 16;  // compact when more than 48 held
+constexpr int S2_CAP = 64;                // candidate slots per query (k <= 32 plus 32 of slack)
+constexpr int S2_TH = S2_CAP - 16;        // compact when more than 48 held (a row gains <= 16 between checks)
+constexpr int S2_LDS = 160 * 1024;        // whole LDS of a CU: one workgroup per CU
+constexpr int S2_CAND = 8 * 16 * S2_CAP * 8;
+// 32 haplotypes per LDS stage, ring of up to 3 stages in the LDS left beside the
+// candidate lists.  Measured (1 M haplotypes x 1024 sites, 48/96/128 queries): 16-row
+// stages in a 6-deep ring are 15-17 % slower (per-stage barrier + filter overhead
+// dominates, not HBM latency), and 48-slot candidate lists another 12 % (compaction
+// after every insert once k = 32 slots are held).
+__host__ __device__ constexpr int s2_rows(int KS) { return 32; }
+__host__ __device__ constexpr int s2_nst(int KS) {
+  return (S2_LDS - S2_CAND) / (s2_rows(KS) * KS * 64) > 3 ? 3 : (S2_LDS - S2_CAND) / (s2_rows(KS) * KS * 64);
+}
+
+// s_waitcnt vmcnt(PPW * min(y, V)): retire all but the y (<= V) youngest stages' loads
+template <int PPW, int V>
+__device__ __forceinline__ void vm_wait_stages(int y) {
+  if constexpr (V <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (y >= V) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * V) : "memory");
+      return;
+    }
+    vm_wait_stages<PPW, V - 1>(y);
+  }
+}
 #ifndef S2_QTW1
 #define S2_QTW1 1                         // query tiles per wave of the reduced one-limb scan
 #endif
@@ -527,12 +551,14 @@ template <int KS, int LIMBS, int QTW, int MODE>
 __device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict__ codes, long n_ref, long ld,
                                            const int8_t* __restrict__ lut, const int* __restrict__ mult, int nq,
                                            int k, long range, long ref_offset, uint64_t* __restrict__ parts,
-                                           const int* __restrict__ th_init, int part, int group) {
+                                           const int* __restrict__ th_init, int part, int group, int ntpol) {
   constexpr int ROWB = KS * 64;                        // staged row bytes
+  constexpr int S2_R = s2_rows(KS);
   constexpr int STAGE = S2_R * ROWB;
   constexpr int PPW = STAGE / 1024 / 8;                // glds pieces per wave per stage
-  constexpr int NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;  // ring depth within 96 KiB
+  constexpr int NST = s2_nst(KS);                      // ring depth
   static_assert(NST >= 2, "stage too large");
+  static_assert(PPW * (NST - 2) <= 63, "vmcnt range");
   static_assert(ROWB % 256 == 0 && PPW >= 1, "rows must be multiples of 256 B");
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + NST * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -573,9 +599,10 @@ __device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict
       long r = r0 + row;
       r = r < r_end ? r : r_end - 1;
       const int src_ch = ch ^ (row & 15);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(codes + r * ld + src_ch * 16),
-                                       (__attribute__((address_space(3))) void*)(smem + st * STAGE + piece * 1024),
-                                       16, 0, 0);
+      const auto* gsrc = (const __attribute__((address_space(1))) void*)(codes + r * ld + src_ch * 16);
+      auto* ldst = (__attribute__((address_space(3))) void*)(smem + st * STAGE + piece * 1024);
+      if (ntpol) __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 2);   // streamed once: nt policy
+      else __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
     }
   };
 
@@ -599,8 +626,7 @@ __device__ __forceinline__ void scan2_body(char* smem, const uint8_t* __restrict
     if (j < nstage) issue(j, r_begin + (long)j * S2_R);
   for (int it = 0; it < nstage; ++it) {
     // retire stage it; up to NST-2 younger stages stay in flight across the barrier
-    if (NST == 3 && it + 1 < nstage) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait_stages<PPW, NST - 2>(nstage - 1 - it);
     __builtin_amdgcn_s_barrier();
     if (MODE != 2 && it + NST - 1 < nstage) issue((it + NST - 1) % NST, r_begin + (long)(it + NST - 1) * S2_R);
     if (!active || MODE == 1) continue;
@@ -713,7 +739,7 @@ __global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ 
                                                     const int8_t* __restrict__ lut, int nq, int k, long range,
                                                     long ref_offset, uint64_t* __restrict__ parts,
                                                     const int* __restrict__ th_init, const int* __restrict__ wide,
-                                                    int n_parts, int n_groups) {
+                                                    int n_parts, int n_groups, int nt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // XCD co-scheduling: the G query groups of one panel range get consecutive dispatch
   // slots 8 apart (same XCD, same round), so the range streams from HBM once and the
@@ -727,21 +753,22 @@ __global__ __launch_bounds__(512) void scan2_kernel(const uint8_t* __restrict__ 
       const int8_t* lut1 = lut + nqt * 2 * KS * 1024;
       const int* mult = reinterpret_cast<const int*>(lut1 + nqt * KS * 1024);
       scan2_body<KS, 1, S2_QTW1, MODE>(smem, codes, n_ref, ld, lut1, mult, nq, k, range, ref_offset, parts, th_init,
-                                       part, group);
+                                       part, group, nt);
       return;
     }
   }
   scan2_body<KS, LIMBS, 1, MODE>(smem, codes, n_ref, ld, lut, nullptr, nq, k, range, ref_offset, parts, th_init,
-                                 part, group);
+                                 part, group, nt);
 }
 
 template <int KS, int LB>
 static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* codes, long n_ref, long ld,
                          const int8_t* lut, int k, long range, long off, uint64_t* parts, const int* th,
                          const int* wide) {
-  constexpr size_t STAGE = (size_t)S2_R * KS * 64;
-  constexpr size_t NST = (98304 / STAGE) < 3 ? (98304 / STAGE) : 3;
-  const size_t lds = NST * STAGE + 8 * 16 * S2_CAP * sizeof(uint64_t);
+  constexpr size_t STAGE = (size_t)s2_rows(KS) * KS * 64;
+  constexpr size_t NST = s2_nst(KS);
+  const size_t lds = NST * STAGE + S2_CAND;
+  static_assert(NST * STAGE + S2_CAND <= S2_LDS, "LDS budget");
   auto kern = scan2_kernel<KS, LB, 0>;
   if constexpr (KS == 16 && LB == 2) {
     const char* m = getenv("SNVRAG_SCAN_MODE");
@@ -751,8 +778,12 @@ static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* code
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int G = ((nq + 15) / 16 + 7) / 8;
   const long nwg = (long)((n_parts + 7) / 8) * 8 * G;
+  // one query group: every code byte is read by exactly one workgroup, so stream it with
+  // the non-temporal policy; with G > 1 the other groups read the range from L2 (default)
+  const char* pol = getenv("SNVRAG_SCAN_NT");
+  const int nt = pol ? (pol[0] == '1') : (G == 1);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th,
-                     wide, n_parts, G);
+                     wide, n_parts, G, nt);
 }
 
 static int scan_parts(long n_ref) {
