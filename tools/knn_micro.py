@@ -28,7 +28,7 @@ def timeit(fn, reps=10):
 
 def main():
     n_ref = int(os.environ.get("KM_N", 1 << 20))
-    S, nq, L = 1024, 128, 1030
+    S, nq, L = 1024, int(os.environ.get("KM_NQ", 128)), 1030
     dev = "cuda"
     rng = np.random.default_rng(0)
     af = torch.from_numpy(rng.beta(0.3, 3.0, S).astype(np.float32)).to(dev)
@@ -43,6 +43,15 @@ def main():
     smask = torch.from_numpy(mask).to(dev)
     lut, exps, consts = index.lut(tok, W, smask, 2)
     byts = n_ref * index.n_sites_pad
+    if os.environ.get("KM_QUICK"):   # full scan vs its loads-only / compute-only halves
+        for mode, name in (("0", "full"), ("1", "loads only"), ("2", "compute only")):
+            os.environ["SNVRAG_SCAN_MODE"] = mode
+            ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 32, 0))
+            ms2 = timeit(lambda: index.scan_keys(lut, nq, 2, 32, presample=True))
+            print(f"nq={nq} scan v2 k=32 {name}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s; "
+                  f"with threshold pre-pass (bench path): {ms2:7.3f} ms", flush=True)
+        os.environ.pop("SNVRAG_SCAN_MODE", None)
+        return
     for ver in ("v2", "v1"):
         if ver == "v1":
             os.environ["SNVRAG_SCAN_V1"] = "1"
