@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--heads", type=int, default=12)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--level", type=int, default=4, help="curriculum mask level (4 -> 50%%, rare 70%%)")
+    p.add_argument("--f32-leg", type=int, default=2,
+                   help="steps of the same batch on the exact-f32 path (bf16-vs-f32 call agreement); 0 = skip")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on host cores (rank 0)")
     p.add_argument("--cpu-panel", type=int, default=65536, help="panel sample for the CPU kNN timing")
     p.add_argument("--train-steps", type=int, default=3,
@@ -86,17 +88,64 @@ def make_queries(args, af_np, seed, rank):
     return alle, src
 
 
+def build_workload(args, dev, vocab, rank=0, seed=1234):
+    """configs[2] workload: one window of ``args.window`` sites, an ``args.n_ref``-haplotype panel
+    generated on the device (HBM-resident), ``args.batch`` query samples copied from panel rows with
+    2 % flips, AF-guided masks at ``args.level``.  Shared by the bench and the launch-shape kNN
+    parity test (tests/test_gpu_knn_scale.py)."""
+    from types import SimpleNamespace
+    from src.dataset import utils as U
+    from src.retrieval import PanelIndex
+    S, B, L = args.window, args.batch, 1030
+    rng = np.random.default_rng(seed)
+    af_np = rng.beta(0.3, 3.0, S).astype(np.float32)
+    pos = np.sort(rng.choice(np.arange(1, 50 * S), S, replace=False))
+    af_dev = torch.from_numpy(af_np).to(dev)
+    ref_af = U.sequence_padding(af_np, "float").astype(np.float32)
+    index = PanelIndex.synthetic(args.n_ref, S, af_dev, torch.from_numpy(ref_af).to(dev), seed)
+    raw_mask = U.af_guided_mask(af_np, args.level, 0, 0)
+    mask = U.sequence_padding(raw_mask, "int")
+    alle, src = make_queries(args, af_np, seed, rank)
+    pad = lambda a: torch.from_numpy(np.stack([U.sequence_padding(r, "float") for r in a]).astype(np.float32)).to(dev)
+    afp = np.clip(af_np[None] + 0.05 * rng.standard_normal((B, S)), 0, 1)
+    x = dict(hap_1=torch.from_numpy(vocab.tokenize(alle[:, 0], mask)).to(dev),
+             hap_2=torch.from_numpy(vocab.tokenize(alle[:, 1], mask)).to(dev),
+             af=pad(np.broadcast_to(af_np, (B, S))), af_p=pad(afp),
+             pos=pad(np.broadcast_to(U.position_normalize(pos), (B, S))),
+             ref=pad((1 - afp) ** 2), het=pad(2 * afp * (1 - afp)), hom=pad(afp ** 2))
+    site_mask = torch.from_numpy(raw_mask.astype(np.uint8)).to(dev)
+    tok = torch.cat([x["hap_1"], x["hap_2"]]).contiguous()
+    return SimpleNamespace(index=index, x=x, site_mask=site_mask, tok=tok, raw_mask=raw_mask, af_np=af_np,
+                           ref_af=ref_af, alle=alle, src=src, S=S, B=B, L=L,
+                           masked_per_step=2 * B * int(raw_mask.sum()))
+
+
+def make_step(wl, eng, k):
+    """One step: exact kNN over the panel -> neighbour K-mean written straight into the
+    encoder's input block -> full eval forward (engine dtype)."""
+    from src import kernels as K
+    P = eng.packed()
+    Ar = eng.af_embedding(torch.from_numpy(wl.ref_af).to(wl.tok.device)[None]).float()[0].contiguous()
+    B, L, D = wl.B, wl.L, P.D
+
+    def step():
+        idx, _ = wl.index.search(wl.tok, P.W, wl.site_mask, k)
+        block = torch.empty(4 * B, L, D, device=wl.tok.device, dtype=eng.dtype)
+        K.rag_mean(idx, wl.index.codes, wl.S, P.W, P.pe, Ar, L, eng.dtype, out=block[2 * B:])
+        wl.x["rag_block"] = block
+        return eng.forward(wl.x)
+    return step
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
-    from src import kernels as K, native as N
+    from src import native as N
     from src.dataset import synthetic
-    from src.dataset import utils as U
     from src.dataset.vocab import WordVocab
     from src.engine import engine_for
     from src.model import build_model
-    from src.retrieval import PanelIndex
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     vocab = WordVocab(synthetic.POPS)
@@ -107,35 +156,14 @@ def main():
     P = eng.packed()
 
     # ---- window, panel (HBM-resident, generated on device), queries ----
-    S, B, L = args.window, args.batch, 1030
-    seed = 1234
-    rng = np.random.default_rng(seed)
-    af_np = rng.beta(0.3, 3.0, S).astype(np.float32)
-    pos = np.sort(rng.choice(np.arange(1, 50 * S), S, replace=False))
-    af_dev = torch.from_numpy(af_np).to(dev)
-    ref_af = U.sequence_padding(af_np, "float").astype(np.float32)
-    index = PanelIndex.synthetic(args.n_ref, S, af_dev, torch.from_numpy(ref_af).to(dev), seed)
-    raw_mask = U.af_guided_mask(af_np, args.level, 0, 0)
-    mask = U.sequence_padding(raw_mask, "int")
-    alle, _ = make_queries(args, af_np, seed, rank)
-    pad = lambda a: torch.from_numpy(np.stack([U.sequence_padding(r, "float") for r in a]).astype(np.float32)).to(dev)
-    afp = np.clip(af_np[None] + 0.05 * rng.standard_normal((B, S)), 0, 1)
-    x = dict(hap_1=torch.from_numpy(vocab.tokenize(alle[:, 0], mask)).to(dev),
-             hap_2=torch.from_numpy(vocab.tokenize(alle[:, 1], mask)).to(dev),
-             af=pad(np.broadcast_to(af_np, (B, S))), af_p=pad(afp),
-             pos=pad(np.broadcast_to(U.position_normalize(pos), (B, S))),
-             ref=pad((1 - afp) ** 2), het=pad(2 * afp * (1 - afp)), hom=pad(afp ** 2))
-    site_mask = torch.from_numpy(raw_mask.astype(np.uint8)).to(dev)
-    tok = torch.cat([x["hap_1"], x["hap_2"]]).contiguous()
-    Ar = eng.af_embedding(torch.from_numpy(ref_af).to(dev)[None]).float()[0].contiguous()
-    masked_per_step = 2 * B * int(raw_mask.sum())
+    wl = build_workload(args, dev, vocab, rank)
+    S, B, L = wl.S, wl.B, wl.L
+    index, x, tok, site_mask = wl.index, wl.x, wl.tok, wl.site_mask
+    af_np, ref_af, raw_mask = wl.af_np, wl.ref_af, wl.raw_mask
+    masked_per_step = wl.masked_per_step
     index_sites_pad = index.n_sites_pad
     k = args.k
-
-    def step():
-        idx, _ = index.search(tok, P.W, site_mask, k)
-        x["rag_mean"] = K.rag_mean(idx, index.codes, S, P.W, P.pe, Ar, L, dtype)
-        return eng.forward(x)
+    step = make_step(wl, eng, k)
 
     for _ in range(args.warmup):
         step()
@@ -188,6 +216,9 @@ def main():
         probes.append(pr)
     probe = dict(probes[-1], per_queries=[{kq: p[kq] for kq in ("queries", "avg_launch_ms", "achieved_gbs", "frac")}
                                           for p in probes])
+    # precision leg: the same batch through the exact-f32 path, whose logits
+    # carry the 1e-3 parity bar; report how often the bf16 run's imputed calls agree with it
+    precision = precision_leg(args, wl, eng, k, out) if (args.f32_leg and dtype == torch.bfloat16) else None
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev)
@@ -241,6 +272,7 @@ def main():
                                   "above ~150 queries the scan is int8-MFMA/LDS bound, see knn_hbm_probe"),
             "knn_hbm_probe": dict(probe, bound="hbm", peak=HBM_PEAK_GBS),
             "knn_search_ms": round(knn_ms, 4),
+            "knn_search_queries_per_s": round(2 * B / (knn_ms * 1e-3), 1),
             "gemm": dict(achieved_tflops=round(gemm["rate"] / 1e12, 2), frac=round(gemm["rate"] / 1e12 / peak_f, 4),
                          ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
             "ffn_fused": (dict(achieved_tflops=round(ffn["rate"] / 1e12, 2), frac=round(ffn["rate"] / 1e12 / peak_f, 4),
@@ -263,9 +295,49 @@ def main():
         "config": {"workload": "configs[2]: v18 embedding-RAG imputation, window=1024 sites (L=1030 tokens), "
                                f"k={k}, {args.n_ref}-haplotype panel resident in HBM, d{args.dims}/L{args.layers}/H{args.heads}",
                    "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (panel replicated)"},
-        "roofline": roofline, "cpu_baseline": cpu, **extra, "train": train,
+        "roofline": roofline, "cpu_baseline": cpu, **extra, "precision_parity": precision, "train": train,
     }
     print(json.dumps(line))
+
+
+def call_agreement(o_lo, o_hi, raw_mask):
+    """Imputed-call agreement of two forwards over the masked sites (token l = site + 1):
+    haplotype calls p(alt) > 0.5 (infer_embedding_rag.py:145-152: softmax is monotone, so the
+    reference's second softmax does not move the threshold) and the genotype argmax."""
+    sites = torch.from_numpy(np.nonzero(raw_mask)[0] + 1).to(o_lo["probs_h1"].device)
+    hp = lambda o: torch.stack([o["probs_h1"][:, sites, 1], o["probs_h2"][:, sites, 1]]).float()
+    a, b = hp(o_lo), hp(o_hi)
+    ga, gb = o_lo["gt"][:, sites].argmax(-1), o_hi["gt"][:, sites].argmax(-1)
+    margin = (b - 0.5).abs()
+    conf = margin > 2e-2                     # f32 call clear of the bf16 probability tolerance
+    return dict(masked_haplotype_calls=int(a.numel()),
+                hap_call_agreement=round(float(((a > 0.5) == (b > 0.5)).float().mean()), 6),
+                hap_call_agreement_confident=round(float(((a > 0.5) == (b > 0.5))[conf].float().mean()), 6)
+                if bool(conf.any()) else None,
+                confident_fraction=round(float(conf.float().mean()), 4),
+                gt_argmax_agreement=round(float((ga == gb).float().mean()), 6),
+                max_abs_prob_diff=round(float((a - b).abs().max()), 5),
+                mean_abs_prob_diff=round(float((a - b).abs().mean()), 6))
+
+
+def precision_leg(args, wl, eng, k, out_bf16):
+    """Same batch, same neighbours on the exact-f32 engine (f32 MFMA, the 1e-3 logit-parity path):
+    its throughput and the bf16 run's call agreement with it."""
+    keep = {kk: out_bf16[kk].clone() for kk in ("probs_h1", "probs_h2", "gt")}
+    eng.set_dtype(torch.float32)
+    step32 = make_step(wl, eng, k)
+    out32 = step32()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.f32_leg):
+        out32 = step32()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.f32_leg
+    res = dict(call_agreement(keep, out32, wl.raw_mask), f32_ms_per_step=round(el * 1e3, 2),
+               f32_masked_snvs_per_s=round(wl.masked_per_step / el, 1), f32_steps=args.f32_leg)
+    eng.set_dtype(torch.bfloat16)
+    wl.x.pop("rag_block", None)
+    return res
 
 
 def train_bench(args, world, rank, dev):

@@ -178,16 +178,17 @@ def gt_head(p1, p2, ref, het, hom, sd, p="gt_classifier"):
 
 def forward(x: Dict[str, np.ndarray], sd: Dict[str, np.ndarray], layers: int, heads: int):
     """BERTFoundationModel.forward (eval).  ``x['rag_mean_h*']`` is the K-mean of the
-    retrieved neighbour embeddings ([B, L, D]); returns a dict of outputs."""
+    retrieved neighbour embeddings ([B, L, D]; absent = the no-RAG path); returns a dict."""
     af, af_p = x["af"].astype(F32), x["af_p"].astype(F32)
     e1, e2 = embed(x["hap_1"], af, sd), embed(x["hap_2"], af, sd)
     pf = pos_feat(x["pos"], sd)
     h1 = emb_fusion(e1, pf, af, sd)
     h2 = emb_fusion(e2, pf, af, sd)
-    r1 = emb_fusion(x["rag_mean_h1"].astype(F32), pf, af, sd)
-    r2 = emb_fusion(x["rag_mean_h2"].astype(F32), pf, af, sd)
-    h1 = rag_fusion(h1, r1, af, af_p, sd)
-    h2 = rag_fusion(h2, r2, af, af_p, sd)
+    if "rag_mean_h1" in x:                  # bert.py:171-206; without neighbours :207-210
+        r1 = emb_fusion(x["rag_mean_h1"].astype(F32), pf, af, sd)
+        r2 = emb_fusion(x["rag_mean_h2"].astype(F32), pf, af, sd)
+        h1 = rag_fusion(h1, r1, af, af_p, sd)
+        h2 = rag_fusion(h2, r2, af, af_p, sd)
     for i in range(layers):
         h1 = block(h1, sd, f"bert.transformer_blocks.{i}", heads)
     for i in range(layers):

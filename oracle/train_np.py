@@ -8,6 +8,8 @@ INFRASTRUCTURE ONLY (imported by tests/ and never by the product path).
                clip_grad_norm_(max_norm) (:239-241): L2 weight decay in the gradient,
                bias-corrected moments.
   lr_schedule  ScheduledOptim._get_lr_scale (optim_schedule.py:33-38).
+  confusion    cal_pr (optim_schedule.py:167-203): per-class TP/FP/FN of argmax predictions
+               over the masked rows.
 """
 
 from __future__ import annotations
@@ -53,3 +55,17 @@ def lr_schedule(step: int, warmup: int, init_lr: float, max_lr: float) -> float:
     if step <= warmup:
         return (max_lr - init_lr) / warmup * step + init_lr
     return max_lr * (warmup ** 0.5) * (step ** -0.5)
+
+
+def confusion(probs: np.ndarray, labels: np.ndarray, mask: np.ndarray, num_classes: int) -> np.ndarray:
+    """int64 [3, C] = (tp, fp, fn) per class over rows with mask (argmax: first maximum)."""
+    p = np.asarray(probs).reshape(-1, num_classes).argmax(-1)
+    y = np.asarray(labels).reshape(-1)
+    m = np.asarray(mask).reshape(-1).astype(bool)
+    p, y = p[m], y[m]
+    out = np.zeros((3, num_classes), np.int64)
+    for c in range(num_classes):
+        out[0, c] = ((p == c) & (y == c)).sum()
+        out[1, c] = ((p == c) & (y != c)).sum()
+        out[2, c] = ((p != c) & (y == c)).sum()
+    return out

@@ -172,7 +172,9 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     groups = defaultdict(list)
     for i, w in enumerate(batch["window_idx"]):
         groups[int(w)].append(i)
-    rag_mean = None if train else torch.empty(2 * B, L, D, device=dev, dtype=eng.dtype)
+    # eval: the neighbour means land directly in rows [2B:] of the encoder's input block
+    block = None if train else eng.input_block(B, L, dev)
+    rag_mean = None if train else block[2 * B:]
     rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
     rag_groups = []
     for w, rows in groups.items():
@@ -199,9 +201,12 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
             # the model re-encodes the neighbours WITH grad (train_forward.neighbour_means)
             rag_groups.append((rows_t, idx[:nb], idx[nb:], index))
         else:
-            means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
-            rag_mean[rows_t] = means[:nb]
-            rag_mean[rows_t + B] = means[nb:]
+            if nb == B and rows == list(range(B)):      # one window, batch order: no scatter
+                K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, out=rag_mean)
+            else:
+                means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
+                rag_mean[rows_t] = means[:nb]
+                rag_mean[rows_t + B] = means[nb:]
         rag_idx[rows_t] = idx[:nb]
         rag_idx[rows_t + B] = idx[nb:]
     batch["rag_idx_h1"], batch["rag_idx_h2"] = rag_idx[:B], rag_idx[B:]
@@ -214,6 +219,7 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     batch["rag_emb_h1"] = rag_mean[:B].unsqueeze(1)
     batch["rag_emb_h2"] = rag_mean[B:].unsqueeze(1)
     batch["rag_mean"] = rag_mean
+    batch["rag_block"] = block
     return batch
 
 

@@ -61,26 +61,44 @@ class WindowMajorSampler(Sampler):
 
 
 class DistributedWindowSampler(Sampler):
-    """Rank-aware window-major order: every rank visits windows in the same order and
-    takes a contiguous share of each window's samples, so the per-window panel index
-    (and its kNN shard) is the same on all ranks at the same time."""
+    """Rank-aware WindowGroupedSampler (sampler.py:87-135 semantics across ranks).
 
-    def __init__(self, dataset, rank: int, world: int, window_order=None):
-        self.rank, self.world = rank, world
+    Every rank draws the same per-epoch permutation (private ``random.Random(seed + epoch)``,
+    identical on all ranks): the window order is shuffled, then each window's samples; a
+    window's list is padded by wrapping to a multiple of ``world`` (as torch's
+    DistributedSampler pads) and rank r takes positions r, r + world, ...  So all ranks visit
+    the windows in lock-step (one panel index per window live at a time), every rank yields
+    exactly ``ceil(samples_per_window / world)`` items per window — equal batch counts, so
+    the bucketed gradient all-reduce never waits on a rank that ran out — and the union
+    over ranks covers every sample of every window."""
+
+    def __init__(self, dataset, rank: int, world: int, shuffle: bool = True, seed: int = 42, window_order=None):
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
+        self.rank, self.world, self.shuffle, self.seed, self.epoch = rank, world, shuffle, seed, 0
         self.num_windows = dataset.window_count
         self.num_samples = len(dataset) // self.num_windows
-        self.order = list(window_order) if window_order is not None else list(range(self.num_windows))
+        if self.num_samples == 0:
+            raise ValueError("dataset has fewer items than windows")
+        self.order = list(window_order) if window_order is not None else None
+        self.per_rank = (self.num_samples + world - 1) // world
 
-    def _share(self):
-        per = (self.num_samples + self.world - 1) // self.world
-        lo = min(self.num_samples, self.rank * per)
-        return range(lo, min(self.num_samples, lo + per))
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
 
     def __iter__(self):
-        share = self._share()
-        for w in self.order:
-            for s in share:
+        rng = random.Random(self.seed + self.epoch)
+        windows = list(self.order) if self.order is not None else list(range(self.num_windows))
+        if self.shuffle and self.order is None:
+            rng.shuffle(windows)
+        total = self.per_rank * self.world
+        for w in windows:
+            samples = list(range(self.num_samples))
+            if self.shuffle:
+                rng.shuffle(samples)
+            samples = (samples * ((total + len(samples) - 1) // len(samples)))[:total]
+            for s in samples[self.rank::self.world]:
                 yield s * self.num_windows + w
 
     def __len__(self):
-        return len(self._share()) * self.num_windows
+        return self.per_rank * self.num_windows

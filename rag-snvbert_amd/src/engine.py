@@ -241,8 +241,17 @@ class Engine:
         return (h1.long().contiguous(), h2.long().contiguous(), g("af"), g("af_p") if "af_p" in x else g("af"),
                 g("pos"))
 
+    def input_block(self, B: int, L: int, device) -> torch.Tensor:
+        """A fresh [4B, L, D] encoder input block: rows [2B:] are where a caller writes the
+        neighbour K-means (``K.rag_mean(..., out=block[2 * B:])``) before passing
+        ``x["rag_block"] = block`` to the forward, which then embeds the queries into rows [:2B]
+        without copying the 2B*L*D neighbour rows again."""
+        return torch.empty(4 * B, L, self.packed(allow_train=True).D, device=device, dtype=self.dtype)
+
     def rag_means(self, x: Dict[str, torch.Tensor], B: int, L: int, D: int) -> Optional[torch.Tensor]:
         """[2B, L, D] K-means of retrieved neighbours in compute dtype (bert.py:171-183)."""
+        if "rag_block" in x:
+            return x["rag_block"][2 * B:]
         if "rag_mean" in x:
             return x["rag_mean"].to(self.dtype).contiguous()
         if "rag_emb_h1" not in x:
@@ -263,9 +272,15 @@ class Engine:
         afemb = self.af_embedding(af)                                 # [B, L, D]
         rag = self.rag_means(x, B, L, D)
         nblk = 4 if rag is not None else 2
-        hm = torch.empty(nblk * B, L, D, device=h1.device, dtype=T)
+        blk = x.get("rag_block")
+        if blk is not None:
+            if blk.dtype != T or tuple(blk.shape) != (4 * B, L, D) or not blk.is_contiguous():
+                raise ValueError(f"rag_block must be a contiguous {T} [4B, L, D] block (Engine.input_block)")
+            hm = blk                                                  # rag rows already in place
+        else:
+            hm = torch.empty(nblk * B, L, D, device=h1.device, dtype=T)
         K.embed_tokens(torch.cat([h1, h2], 0), P.W, P.pe, afemb, B, T, out=hm[:2 * B])
-        if rag is not None:
+        if rag is not None and blk is None:
             hm[2 * B:].copy_(rag)
         pf = K.posfeat(pos, P.pf)                                     # [B, L]
         ef = P.ef

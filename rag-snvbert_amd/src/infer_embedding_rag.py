@@ -77,22 +77,38 @@ def geometry(h1, h2, gt, mask, n_windows: int, n_variants: int, window_len: int)
     return padf(h1), padf(h2), padf(gt), padf(mask)
 
 
-def write_vcf(path, chrom, pos, h1, h2, gt, samples, ref=None, alt=None):
-    """Minimal VCF 4.2: GT (phased, p > 0.5), DS = p1 + p2, GP = (p00, p01+p10, p11)."""
+GT_MAP = ("0|0", "0|1", "1|0", "1|1")       # src/dataset/utils.py:15-20
+
+
+def vcf_cells(h1, h2, gt):
+    """Per-sample FORMAT cells GT:HDS:GP:DS of one site, as generate_vcf_efficient_optimized
+    writes them (src/dataset/utils.py:406-461): GT = GT_MAP[argmax gt], HDS = (p1, p2),
+    GP = (p00, p01 + p10, p11), DS = GP1 + 2 GP2, all '%.3f'."""
+    g = np.argmax(gt, -1)
+    gp0, gp1, gp2 = gt[..., 0], gt[..., 1] + gt[..., 2], gt[..., 3]
+    ds = gp1 + 2 * gp2
+    return [f"{GT_MAP[g[s]]}:{h1[s]:.3f},{h2[s]:.3f}:{gp0[s]:.3f},{gp1[s]:.3f},{gp2[s]:.3f}:{ds[s]:.3f}"
+            for s in range(len(h1))]
+
+
+def write_vcf(path, chrom, pos, h1, h2, gt, samples, pos_flag=None, ref=None, alt=None):
+    """VCF 4.2 records of the imputed sites (utils.py:378-479 layout: FORMAT GT:HDS:GP:DS,
+    ID '.', REF/ALT '.' unless given, QUAL 0, FILTER PASS).  ``pos_flag`` selects the sites
+    written (the reference writes only flagged = imputed positions, infer_embedding_rag.py:237)."""
     with open(path, "w") as f:
         f.write("##fileformat=VCFv4.2\n##source=rag-snvbert_amd\n")
-        f.write('##FORMAT=<ID=GT,Number=1,Type=String,Description="Phased genotype">\n')
-        f.write('##FORMAT=<ID=DS,Number=1,Type=Float,Description="ALT dosage">\n')
+        f.write('##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype (argmax of GP)">\n')
+        f.write('##FORMAT=<ID=HDS,Number=2,Type=Float,Description="Haplotype ALT dosages">\n')
         f.write('##FORMAT=<ID=GP,Number=3,Type=Float,Description="Genotype probabilities">\n')
+        f.write('##FORMAT=<ID=DS,Number=1,Type=Float,Description="ALT dosage">\n')
         f.write("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples) + "\n")
-        a1, a2 = (h1 > 0.5).astype(int), (h2 > 0.5).astype(int)
-        ds = h1 + h2
         for i in range(len(pos)):
-            cells = [f"{a1[i, s]}|{a2[i, s]}:{ds[i, s]:.3f}:{gt[i, s, 0]:.3f},{gt[i, s, 1] + gt[i, s, 2]:.3f},"
-                     f"{gt[i, s, 3]:.3f}" for s in range(h1.shape[1])]
-            r = ref[i] if ref is not None else "N"
+            if pos_flag is not None and not pos_flag[i]:
+                continue
+            r = ref[i] if ref is not None else "."
             a = alt[i] if alt is not None else "."
-            f.write(f"{chrom}\t{int(pos[i])}\t.\t{r}\t{a}\t.\tPASS\t.\tGT:DS:GP\t" + "\t".join(cells) + "\n")
+            f.write(f"{chrom}\t{int(pos[i])}\t.\t{r}\t{a}\t0.0\tPASS\t.\tGT:HDS:GP:DS\t" +
+                    "\t".join(vcf_cells(h1[i], h2[i], gt[i])) + "\n")
 
 
 def build_dataset(args):
@@ -130,7 +146,9 @@ def infer(argv=None):
         ck = torch.load(args.check_point, map_location="cpu", weights_only=True)
         sd = ck.get("model", ck) if isinstance(ck, dict) else ck
         sd = {k.replace("module.", ""): v for k, v in sd.items()}
-        model.load_state_dict(sd, strict=False)
+        # strict: a missing or renamed key must not silently impute with random-init weights
+        # (the reference loads with strict=False, infer_embedding_rag.py:99)
+        model.load_state_dict(sd, strict=True)
     model = model.to(dev).eval()
     engine_for(model).set_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     emb = model.bert.embedding

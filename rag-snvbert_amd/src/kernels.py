@@ -321,10 +321,15 @@ def knn_decode(keys: torch.Tensor, exps: Optional[torch.Tensor] = None, consts: 
 
 
 def rag_mean(idx: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor, pe: torch.Tensor,
-             Ar: Optional[torch.Tensor], L: int, dtype: torch.dtype, tok0=5, tok1=6, sos=2, eos=3, pad=0):
+             Ar: Optional[torch.Tensor], L: int, dtype: torch.dtype, tok0=5, tok1=6, sos=2, eos=3, pad=0,
+             out: Optional[torch.Tensor] = None):
+    """[nq, L, D] mean over the k neighbours of their complete-token embeddings; ``out`` (e.g. the
+    rag half of the encoder's input block) is written in place."""
     nq, k = idx.shape
     D = W.shape[1]
-    out = torch.empty(nq, L, D, device=idx.device, dtype=dtype)
+    if out is None:
+        out = torch.empty(nq, L, D, device=idx.device, dtype=dtype)
+    assert out.dtype == dtype and tuple(out.shape) == (nq, L, D) and out.is_contiguous()
     check(N.lib().snvrag_rag_mean(_dt(dtype), nq, L, D, k, ptr(_c(idx)), ptr(_c(codes)), codes.shape[1], n_sites,
                                   ptr(_c(W)), ptr(_c(pe)), ptr(Ar), tok0, tok1, sos, eos, pad, ptr(out),
                                   stream_ptr()), "rag_mean")

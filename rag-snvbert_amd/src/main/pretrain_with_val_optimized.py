@@ -87,10 +87,12 @@ class BERTTrainerWithValidationOptimized:
         """One micro-batch: retrieval, forward, loss, backward (+ optimizer step on the last
         micro-batch of an accumulation group).  Returns the device loss (no sync)."""
         ds = self.rag_train_dataset
+        # train mode BEFORE retrieval (pretrain_with_val_optimized.py:127): after validate() the
+        # model is in eval mode, and retrieval in eval mode would return detached means
+        self.model.train()
         if ds is not None and hasattr(ds, "process_batch_retrieval"):
             data = ds.process_batch_retrieval(data, self.embedding_layer, self.device, k_retrieve=self.rag_k)
         data = self.to_device(data)
-        self.model.train()
         last = (self.accum_step + 1) % self.grad_accum_steps == 0
         self.ddp.enabled = last
         output = self.model(data)

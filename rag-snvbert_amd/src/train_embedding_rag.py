@@ -72,11 +72,12 @@ def build_data(args, rank: int, world: int):
     mk = lambda ds, sampler, bs: torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler,
                                                              num_workers=args.num_workers,
                                                              collate_fn=embedding_rag_collate_fn)
+    # train_embedding_rag.py:218, :260 — seed 42 for the train order, deterministic validation
     if world > 1:
-        ts = DistributedWindowSampler(train, rank, world)
-        vs = DistributedWindowSampler(val, rank, world)
+        ts = DistributedWindowSampler(train, rank, world, shuffle=True, seed=42)
+        vs = DistributedWindowSampler(val, rank, world, shuffle=False)
     else:
-        ts, vs = WindowGroupedSampler(train, shuffle=True, seed=args.seed), WindowGroupedSampler(val, shuffle=False)
+        ts, vs = WindowGroupedSampler(train, shuffle=True, seed=42), WindowGroupedSampler(val, shuffle=False)
     return mk(train, ts, args.train_batch_size), mk(val, vs, args.val_batch_size), vocab
 
 
@@ -125,6 +126,8 @@ def main(argv=None):
         trainer.val_data = _Cap(val_loader, args.max_steps)
     for epoch in range(start, args.epochs):
         ds = train_loader.dataset
+        if hasattr(train_loader.sampler, "set_epoch"):      # train_embedding_rag.py:349-351
+            train_loader.sampler.set_epoch(epoch)
         if epoch > 0 and hasattr(ds, "regenerate_masks"):
             ds.current_epoch = epoch
             ds.regenerate_masks(seed=epoch)

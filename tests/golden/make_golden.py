@@ -265,6 +265,31 @@ def run_case(name, d, layers, heads, B, n_sites, n_ref, k, level=4, seed=0, epoc
     print(f"{name}: digest={digest} ref-vs-canonical index sets equal per query: h1={same1.tolist()}")
 
 
+def run_norag_case(name, d, layers, heads, B, n_sites, n_ref=8, level=4, seed=0, epoch=2024, w=0):
+    """configs[0]: the same model with no retrieved embeddings in the batch (bert.py:207-210:
+    emb_fusion only, no rag_fusion)."""
+    torch.set_num_threads(8)
+    vocab = ref_vocab()
+    model, digest = build_model(d, layers, heads, len(vocab), seed)
+    win = synthetic.SynthWindow(n_sites, n_ref, B, seed=seed + 17)
+    x = make_inputs(win, vocab, level, epoch, w)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    logits = []
+    hook = model.hap_classifier.net.register_forward_hook(lambda m, i, o: logits.append(o.detach().clone()))
+    with torch.no_grad():
+        out = model({key: T(x[key]) for key in ("hap_1", "hap_2", "af", "af_p", "pos", "ref", "het", "hom")})
+    hook.remove()
+    res = dict(cfg=np.array(json.dumps(dict(d=d, layers=layers, heads=heads, vocab=len(vocab), B=B,
+                                              n_sites=n_sites, n_ref=n_ref, k=0, level=level, seed=seed,
+                                              epoch=epoch, w=w, sd_digest=digest))),
+               probs_h1=out[0].numpy(), probs_h2=out[1].numpy(), gt=out[2].numpy(),
+               logits_h1=logits[0].numpy(), logits_h2=logits[1].numpy())
+    for key in ("hap_1", "hap_2", "mask", "raw_mask", "af", "af_p", "pos", "ref", "het", "hom"):
+        res[key] = x[key]
+    np.savez_compressed(OUT / f"{name}.npz", **res)
+    print(f"{name}: digest={digest}")
+
+
 def _kth_margin(dist, k):
     s = np.sort(dist, 1)
     return (s[:, k] - s[:, k - 1]) if s.shape[1] > k else np.full(s.shape[0], np.inf)
@@ -304,7 +329,7 @@ def masks_fixture():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["data", "tiny", "small", "full"]
+    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag"]
     if "data" in which:
         masks_fixture()
     if "tiny" in which:
@@ -314,3 +339,5 @@ if __name__ == "__main__":
         run_case("fwd_small", d=128, layers=2, heads=4, B=3, n_sites=300, n_ref=96, k=8, seed=1)
     if "full" in which:
         run_case("fwd_full", d=384, layers=12, heads=12, B=2, n_sites=1020, n_ref=64, k=4, seed=2)
+    if "norag" in which:
+        run_norag_case("fwd_norag", d=128, layers=2, heads=4, B=3, n_sites=128, seed=4)

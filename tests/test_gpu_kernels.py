@@ -14,6 +14,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from oracle import knn_np  # noqa: E402
+from knn_helpers import decode_lut, lut_wide_flag, rand_case as _rand_case  # noqa: E402
 
 
 def K():
@@ -125,36 +126,6 @@ def test_attention(dt, nseq, L, H, dh):
 
 
 # ------------------------------------------------------------------------ kNN --
-def decode_lut(lut: torch.Tensor, nq: int, n_sites_pad: int, limbs: int) -> np.ndarray:
-    """Inverse of the fragment layout [qt][limb][ks][lane][16] -> int32 dq[q, s]."""
-    KS = n_sites_pad // 64
-    nqt = (nq + 15) // 16
-    b = lut.cpu().numpy().view(np.int8)[:nqt * limbs * KS * 1024]
-    b = b.reshape(nqt, limbs, KS, 4, 16, 16)                                   # [qt][limb][ks][g][li][j]
-    b = b.transpose(0, 4, 1, 2, 3, 5).reshape(nqt * 16, limbs, n_sites_pad).astype(np.int32)
-    dq = b[:, 0] * 128 + b[:, 1] if limbs == 2 else b[:, 0]
-    return dq[:nq]
-
-
-def _rand_case(n_ref, n_sites, nq, seed, tie_heavy=False):
-    rng = np.random.default_rng(seed)
-    W = rng.standard_normal((12, 64)).astype(np.float32)
-    af = rng.beta(0.3, 3.0, n_sites)
-    panel = (rng.random((n_ref, n_sites)) < af).astype(np.uint8)
-    if tie_heavy:
-        panel[: n_ref // 2] = panel[0]
-    q_alle = panel[rng.integers(0, n_ref, nq)] ^ (rng.random((nq, n_sites)) < 0.05)
-    site_mask = (rng.random(n_sites) < 0.4).astype(np.uint8)
-    L = 1030
-    tok = np.zeros((nq, L), np.int64)
-    tok[:, 0] = 2
-    tok[:, 1:1 + n_sites] = np.where(site_mask[None] == 1, 4, 5 + q_alle)
-    tok[:, 1 + n_sites] = 3
-    if not tie_heavy:   # a few query positions masked where the panel is not (misaligned masks)
-        tok[:, 1:1 + n_sites][:, rng.random(n_sites) < 0.05] = 4
-    return W, panel, site_mask, tok
-
-
 @pytest.mark.parametrize("n_ref,n_sites,nq,k,limbs,tie", [
     (5000, 300, 20, 8, 2, False), (4099, 1020, 48, 32, 2, True), (3000, 512, 64, 32, 1, True),
     (777, 1028, 70, 4, 2, False), (10, 200, 5, 32, 2, False), (33, 64, 17, 1, 1, True)])
@@ -182,9 +153,7 @@ def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
     if limbs == 2:
         # binary Delta (aligned masks) reduces to the one-limb scan; either way the keys
         # equal the forced two-limb scan's
-        nqt, KS = (nq + 15) // 16, idx_t.n_sites_pad // 64
-        wide = lut.cpu().numpy().view(np.int8)[nqt * 3 * KS * 1024 + nqt * 64:][:4].view(np.int32)[0]
-        assert wide == (0 if tie else 1)
+        assert lut_wide_flag(lut, nq, idx_t.n_sites_pad) == (0 if tie else 1)
         os.environ["SNVRAG_KNN_NO_REDUCE"] = "1"
         try:
             keys2 = idx_t.scan_keys(lut, nq, 2, k)

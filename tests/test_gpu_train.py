@@ -293,3 +293,58 @@ def test_trainer_steps_reduce_loss_with_retrieval():
     losses = [tr.train_step(dict(batch)).item() for _ in range(12)]
     assert all(np.isfinite(losses))
     assert losses[-1] < 0.8 * losses[0], losses
+
+
+@pytest.mark.parametrize("C", [2, 4])
+def test_device_confusion_vs_oracle_cal_pr(C):
+    """snvrag_confusion (DeviceConfusion) == cal_pr (optim_schedule.py:167-203) restated in the
+    oracle, accumulated over two batches, with and without the rare/common second mask."""
+    from src.main.optim_schedule import DeviceConfusion
+    rng = np.random.default_rng(C)
+    conf, conf2 = DeviceConfusion(C, DEV), DeviceConfusion(C, DEV)
+    exp, exp2 = np.zeros((3, C), np.int64), np.zeros((3, C), np.int64)
+    for b in range(2):
+        probs = rng.random((3, 1030, C)).astype(np.float32)
+        lab = rng.integers(0, C, (3, 1030))
+        m = rng.random((3, 1030)) < 0.4
+        m2 = rng.random((3, 1030)) < 0.5
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+        conf.update(T(probs), T(lab), T(m))
+        conf2.update(T(probs), T(lab), T(m), T(m2 & m))
+        exp += train_np.confusion(probs, lab, m, C)
+        exp2 += train_np.confusion(probs, lab, m & m2, C)
+    np.testing.assert_array_equal(conf.counts.cpu().numpy(), exp)
+    np.testing.assert_array_equal(conf2.counts.cpu().numpy(), exp2)
+
+
+def test_checkpoint_round_trip(tmp_path):
+    """trainer.save -> a fresh trainer.load restores weights, the bf16 mirror, Adam moments and
+    the LR-schedule step; the next training step then matches the uninterrupted run (up to the
+    order of the loss kernel's float atomics)."""
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.dataset.synthetic import make_rag_dataset
+    from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
+    from src.model import build_model
+    ds, vocab = make_rag_dataset(n_samples=4, n_sites=200, n_windows=1, n_ref_samples=16, seed=3, name="train")
+    batch = embedding_rag_collate_fn([ds[i] for i in range(4)])
+
+    def trainer(seed):
+        torch.manual_seed(seed)
+        m = build_model(len(vocab), 64, 2, 2, dropout=0.0).to(DEV)
+        t = BERTTrainerWithValidationOptimized(m, None, None, vocab, lr=1e-3, warmup_steps=5, log_freq=0)
+        t.rag_train_dataset, t.rag_k = ds, 2
+        return t
+    a = trainer(0)
+    for _ in range(2):
+        a.train_step(dict(batch))
+    path = a.save(1, str(tmp_path / "ck"))
+    b = trainer(1)                                      # different init
+    assert b.load(path) == 1
+    for (ka, va), (kb, vb) in zip(a.model.state_dict().items(), b.model.state_dict().items()):
+        assert ka == kb
+        torch.testing.assert_close(va, vb, rtol=0, atol=0)
+    assert b.optim_schedule.n_current_steps == a.optim_schedule.n_current_steps
+    la, lb = a.train_step(dict(batch)), b.train_step(dict(batch))
+    torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-5)
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-6)

@@ -36,9 +36,34 @@ def test_samplers_match_reference():
     s.set_epoch(1)
     np.testing.assert_array_equal(list(iter(s)), g["grouped_sampler_ep1"])
     np.testing.assert_array_equal(list(iter(WindowMajorSampler(DS()))), g["major_sampler"])
-    shards = [list(iter(DistributedWindowSampler(DS(), r, 2))) for r in range(2)]
-    assert sorted(shards[0] + shards[1]) == list(range(35))
+    shards = [list(iter(DistributedWindowSampler(DS(), r, 2, shuffle=False))) for r in range(2)]
+    assert sorted(set(shards[0] + shards[1])) == list(range(35))
     assert [i % 7 for i in shards[0][:3]] == [0, 0, 0]
+
+
+@pytest.mark.parametrize("n_samples,world", [(10, 4), (5, 4), (7, 3), (6, 2), (1, 3)])
+def test_distributed_window_sampler_equal_shares_shuffled_lockstep(n_samples, world):
+    """Uneven sample counts: every rank gets the same number of items (no rank runs out of
+    batches while the others wait in the gradient all-reduce), ranks walk the SAME shuffled
+    window order in lock-step, every sample is covered, and the order changes per epoch."""
+    from src.dataset.sampler import DistributedWindowSampler
+
+    class DS:
+        window_count = 5
+        def __len__(self): return 5 * n_samples
+    samplers = [DistributedWindowSampler(DS(), r, world, shuffle=True, seed=42) for r in range(world)]
+    streams = [list(iter(s)) for s in samplers]
+    per = -(-n_samples // world)
+    assert all(len(st) == per * 5 == len(s) for st, s in zip(streams, samplers))
+    wins = [[i % 5 for i in st] for st in streams]
+    assert all(w == wins[0] for w in wins)                                   # lock-step windows
+    assert wins[0] != sorted(wins[0]) or n_samples * world == 1
+    assert sorted(set(sum(streams, []))) == list(range(5 * n_samples))     # full coverage
+    for s in samplers:
+        s.set_epoch(1)
+    streams1 = [list(iter(s)) for s in samplers]
+    assert streams1 != streams
+    assert all([i % 5 for i in st] == [i % 5 for i in streams1[0]] for st in streams1)
 
 
 def test_golden_inputs_rebuilt_by_product_featurisation():

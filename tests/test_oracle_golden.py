@@ -31,6 +31,19 @@ def test_oracle_forward_matches_reference(case):
             np.testing.assert_allclose(o[key], g[pre + key], rtol=1e-4, atol=1e-5)
 
 
+def test_oracle_norag_forward_matches_reference():
+    """configs[0] path: no retrieved embeddings in the batch (bert.py:207-210)."""
+    g = load_golden("fwd_norag")
+    cfg = g["cfg"]
+    sd = golden_state_dict(cfg)
+    x = {k: g[k] for k in ("hap_1", "hap_2", "af", "af_p", "pos", "ref", "het", "hom")}
+    o = model_np.forward(x, sd, cfg["layers"], cfg["heads"])
+    for key in ("logits_h1", "logits_h2"):
+        np.testing.assert_allclose(o[key], g[key], rtol=1e-4, atol=1e-4)
+    for key in ("probs_h1", "probs_h2", "gt"):
+        np.testing.assert_allclose(o[key], g[key], rtol=1e-4, atol=1e-5)
+
+
 def test_oracle_intermediates_tiny():
     g = load_golden("fwd_tiny")
     sd = golden_state_dict(g["cfg"])
