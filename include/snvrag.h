@@ -281,6 +281,21 @@ int snvrag_block_tail_forward(int64_t M, int D, const void* att, void* x, const 
                               const float* b_o, const float* ln1_g, const float* ln1_b,
                               const void* ffn_stream, const float* ffn_vec, float eps, void* stream);
 
+/* Block tail on 32x32x16 MFMAs (csrc/tail.hip), bf16, eval — same math as
+ * snvrag_block_tail_forward: x1 = LN1(x + att W_o^T + b_o); x = LN2(x1 + FFN(x1)), in place
+ * on x.  128 token rows per workgroup (4 waves x 32 rows), activations in registers, the
+ * LDS a 9-slot ring of 16 KiB weight slabs.  ONE weight stream of snvrag_tail_pack_bytes(D)
+ * bytes packed by snvrag_tail_pack(D, w_o [D,D], w1 [4D,D], w2g [D,4D], out, stream)
+ * (w2g as for snvrag_ffn_pack); ffn_vec as for snvrag_ffn_forward.  att and x must not
+ * alias; pointers 16-byte aligned; D in {128, 256, 384}.
+ * snvrag_tail_ffn_forward: the FFN sublayer alone (out = LN2(x1 + FFN(x1))), same stream. */
+size_t snvrag_tail_pack_bytes(int D);
+int snvrag_tail_pack(int D, const void* w_o, const void* w1, const void* w2g, void* out, void* stream);
+int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, const void* wstream, const float* b_o,
+                        const float* ln1_g, const float* ln1_b, const float* ffn_vec, float eps, void* stream);
+int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
+                            const float* ffn_vec, float eps, void* stream);
+
 /* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
  * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either
  * act(.) (ln_g == NULL) or LN(act(.) + resid) * ln_g + ln_b (N == K, resid [M, ld_resid]).

@@ -59,12 +59,18 @@ __device__ __forceinline__ void ff_glds16_nt(const void* src, void* lds_wave_bas
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
 }
 
-template <int BPW> __device__ __forceinline__ void ff_wait(int younger) {
-  // wait until at most `younger` slabs (BPW LDS-DMA instructions each) of this wave are in flight
-  switch (younger) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BPW) : "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * BPW) : "memory"); break;
+// wait until at most `younger` (<= MAXY) slabs (BPW LDS-DMA instructions each) of this wave
+// are still in flight
+template <int BPW, int MAXY> __device__ __forceinline__ void ff_wait(int younger) {
+  static_assert(BPW * MAXY <= 63, "vmcnt range");
+  if constexpr (MAXY <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (younger >= MAXY) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BPW * MAXY) : "memory");
+      return;
+    }
+    ff_wait<BPW, MAXY - 1>(younger);
   }
 }
 
@@ -169,7 +175,7 @@ void ffn_kernel(int M, const bf16* __restrict__ x1, bf16* out, const char* __res
       }
     } else {
       if (DBG != 1) {
-        ff_wait<BPW>(min(PD - 1, NSLAB - 1 - i));
+        ff_wait<BPW, PD - 1>(min(PD - 1, NSLAB - 1 - i));
         __builtin_amdgcn_s_barrier();
       }
       issue(i + PD);
@@ -432,19 +438,20 @@ static bool ffn_d_ok(int D) { return D == 128 || D == 256 || D == 384; }
 // variant (SNVRAG_FFN_VARIANT): 0 = slab-wise ring (3 in flight), x1 in LDS; 1 = slab pairs, x1 in
 // LDS (default); 2 = 4-slab groups, x1 in VGPRs; 4 = 4 waves x 16 rows, two workgroups per CU
 static int ffn_variant() {
-  static const int v = getenv("SNVRAG_FFN_VARIANT") ? atoi(getenv("SNVRAG_FFN_VARIANT")) : 1;
-  return v;
+  const char* e = getenv("SNVRAG_FFN_VARIANT");
+  return e ? atoi(e) : 1;
 }
 
-template <int D, bool PRE, int NWV, int G, bool XREG, bool NTS, int SLOTS, int WPE>
+template <int D, bool PRE, int NWV, int G, bool XREG, bool NTS, int SLOTS, int WPE, int RT = 1>
 static int launch_ffn_k(int64_t M, const void* x1, void* out, const void* ws, const float* vec, float eps,
                         const FfnPre& pre, hipStream_t s) {
-  auto kern = ffn_kernel<D, 1, NWV, 0, PRE, true, G, XREG, NTS, SLOTS, WPE>;
+  auto kern = ffn_kernel<D, RT, NWV, 0, PRE, true, G, XREG, NTS, SLOTS, WPE>;
   constexpr int KS = D / 32;
-  const size_t lds = XREG ? (size_t)2 * G * FF_SLAB
-                          : (size_t)NWV * KS * 1024 + (size_t)(G == 1 ? SLOTS : 2 * G) * FF_SLAB;
+  const size_t ring = (size_t)(G == 1 ? SLOTS : 2 * G) * FF_SLAB;
+  const size_t lds = XREG ? ring : (size_t)NWV * RT * KS * 1024 + ring;
+  static_assert((XREG ? 0 : NWV * RT * KS * 1024) + (G == 1 ? SLOTS : 2 * G) * FF_SLAB <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, 16 * NWV)), dim3(64 * NWV), lds, s, (int)M, (const bf16*)x1,
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, 16 * NWV * RT)), dim3(64 * NWV), lds, s, (int)M, (const bf16*)x1,
                      (bf16*)out, (const char*)ws, vec, eps, pre);
   SNV_LAUNCH_CHECK();
   return 0;
@@ -459,6 +466,14 @@ static int launch_ffn_v(int64_t M, const void* x1, void* out, const void* ws, co
     // 64-row workgroups two per CU (+4 %: the weight stream is read twice as often)
     case 2: return launch_ffn_k<D, PRE, 8, 4, true, false, 4, 2>(M, x1, out, ws, vec, eps, pre, s);
     case 4: return launch_ffn_k<D, PRE, 4, 1, false, false, 2, 2>(M, x1, out, ws, vec, eps, pre, s);
+    // x1 in VGPRs, the whole LDS a slab-wise ring: 8 / 6 slabs (128 / 96 KiB) in flight
+    case 5: return launch_ffn_k<D, PRE, 8, 1, true, false, 9, 2>(M, x1, out, ws, vec, eps, pre, s);
+    case 6: return launch_ffn_k<D, PRE, 8, 1, true, false, 7, 2>(M, x1, out, ws, vec, eps, pre, s);
+    // one wave per SIMD, two 16-row tiles per wave (each A fragment read from LDS feeds two MFMAs)
+    case 7: return launch_ffn_k<D, PRE, 4, 1, false, false, 4, 1, 2>(M, x1, out, ws, vec, eps, pre, s);
+    case 8: return launch_ffn_k<D, PRE, 4, 2, false, false, 4, 1, 2>(M, x1, out, ws, vec, eps, pre, s);
+    // ... with x1 in VGPRs and a deep slab-wise ring
+    case 9: return launch_ffn_k<D, PRE, 4, 1, true, false, 9, 1, 2>(M, x1, out, ws, vec, eps, pre, s);
     default: return launch_ffn_k<D, PRE, 8, 2, false, false, 4, 2>(M, x1, out, ws, vec, eps, pre, s);
   }
 }

@@ -1,0 +1,536 @@
+// Transformer block tail as ONE kernel on 32x32x16 bf16 MFMAs (gfx950), eval:
+//
+//   x1  = LN1(x + att W_o^T + b_o)                     multi_head_attention.py:51, sublayer.py:15-16
+//   x   = LN2(x1 + lrelu(LN_f(lrelu(x1 W1^T + b1)) W2^T + b2))   feed_forward.py:18-21
+//
+// A workgroup owns 128 token rows: 4 waves (one per SIMD, up to 512 registers each) x 32
+// rows.  Every MFMA computes a TRANSPOSED 32x32 tile (32 weight rows x 32 tokens), so the
+// weight fragment (A operand, 1 KiB) read from LDS feeds 2 x 32 x 32 x 16 FLOP — twice the
+// work per LDS byte of a 16x16x32 tile — and each lane ends up holding one token's values.
+//
+// Operands:
+//   * activations (att, then x1) live in VGPRs as B fragments for the whole launch
+//     (96 registers at D = 384); the LDS is ONE ring of 16 KiB weight slabs streamed
+//     once per workgroup by LDS-DMA, 7 slabs (112 KiB) in flight, one barrier per slab
+//     placed PF fragments before the slab boundary so LDS reads run ahead across it;
+//   * the 4D hidden of a 64-unit chunk stays in registers: phase-1 accumulators are
+//     packed straight into phase-2 B fragments (k order baked into W2');
+//   * the FFN LayerNorm is folded: W2' = W2 diag(g_f), c1 = rowsum W2',
+//     b2' = b2 + W2 b_f, LN_f(h) W2^T + b2 = rstd (h W2'^T) - rstd mean c1 + b2'.
+// Lane (token n = lane % 32, half hh = lane / 32) holds output features 32T + 16hh + i
+// (i < 16) of tile T: weight ROWS are permuted at pack time (tail_out_feat), the input
+// feature order of every B fragment (tail_in_feat) is shared by W_o', W1 and the
+// activation loads, so the LN epilogues, the x1 hand-over and the 32-B stores need no
+// lane exchange except one xor-32 shuffle per row reduction.
+#include "common.h"
+
+#include <utility>
+
+namespace snvrag {
+
+constexpr int TL_FRAG = 1024;               // one A fragment: 32 rows x 16 k bf16
+constexpr int TL_SLAB = 16 * TL_FRAG;
+constexpr int TL_NSLOT = 9;                 // ring slots (144 KiB)
+constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead
+constexpr int TL_ROWS = 128;
+constexpr int TL_VEC_LDS = 11 * 1024;       // b1 [4D] + g1, be1, b_o [D] (f32, D <= 384)
+
+template <int D> struct TailShape {
+  static constexpr int NT = D / 32;             // 32-feature output tiles
+  static constexpr int KS = D / 16;             // 16-wide k steps over D
+  static constexpr int NCH = 4 * D / 64;        // 64-unit hidden chunks
+  static constexpr int FW1 = 2 * KS;            // W1 fragments per chunk
+  static constexpr int FW2 = 4 * NT;            // W2' fragments per chunk
+  static constexpr int FPC = FW1 + FW2;         // fragments per chunk
+  static constexpr int SPC = FPC / 16;          // slabs per chunk
+  static constexpr int FPRE = NT * KS;          // W_o' fragments
+  static constexpr int NPRE = FPRE / 16;        // W_o' slabs
+  static constexpr int NSLAB = NPRE + NCH * SPC;
+  static_assert(FW1 % 16 == 0 && FW2 % 16 == 0 && FPRE % 16 == 0, "parts are whole slabs");
+};
+
+// output feature held by MFMA row m of 32-row tile T (lane half hh = (m/4)%2, acc i = 4(m/8) + m%4)
+__host__ __device__ constexpr int tail_out_feat(int T, int m) { return 32 * T + 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); }
+// input feature at k = 8 kh + j of k-step s (B fragments of att / x1; columns of W_o', W1)
+__host__ __device__ constexpr int tail_in_feat(int s, int kh, int j) { return 32 * (s >> 1) + 16 * kh + 8 * (s & 1) + j; }
+// hidden unit (within a 64-unit chunk) at k = 8 kh + j of phase-2 k-step s2 (columns of W2')
+__host__ __device__ constexpr int tail_hid(int s2, int kh, int j) {
+  return 32 * (s2 >> 1) + 8 * ((8 * (s2 & 1) + j) >> 2) + 4 * kh + ((8 * (s2 & 1) + j) & 3);
+}
+
+__device__ __forceinline__ f32x16 mfma32(const u32x4& a, const u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+typedef __bf16 tl_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float tl_f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (RNE) in ONE v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t tl_pack2(float a, float b) {
+  const tl_f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, tl_bf16x2));
+}
+__device__ __forceinline__ float tl_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float tl_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float tl_bf(const u32x4& v, int j) { return (j & 1) ? tl_hi(v[j >> 1]) : tl_lo(v[j >> 1]); }
+
+// wait until at most `younger` (<= MAXY) slabs of this wave (4 LDS-DMA instructions each) are in flight
+template <int MAXY> __device__ __forceinline__ void tl_wait(int younger) {
+  static_assert(4 * MAXY <= 63, "vmcnt range");
+  if constexpr (MAXY <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (younger >= MAXY) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * MAXY) : "memory");
+      return;
+    }
+    tl_wait<MAXY - 1>(younger);
+  }
+}
+
+// calls body(std::integral_constant<int, I>{}) for I = 0 .. N-1: a forced full unroll (every
+// register-array index in the body is a compile-time constant)
+template <typename Body, int... Is>
+__device__ __forceinline__ void tl_unroll(Body&& body, std::integer_sequence<int, Is...>) {
+  (body(std::integral_constant<int, Is>{}), ...);
+}
+
+struct TailArgs {
+  int M;
+  const bf16* act;      // PRE: att [M, D]; else x1 [M, D]
+  const bf16* resid;    // PRE: x (residual of LN1) [M, D]
+  bf16* out;            // [M, D] (PRE: may alias resid)
+  const char* ws;       // weight stream (snvrag_tail_pack)
+  const float* vec;     // [b1 4D | b2' | c1 | g2 | be2]
+  const float* b_o; const float* g1; const float* be1;
+  float eps;
+};
+
+// VAR (diagnostics / tuning): 0 default; 1 = no weight DMA after the prologue (compute-side
+// ceiling; results are garbage)
+template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void tail_kernel(TailArgs p) {
+  using S = TailShape<D>;
+  constexpr int NT = S::NT, KS = S::KS;
+  constexpr int NSLAB = (PRE ? S::NPRE : 0) + S::NCH * S::SPC;      // slabs consumed by this launch
+  constexpr int RING = TL_NSLOT * TL_SLAB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  float* sv = reinterpret_cast<float*>(smem + RING);               // b1 [4D], g1, be1, b_o
+  // wave index as a scalar: every LDS / stream offset below stays in SGPRs
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ln = lane & 31, hh = lane >> 5;
+  const long row = (long)blockIdx.x * TL_ROWS + wave * 32 + ln;
+  const long rc = row < p.M ? row : (long)p.M - 1;
+
+  // ---- activations as B fragments (k-step s: features tail_in_feat(s, hh, 0..7)), residual rows
+  u32x4 xr[KS];                                      // x1 B fragments (PRE: produced by LN1)
+  u32x4 xa[PRE ? KS : 1];                            // PRE: att B fragments
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    // (default cache policy: non-temporal activation loads/stores measured 8 % slower)
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p.act + rc * D + tail_in_feat(s, hh, 0));
+    if constexpr (PRE) xa[s] = v; else xr[s] = v;
+  }
+  u32x4 rr[PRE ? 2 * NT : 1];                        // PRE: residual rows x (folded into ao below)
+  if constexpr (PRE) {
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        rr[2 * T + h2] = *reinterpret_cast<const u32x4*>(p.resid + rc * D + 32 * T + 16 * hh + 8 * h2);
+  }
+  for (int i = tid; i < 4 * D; i += 256) sv[i] = p.vec[i];
+  if constexpr (PRE)
+    for (int i = tid; i < D; i += 256) { sv[4 * D + i] = p.g1[i]; sv[5 * D + i] = p.be1[i]; sv[6 * D + i] = p.b_o[i]; }
+
+  // ---- weight stream: buffer_load ... lds with scalar offsets; chunks rotated per workgroup
+  const int rot = (int)(blockIdx.x % S::NCH);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, S::NSLAB * TL_SLAB, 0x00020000);
+  const int voff = lane * 16;
+  // FFN block order (software pipeline, see the chunk loop): with the stream's blocks
+  // B(2c) = W1(c), B(2c+1) = W2'(c) (H slabs each) and r = rot, block s of the launch is
+  //   s = 0: W1(r);  s = 2k-1 < 2N-1: W1(r+k) = B(2r+s+1);  s = 2k >= 2: W2'(r+k-1) = B(2r+s-1);
+  //   s = 2N-1: W2'(r+N-1) = B(2r+s)   (block indices mod 2N)
+  constexpr int H = S::FW1 / 16;                     // slabs per W1 (= per W2') block
+  constexpr int NB2 = 2 * S::NCH;
+  int is_slot = 0;                                   // ring slot (byte offset) of the next issue
+  int is_pre = 0;                                    // PRE: W_o' slabs issued so far
+  int is_s = 0, is_j = 0;                            // FFN block / slab-in-block of the next issue
+  auto ffn_src = [&]() -> int {
+    int m = 2 * rot + is_s + ((is_s == 0 || is_s == NB2 - 1) ? 0 : (is_s & 1) ? 1 : -1);
+    m = m >= NB2 ? m - NB2 : m;
+    m = m >= NB2 ? m - NB2 : m;                      // (overrun issues run past s = 2N - 1)
+    return (S::NPRE + m * H + is_j) * TL_SLAB;
+  };
+  // Issues run NSLOT - 2 slabs past the end of the launch's stream (the wrapped stream
+  // continues, so the addresses stay valid): every sync then has the same number of slabs in
+  // flight behind the one it waits for — one constant vmcnt, no per-slab branches.  The
+  // overrun lands in slots nobody reads; the epilogue drains it before reusing the ring.
+  auto issue_next = [&]() {
+    auto* dst = (__attribute__((address_space(3))) void*)(ring + is_slot + wave * 4 * TL_FRAG);
+    int src;
+    if (PRE && is_pre < S::NPRE) {
+      src = is_pre * TL_SLAB;
+      ++is_pre;
+    } else {
+      src = ffn_src();
+      ++is_j;
+      if (is_j == H) { is_j = 0; ++is_s; }
+    }
+    tl_unroll([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      // (instruction offset 0: the slab offset rides in soffset, the LDS slot in M0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) char*)dst + j * TL_FRAG, 16,
+                                               voff, src + (wave * 4 + j) * TL_FRAG, 0, 0);
+    }, std::make_integer_sequence<int, 4>{});
+    is_slot = is_slot + TL_SLAB == RING ? 0 : is_slot + TL_SLAB;
+  };
+#pragma unroll
+  for (int g = 0; g < TL_NSLOT - 1; ++g) issue_next();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 2)) : "memory");
+  __syncthreads();                                   // slab 0 + the vector table visible
+
+  // read side: rd_g = launch slab of the current part start, rd_slot its ring slot
+  int rd_g = 0, rd_slot = 0;
+  const int vlane = lane * 16;
+  auto rdA = [&](int j, int fi) -> u32x4 {           // fragment fi of slab rd_g + j (j, fi static)
+    int so = rd_slot + j * TL_SLAB;
+    so = so >= RING ? so - RING : so;
+    return *reinterpret_cast<const u32x4*>(ring + so + vlane + fi * TL_FRAG);
+  };
+  // sync before the first read of slab g (reached PF fragments before its boundary)
+  auto sync = [&](int g) {
+    (void)g;
+    if constexpr (VAR == 1) {
+      __builtin_amdgcn_s_barrier();
+      return;
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 3)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_next();                                    // slab g - 2 + NSLOT into the slot of slab g - 2
+  };
+
+  u32x4 a[TL_PF];
+#pragma unroll
+  for (int i = 0; i < TL_PF; ++i) a[i] = rdA(0, i);
+
+  // consume NF fragments (whole slabs) of the part starting at slab rd_g: mma(f, A) per
+  // fragment, LDS reads PF ahead (into the next part), one sync per slab
+  auto run = [&](auto nf_tag, auto&& mma) {
+    constexpr int NF = decltype(nf_tag)::value;
+    static_assert(NF % 16 == 0, "parts are whole slabs");
+    tl_unroll([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      const u32x4 cur = a[f % TL_PF];
+      if constexpr ((f & 15) == 16 - TL_PF) {
+        // fence the scheduler at every slab sync: bounds the register live ranges of the
+        // fully unrolled stream (hipcc otherwise hoists reads across slabs and spills)
+        __builtin_amdgcn_sched_barrier(0);
+        sync(rd_g + (f >> 4) + 1);
+      }
+      // (past the end of the stream this reads stale ring bytes that are never used)
+      constexpr int qn = f + TL_PF;
+      a[f % TL_PF] = rdA(qn >> 4, qn & 15);
+      mma(fc, cur);
+    }, std::make_integer_sequence<int, NF>{});
+    rd_g += NF / 16;
+    rd_slot += (NF / 16) * TL_SLAB;
+    rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
+  };
+
+  // (ao: out-projection accumulators; acc: FFN accumulators, born in the first chunk with a zero
+  // C operand — explicit zero vectors here get materialised in VGPRs and spilled)
+  f32x16 acc[NT];
+  if constexpr (PRE) {
+    // PRE: the out-projection accumulates onto (x + b_o), so LN1 reads ao alone
+    f32x16 ao[NT];
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ao[T][i] = tl_bf(rr[2 * T + (i >> 3)], i & 7) + sv[6 * D + 32 * T + 16 * hh + i];
+    // ---- ao += att W_o'^T;  fragment f: k-step f / NT, tile f % NT.  A runtime loop over
+    // groups of 4 k-steps (4 NT fragments = whole slabs): the att fragments of the group are
+    // xa[0..3], shifted down after each group (a straight-line 288-MFMA body makes hipcc
+    // shuffle the accumulators between AGPRs)
+    static_assert(KS % 4 == 0 && (4 * NT) % 16 == 0, "groups of 4 k-steps are whole slabs");
+#pragma unroll 1
+    for (int g = 0; g < KS / 4; ++g) {
+      run(std::integral_constant<int, 4 * NT>{}, [&](auto fc, const u32x4& A) {
+        constexpr int f = decltype(fc)::value;
+        ao[f % NT] = mfma32(A, xa[f / NT], ao[f % NT]);
+      });
+#pragma unroll
+      for (int k = 0; k + 4 < KS; ++k) xa[k] = xa[k + 4];
+    }
+    // ---- x1 = LN1(ao) -> xr (B fragments): pass 1 sums v and v^2, pass 2 normalises
+    // (v re-read from the AGPR accumulators, never all held in VGPRs)
+    float sum = 0.f, sq = 0.f;
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { const float v = ao[T][i]; sum += v; sq = fmaf(v, v, sq); }
+#pragma unroll
+    for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(ao[T]));
+    asm volatile("" ::: "memory");
+    sum += __shfl_xor(sum, 32, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    const float mean = sum * (1.0f / D);
+    const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float y[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ft = 32 * T + 16 * hh + i;
+        y[i] = (ao[T][i] - mean) * rstd * sv[4 * D + ft] + sv[5 * D + ft];
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        xr[2 * T + h2] = u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                               tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+    }
+  }
+  // x1 opaque from here on: otherwise hipcc folds the epilogue's bf16 -> f32 unpacking of x1
+  // into LN1 (it knows pack(y)) and carries 192 unpacked floats through the FFN loop
+#pragma unroll
+  for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(xr[k]));
+
+  // ---- FFN over 64-unit hidden chunks, software-pipelined: the MFMAs of phase 1 (W1) of
+  // chunk k run while the VALU epilogue of chunk k-1 (LeakyReLU, LN_f sums, bf16 packing of
+  // its hidden into phase-2 B fragments) is interleaved between them; then phase 2 (W2') of
+  // chunk k-1.  Stream order: W1(0), W1(1), W2'(0), W1(2), W2'(1), ..., W2'(N-1).
+  float st1 = 0.f, st2 = 0.f;
+  f32x16 hc[2], hn[2];                               // hidden of chunk k-1 (epilogue) / k (phase 1)
+  u32x4 hf[4];                                       // phase-2 B fragments (k-step 2t + q)
+  auto epi_pair = [&](int m) {                       // hidden values 2m, 2m+1 of hc (m < 16)
+    const int t = m >> 3, i = 2 * (m & 7);
+    float x0 = hc[t][i], x1 = hc[t][i + 1];
+    x0 = fmaxf(x0, 0.1f * x0);                       // LeakyReLU(0.1)
+    x1 = fmaxf(x1, 0.1f * x1);
+    st1 += x0 + x1;
+    st2 = fmaf(x0, x0, fmaf(x1, x1, st2));
+    hf[2 * t + (i >> 3)][(i & 7) >> 1] = tl_pack2(x0, x1);
+  };
+  // phase 1 of chunk k into hn: h^T = W1_c x1^T + b1 (fragment f: k-step f / 2, tile f % 2; the
+  // bias is the C operand of the first k-step, hidden unit of acc element i: 8(i/4) + 4hh + i%4)
+  auto phase1 = [&](int k, auto epi_tag) {
+    constexpr bool EPI = decltype(epi_tag)::value;
+    const int c = k + rot >= S::NCH ? k + rot - S::NCH : k + rot;
+    const float* b1 = sv + 64 * c + 4 * hh;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float4 bv = *reinterpret_cast<const float4*>(b1 + 32 * t + 8 * r);
+        hn[t][4 * r] = bv.x; hn[t][4 * r + 1] = bv.y; hn[t][4 * r + 2] = bv.z; hn[t][4 * r + 3] = bv.w;
+      }
+    run(std::integral_constant<int, S::FW1>{}, [&](auto fc, const u32x4& A) {
+      constexpr int f = decltype(fc)::value;
+      hn[f & 1] = mfma32(A, xr[f >> 1], hn[f & 1]);
+      constexpr int SP = S::FW1 / 16;                // 16 epilogue pairs spread over the MFMAs
+      if constexpr (EPI && f % SP == 0) epi_pair(f / SP);
+    });
+  };
+  // phase 2 of the chunk whose hidden sits in hf: out^T += W2'_c h_c^T (fragment f: k-step
+  // f / NT, output tile f % NT); the first one starts acc with a zero C operand
+  auto phase2 = [&](auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    run(std::integral_constant<int, S::FW2>{}, [&](auto fc, const u32x4& A) {
+      constexpr int f = decltype(fc)::value;
+      if constexpr (FIRST && f < NT) acc[f] = mfma32(A, hf[0], f32x16{});
+      else acc[f % NT] = mfma32(A, hf[f / NT], acc[f % NT]);
+    });
+  };
+  phase1(0, std::false_type{});
+  hc[0] = hn[0]; hc[1] = hn[1];
+  phase1(1, std::true_type{});
+  phase2(std::true_type{});
+  hc[0] = hn[0]; hc[1] = hn[1];
+#pragma unroll 1
+  for (int k = 2; k < S::NCH; ++k) {
+    phase1(k, std::true_type{});
+    phase2(std::false_type{});
+    hc[0] = hn[0]; hc[1] = hn[1];
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) epi_pair(m);
+  phase2(std::false_type{});
+
+  // ---- epilogue: out = LN2(x1 + lrelu(rstd_f acc - rstd_f mean_f c1 + b2'))
+  st1 += __shfl_xor(st1, 32, 64);
+  st2 += __shfl_xor(st2, 32, 64);
+  const float hm = st1 * (1.0f / (4 * D));
+  const float hr = 1.0f / sqrtf(fmaxf(st2 * (1.0f / (4 * D)) - hm * hm, 0.f) + p.eps);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stream overrun has landed
+  __syncthreads();                                   // every wave is done with the ring
+  float* ev = reinterpret_cast<float*>(ring);        // [b2' | c1 | g2 | be2]
+  for (int i = tid; i < 4 * D; i += 256) ev[i] = p.vec[4 * D + i];
+  __syncthreads();
+  const float* b2 = ev;
+  const float* c1 = ev + D;
+  const float* g2 = ev + 2 * D;
+  const float* be2 = ev + 3 * D;
+  // two passes recomputing v from acc (see LN1): sums of v and v^2, then normalise + store
+  auto v2 = [&](int T, int i) {
+    const int ft = 32 * T + 16 * hh + i;
+    float u = hr * acc[T][i] - hr * hm * c1[ft] + b2[ft];
+    u = fmaxf(u, 0.1f * u);
+    return u + tl_bf(xr[2 * T + (i >> 3)], i & 7);
+  };
+  float sum = 0.f, sq = 0.f;
+#pragma unroll
+  for (int T = 0; T < NT; ++T)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { const float v = v2(T, i); sum += v; sq = fmaf(v, v, sq); }
+#pragma unroll
+  for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(acc[T]));
+#pragma unroll
+  for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(xr[k]));
+  asm volatile("" ::: "memory");
+  sum += __shfl_xor(sum, 32, 64);
+  sq += __shfl_xor(sq, 32, 64);
+  const float mean = sum * (1.0f / D);
+  const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+  if (row < p.M) {
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float y[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ft = 32 * T + 16 * hh + i;
+        y[i] = (v2(T, i) - mean) * rstd * g2[ft] + be2[ft];
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        *reinterpret_cast<u32x4*>(p.out + row * D + 32 * T + 16 * hh + 8 * h2) =
+            u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                  tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+    }
+  }
+}
+
+// One thread per 16-byte piece (8 bf16) of the stream: slab order = consumption order
+// (W_o' fragments, then per 64-unit chunk: W1 then W2').  Fragment lane l = (m = l % 32,
+// kh = l / 32) holds A[m][8 kh .. 8 kh + 7].
+__global__ void tail_pack_kernel(int D, long n_pieces, const bf16* __restrict__ wo, const bf16* __restrict__ w1,
+                                 const bf16* __restrict__ w2g, bf16* __restrict__ out) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pieces) return;
+  const int NT = D / 32, KS = D / 16, FW1 = 2 * KS, FW2 = 4 * NT, FPC = FW1 + FW2, FPRE = NT * KS;
+  const long F = p / 64;
+  const int l = (int)(p % 64), m = l & 31, kh = l >> 5;
+  bf16 v[8];
+  if (F < FPRE) {
+    const int s = (int)(F / NT), T = (int)(F % NT);
+    const int n = tail_out_feat(T, m);
+    for (int j = 0; j < 8; ++j) v[j] = wo[(long)n * D + tail_in_feat(s, kh, j)];
+  } else {
+    const long g = F - FPRE;
+    const int c = (int)(g / FPC), f = (int)(g % FPC);
+    if (f < FW1) {
+      const int s = f >> 1, t = f & 1;
+      const long hid = (long)c * 64 + 32 * t + m;
+      for (int j = 0; j < 8; ++j) v[j] = w1[hid * D + tail_in_feat(s, kh, j)];
+    } else {
+      const int f2 = f - FW1, s2 = f2 / NT, T = f2 % NT;
+      const int n = tail_out_feat(T, m);
+      for (int j = 0; j < 8; ++j) v[j] = w2g[(long)n * 4 * D + (long)c * 64 + tail_hid(s2, kh, j)];
+    }
+  }
+  for (int j = 0; j < 8; ++j) out[p * 8 + j] = v[j];
+}
+
+template <int D, bool PRE>
+static int launch_tail(const TailArgs& a, hipStream_t s) {
+  const char* ev = getenv("SNVRAG_TAIL_VARIANT");
+  const int var = ev ? atoi(ev) : 0;
+  auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, 4, 1> : tail_kernel<D, PRE>;
+  constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + 7 * D * 4;     // ring + b1, g1, be1, b_o
+  static_assert(7 * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, TL_ROWS)), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+static bool tail_d_ok(int D) { return D == 128 || D == 256 || D == 384; }
+
+static size_t tail_bytes(int D) {
+  switch (D) {
+    case 128: return (size_t)TailShape<128>::NSLAB * TL_SLAB;
+    case 256: return (size_t)TailShape<256>::NSLAB * TL_SLAB;
+    case 384: return (size_t)TailShape<384>::NSLAB * TL_SLAB;
+    default: return 0;
+  }
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" size_t snvrag_tail_pack_bytes(int D) { return tail_bytes(D); }
+
+extern "C" int snvrag_tail_pack(int D, const void* w_o, const void* w1, const void* w2g, void* out, void* stream) {
+  SNV_CHECK_ARG(tail_d_ok(D), "block tail needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(w_o && w1 && w2g && out, "null pointer");
+  const long pieces = (long)(tail_bytes(D) / 16);
+  hipLaunchKernelGGL(tail_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
+                     (const bf16*)w_o, (const bf16*)w1, (const bf16*)w2g, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+static int tail_common(int64_t M, int D, bool pre, const TailArgs& a, void* stream) {
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  int rc;
+  if (pre) {
+    switch (D) {
+      case 128: rc = launch_tail<128, true>(a, s); break;
+      case 256: rc = launch_tail<256, true>(a, s); break;
+      default: rc = launch_tail<384, true>(a, s); break;
+    }
+  } else {
+    switch (D) {
+      case 128: rc = launch_tail<128, false>(a, s); break;
+      case 256: rc = launch_tail<256, false>(a, s); break;
+      default: rc = launch_tail<384, false>(a, s); break;
+    }
+  }
+  if (rc) return rc;
+  evlog_end(s, EV_BLOCK, 2.0 * M * (double)D * D * (pre ? 9 : 8));
+  return 0;
+}
+
+extern "C" int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, const void* wstream, const float* b_o,
+                                   const float* ln1_g, const float* ln1_b, const float* ffn_vec, float eps,
+                                   void* stream) {
+  SNV_CHECK_ARG(tail_d_ok(D), "block tail needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(att && x && wstream && b_o && ln1_g && ln1_b && ffn_vec, "null pointer");
+  SNV_CHECK_ARG(att != x, "att and x must not alias");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)att % 16) == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)wstream % 16) == 0 &&
+                    ((uintptr_t)ffn_vec % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  const TailArgs a{(int)M, (const bf16*)att, (const bf16*)x, (bf16*)x, (const char*)wstream, ffn_vec, b_o, ln1_g,
+                   ln1_b, eps};
+  return tail_common(M, D, true, a, stream);
+}
+
+extern "C" int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
+                                       const float* ffn_vec, float eps, void* stream) {
+  SNV_CHECK_ARG(tail_d_ok(D), "block tail needs D in {128, 256, 384}");
+  SNV_CHECK_ARG(x1 && out && wstream && ffn_vec, "null pointer");
+  SNV_CHECK_ARG(x1 != out, "x1 and out must not alias");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)x1 % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wstream % 16) == 0 &&
+                    ((uintptr_t)ffn_vec % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  const TailArgs a{(int)M, (const bf16*)x1, nullptr, (bf16*)out, (const char*)wstream, ffn_vec, nullptr, nullptr,
+                   nullptr, eps};
+  return tail_common(M, D, false, a, stream);
+}

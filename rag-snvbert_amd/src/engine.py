@@ -60,10 +60,15 @@ class Engine:
 
     # ----------------------------------------------------------------- setup --
     def set_dtype(self, dtype: torch.dtype) -> None:
+        """Compute dtype of this module and of the embedding sub-module's engine (retrieval runs
+        on ``model.bert.embedding`` and writes the neighbour means in this dtype)."""
         if dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("compute dtype must be float32 or bfloat16")
         if dtype != self.dtype:
             self.dtype, self._packed = dtype, None
+        _, _, emb = self._modules()
+        if emb is not None and emb is not self.root:
+            engine_for(emb).set_dtype(dtype)
 
     def _modules(self):
         r = self.root
@@ -251,7 +256,7 @@ class Engine:
     def rag_means(self, x: Dict[str, torch.Tensor], B: int, L: int, D: int) -> Optional[torch.Tensor]:
         """[2B, L, D] K-means of retrieved neighbours in compute dtype (bert.py:171-183)."""
         if "rag_block" in x:
-            return x["rag_block"][2 * B:]
+            return x["rag_block"][2 * B:].to(self.dtype)
         if "rag_mean" in x:
             return x["rag_mean"].to(self.dtype).contiguous()
         if "rag_emb_h1" not in x:
@@ -273,9 +278,9 @@ class Engine:
         rag = self.rag_means(x, B, L, D)
         nblk = 4 if rag is not None else 2
         blk = x.get("rag_block")
+        if blk is not None and (blk.dtype != T or tuple(blk.shape) != (4 * B, L, D) or not blk.is_contiguous()):
+            blk = None                                # produced for another dtype: copy below
         if blk is not None:
-            if blk.dtype != T or tuple(blk.shape) != (4 * B, L, D) or not blk.is_contiguous():
-                raise ValueError(f"rag_block must be a contiguous {T} [4B, L, D] block (Engine.input_block)")
             hm = blk                                                  # rag rows already in place
         else:
             hm = torch.empty(nblk * B, L, D, device=h1.device, dtype=T)

@@ -144,6 +144,47 @@ def block_tail_forward(att: torch.Tensor, x: torch.Tensor, wo_stream: torch.Tens
     return x
 
 
+def tail_pack(w_o: torch.Tensor, w1: torch.Tensor, w2g: torch.Tensor) -> torch.Tensor:
+    """One weight stream (W_o', then per 64-unit hidden chunk W1 and W2') of the 32x32-MFMA
+    block tail (csrc/tail.hip)."""
+    D = w_o.shape[1]
+    nbytes = int(N.lib().snvrag_tail_pack_bytes(D))
+    if nbytes == 0:
+        raise ValueError(f"block tail needs D in (128, 256, 384), got {D}")
+    ws = [_c(t.to(torch.bfloat16).contiguous()) for t in (w_o, w1, w2g)]
+    assert tuple(ws[0].shape) == (D, D) and tuple(ws[1].shape) == (4 * D, D) and tuple(ws[2].shape) == (D, 4 * D)
+    out = torch.empty(nbytes, device=w_o.device, dtype=torch.uint8)
+    check(N.lib().snvrag_tail_pack(D, ptr(ws[0]), ptr(ws[1]), ptr(ws[2]), ptr(out), stream_ptr()), "tail_pack")
+    return out
+
+
+def tail_forward(att: torch.Tensor, x: torch.Tensor, wstream: torch.Tensor, b_o, ln1_g, ln1_b,
+                 ffn_vec: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """x <- LN2(x1 + FFN(x1)), x1 = LN1(x + att W_o^T + b_o), in place (32x32-MFMA kernel)."""
+    N.require_gpu(att, x)
+    assert att.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and x.is_contiguous()
+    D = x.shape[-1]
+    M = x.numel() // D
+    f = [_c(t.float().contiguous()) for t in (b_o, ln1_g, ln1_b)]
+    check(N.lib().snvrag_tail_forward(M, D, ptr(_c(att)), ptr(x), ptr(wstream), ptr(f[0]), ptr(f[1]), ptr(f[2]),
+                                      ptr(_c(ffn_vec)), eps, stream_ptr()), "tail_forward")
+    return x
+
+
+def tail_ffn_forward(x1: torch.Tensor, wstream: torch.Tensor, ffn_vec: torch.Tensor, eps: float = 1e-5,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = LN2(x1 + FFN(x1)) (32x32-MFMA kernel, FFN part of the tail stream)."""
+    N.require_gpu(x1)
+    assert x1.dtype == torch.bfloat16
+    D = x1.shape[-1]
+    M = x1.numel() // D
+    if out is None:
+        out = torch.empty_like(x1)
+    check(N.lib().snvrag_tail_ffn_forward(M, D, ptr(_c(x1)), ptr(out), ptr(wstream), ptr(_c(ffn_vec)), eps,
+                                          stream_ptr()), "tail_ffn_forward")
+    return out
+
+
 def stat_tiles(n: int) -> int:
     """Column tiles of the row-panel GEMM for an N (the stats_out leading dim)."""
     for bn in (384, 256, 128, 64):

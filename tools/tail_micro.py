@@ -1,0 +1,95 @@
+"""32x32-MFMA block tail (csrc/tail.hip) vs the 16x16 one (csrc/ffn.hip): correctness against a
+float64 torch reference on a small M, then launch times at the bench shape (M = 512 x 1030)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
+from src import kernels as K  # noqa: E402
+
+D = 384
+dev, bf = "cuda", torch.bfloat16
+F = torch.nn.functional
+
+
+def case(M, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r = lambda *s, sc=1.0: (sc * torch.randn(*s, generator=g)).to(dev)
+    x, att = r(M, D).to(bf), r(M, D, sc=0.5).to(bf)
+    w_o, w1 = (r(D, D) / D ** 0.5).to(bf), (r(4 * D, D) / D ** 0.5).to(bf)
+    w2 = r(D, 4 * D) / (4 * D) ** 0.5
+    b_o, b1, b2 = r(D, sc=0.1), r(4 * D, sc=0.1), r(D, sc=0.1)
+    g1, be1 = 1 + r(D, sc=0.2), r(D, sc=0.1)
+    gf, bff = 1 + r(4 * D, sc=0.2), r(4 * D, sc=0.1)
+    g2, be2 = 1 + r(D, sc=0.2), r(D, sc=0.1)
+    w2g, b2g, _ = K.fold_layernorm(w2, b2, gf, bff, bf)
+    vec = K.ffn_vec(b1, b2g, w2g, g2, be2)
+    return dict(x=x, att=att, w_o=w_o, w1=w1, w2=w2, w2g=w2g, b_o=b_o, b1=b1, b2=b2, g1=g1, be1=be1, gf=gf,
+                bff=bff, g2=g2, be2=be2, vec=vec)
+
+
+def ref(c, pre=True):
+    xd = c["x"].double()
+    if pre:
+        x1 = F.layer_norm(xd + c["att"].double() @ c["w_o"].double().T + c["b_o"].double(), (D,),
+                          c["g1"].double(), c["be1"].double(), 1e-5)
+    else:
+        x1 = xd
+    h = F.leaky_relu(x1 @ c["w1"].double().T + c["b1"].double(), 0.1)
+    hn = F.layer_norm(h, (4 * D,), c["gf"].double(), c["bff"].double(), 1e-5)
+    f = F.leaky_relu(hn @ c["w2"].double().T + c["b2"].double(), 0.1)
+    return F.layer_norm(x1 + f, (D,), c["g2"].double(), c["be2"].double(), 1e-5)
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+c = case(777 + 128 * 3)
+ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
+xx = c["x"].clone()
+K.tail_forward(c["att"], xx, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+e = (xx.double() - ref(c, True)).abs()
+print(f"tail PRE   max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", flush=True)
+o = K.tail_ffn_forward(c["x"], ts, c["vec"])
+e = (o.double() - ref(c, False)).abs()
+print(f"tail FFN   max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", flush=True)
+old = c["x"].clone()
+K.block_tail_forward(c["att"], old, K.ffn_pre_pack(c["w_o"]), c["b_o"], c["g1"], c["be1"],
+                     K.ffn_pack(c["w1"], c["w2g"]), c["vec"])
+e = (old.double() - ref(c, True)).abs()
+print(f"ffn.hip    max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", flush=True)
+
+M = int(os.environ.get("GM_M", 512 * 1030))
+c = case(M, 1)
+ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
+ws, wo = K.ffn_pack(c["w1"], c["w2g"]), K.ffn_pre_pack(c["w_o"])
+xs = c["x"].clone()
+out = torch.empty_like(c["x"])
+fl9, fl8 = 18.0 * M * D * D, 16.0 * M * D * D
+def tail_var(v):
+    def fn():
+        os.environ["SNVRAG_TAIL_VARIANT"] = str(v)
+        K.tail_forward(c["att"], xs, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+    return fn
+
+
+for name, fn, fl in (
+        ("ffn.hip block tail", lambda: K.block_tail_forward(c["att"], xs, wo, c["b_o"], c["g1"], c["be1"], ws, c["vec"]), fl9),
+        ("tail.hip PRE", tail_var(0), fl9),
+        ("tail.hip PRE PF=8", tail_var(1), fl9),
+        ("tail.hip PRE no-DMA (diag)", tail_var(2), fl9),
+        ("ffn.hip FFN only", lambda: K.ffn_forward(c["x"], ws, c["vec"], out=out), fl8),
+        ("tail.hip FFN only", lambda: (os.environ.__setitem__("SNVRAG_TAIL_VARIANT", "0"),
+                                       K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
+    ms = timeit(fn)
+    print(f"{name:22s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
