@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 10
+#define SNVRAG_ABI_VERSION 11
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -248,6 +248,10 @@ typedef struct {
   /* optional (bf16, with ffn_w/ffn_v): snvrag_ffn_pre_pack of w_o -> the attention
    * output projection + LN1 run inside the fused FFN launch (snvrag_block_tail_forward) */
   const void* o_ws;
+  /* optional (bf16, with ffn_v, D in {128,256,384}): snvrag_tail_pack of (w_o, w1, w2g) ->
+   * the whole block tail runs on the 32x32-MFMA kernel (snvrag_tail_forward); takes
+   * precedence over o_ws / ffn_w */
+  const void* tail_w;
 } snvrag_layer_t;
 
 /* ------------------------------------------------------------------------

@@ -90,6 +90,13 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       const float sc = ly.q_scale > 0.f ? scale / ly.q_scale : scale;
       rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, sc, stream);
       if (rc) return rc;
+      if (fused && dtype == SNVRAG_BF16 && ly.tail_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN") &&
+          !getenv("SNVRAG_NO_TAIL") && !getenv("SNVRAG_TAIL16")) {
+        // the whole block tail on 32x32 MFMAs (csrc/tail.hip): one launch
+        rc = snvrag_tail_forward(M, D, att, xc, ly.tail_w, ly.b_o, ly.ln1_g, ly.ln1_b, ly.ffn_v, 1e-5f, stream);
+        if (rc) return rc;
+        continue;
+      }
       if (fused && dtype == SNVRAG_BF16 && ly.o_ws && ly.ffn_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN") &&
           !getenv("SNVRAG_NO_TAIL")) {
         // x = LN2(x1 + FFN(x1)), x1 = LN1(x + attn Wo^T + bo): one launch, x1 in LDS

@@ -31,7 +31,7 @@ namespace snvrag {
 constexpr int TL_FRAG = 1024;               // one A fragment: 32 rows x 16 k bf16
 constexpr int TL_SLAB = 16 * TL_FRAG;
 constexpr int TL_NSLOT = 9;                 // ring slots (144 KiB)
-constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead
+constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead (4: 1.634 ms, 8: 1.659 ms at M = 527360)
 constexpr int TL_ROWS = 128;
 constexpr int TL_VEC_LDS = 11 * 1024;       // b1 [4D] + g1, be1, b_o [D] (f32, D <= 384)
 
@@ -67,6 +67,17 @@ typedef float tl_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t tl_pack2(float a, float b) {
   const tl_f32x2 v = {a, b};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, tl_bf16x2));
+}
+// LeakyReLU(0.1) in 2 VALU ops (fmaxf on a register hipcc cannot prove canonical costs a third,
+// a v_max x, x canonicalisation)
+__device__ __forceinline__ float tl_lrelu(float x) {
+  float r;
+  asm("v_mul_f32 %0, 0x3dcccccd, %1\n v_max_f32 %0, %1, %0" : "=&v"(r) : "v"(x));
+  return r;
+}
+// 32-bit LDS address of a pointer into dynamic shared memory
+__device__ __forceinline__ uint32_t tl_lds(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 __device__ __forceinline__ float tl_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float tl_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
@@ -104,9 +115,10 @@ struct TailArgs {
   float eps;
 };
 
-// VAR (diagnostics / tuning): 0 default; 1 = no weight DMA after the prologue (compute-side
-// ceiling; results are garbage)
-template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0>
+// VAR (diagnostics): 0 default; 1 = no weight DMA after the prologue (compute-side ceiling;
+// results are garbage).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
+// SNVRAG_TAIL_VARIANT (launch_tail): 1 = PF 8, 2 = VAR 1, 3 = no schedule groups.
+template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0, bool TL_SGB = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void tail_kernel(TailArgs p) {
   using S = TailShape<D>;
@@ -123,7 +135,13 @@ void tail_kernel(TailArgs p) {
   const long row = (long)blockIdx.x * TL_ROWS + wave * 32 + ln;
   const long rc = row < p.M ? row : (long)p.M - 1;
 
-  // ---- activations as B fragments (k-step s: features tail_in_feat(s, hh, 0..7)), residual rows
+  // ---- vector tables to LDS first (their loads are waited on at once), then the activations
+  // as B fragments (k-step s: features tail_in_feat(s, hh, 0..7)); the residual rows of PRE are
+  // loaded after the weight prologue (below) and only needed at LN1, so their HBM burst runs
+  // under the out-projection MFMAs
+  for (int i = tid; i < 4 * D; i += 256) sv[i] = p.vec[i];
+  if constexpr (PRE)
+    for (int i = tid; i < D; i += 256) { sv[4 * D + i] = p.g1[i]; sv[5 * D + i] = p.be1[i]; sv[6 * D + i] = p.b_o[i]; }
   u32x4 xr[KS];                                      // x1 B fragments (PRE: produced by LN1)
   u32x4 xa[PRE ? KS : 1];                            // PRE: att B fragments
 #pragma unroll
@@ -132,17 +150,6 @@ void tail_kernel(TailArgs p) {
     const u32x4 v = *reinterpret_cast<const u32x4*>(p.act + rc * D + tail_in_feat(s, hh, 0));
     if constexpr (PRE) xa[s] = v; else xr[s] = v;
   }
-  u32x4 rr[PRE ? 2 * NT : 1];                        // PRE: residual rows x (folded into ao below)
-  if constexpr (PRE) {
-#pragma unroll
-    for (int T = 0; T < NT; ++T)
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-        rr[2 * T + h2] = *reinterpret_cast<const u32x4*>(p.resid + rc * D + 32 * T + 16 * hh + 8 * h2);
-  }
-  for (int i = tid; i < 4 * D; i += 256) sv[i] = p.vec[i];
-  if constexpr (PRE)
-    for (int i = tid; i < D; i += 256) { sv[4 * D + i] = p.g1[i]; sv[5 * D + i] = p.be1[i]; sv[6 * D + i] = p.b_o[i]; }
 
   // ---- weight stream: buffer_load ... lds with scalar offsets; chunks rotated per workgroup
   const int rot = (int)(blockIdx.x % S::NCH);
@@ -156,13 +163,18 @@ void tail_kernel(TailArgs p) {
   constexpr int H = S::FW1 / 16;                     // slabs per W1 (= per W2') block
   constexpr int NB2 = 2 * S::NCH;
   int is_slot = 0;                                   // ring slot (byte offset) of the next issue
-  int is_pre = 0;                                    // PRE: W_o' slabs issued so far
-  int is_s = 0, is_j = 0;                            // FFN block / slab-in-block of the next issue
-  auto ffn_src = [&]() -> int {
-    int m = 2 * rot + is_s + ((is_s == 0 || is_s == NB2 - 1) ? 0 : (is_s & 1) ? 1 : -1);
+  int is_i = 0;                                      // launch slab index of the next issue
+  // stream byte offset of launch slab is_i, branch-free (selects only: a branch here splits the
+  // unrolled MFMA stream into basic blocks and the register allocator then spills across them)
+  auto src_of = [&](int i) -> int {
+    constexpr int NP = PRE ? S::NPRE : 0;
+    const int q = i - NP > 0 ? i - NP : 0;
+    const int s = q / H, j = q - s * H;              // FFN block, slab within it
+    int m = 2 * rot + s + ((s == 0 || s == NB2 - 1) ? 0 : (s & 1) ? 1 : -1);
     m = m >= NB2 ? m - NB2 : m;
     m = m >= NB2 ? m - NB2 : m;                      // (overrun issues run past s = 2N - 1)
-    return (S::NPRE + m * H + is_j) * TL_SLAB;
+    const int ffn = (S::NPRE + m * H + j) * TL_SLAB;
+    return i < NP ? i * TL_SLAB : ffn;
   };
   // Issues run NSLOT - 2 slabs past the end of the launch's stream (the wrapped stream
   // continues, so the addresses stay valid): every sync then has the same number of slabs in
@@ -170,15 +182,8 @@ void tail_kernel(TailArgs p) {
   // overrun lands in slots nobody reads; the epilogue drains it before reusing the ring.
   auto issue_next = [&]() {
     auto* dst = (__attribute__((address_space(3))) void*)(ring + is_slot + wave * 4 * TL_FRAG);
-    int src;
-    if (PRE && is_pre < S::NPRE) {
-      src = is_pre * TL_SLAB;
-      ++is_pre;
-    } else {
-      src = ffn_src();
-      ++is_j;
-      if (is_j == H) { is_j = 0; ++is_s; }
-    }
+    const int src = src_of(is_i);
+    ++is_i;
     tl_unroll([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       // (instruction offset 0: the slab offset rides in soffset, the LDS slot in M0)
@@ -189,51 +194,74 @@ void tail_kernel(TailArgs p) {
   };
 #pragma unroll
   for (int g = 0; g < TL_NSLOT - 1; ++g) issue_next();
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 2)) : "memory");
-  __syncthreads();                                   // slab 0 + the vector table visible
+  // PRE: the residual rows x, behind the weight prologue in the vmcnt order (NRR loads)
+  constexpr int NRR = PRE ? 2 * NT : 0;
+  u32x4 rr[PRE ? 2 * NT : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        rr[2 * T + h2] = *reinterpret_cast<const u32x4*>(p.resid + rc * D + 32 * T + 16 * hh + 8 * h2);
+  }
+  static_assert(4 * (TL_NSLOT - 2) + NRR <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 2) + NRR) : "memory");
+  __syncthreads();                                   // slab 0, the activations + the vector tables visible
 
   // read side: rd_g = launch slab of the current part start, rd_slot its ring slot
   int rd_g = 0, rd_slot = 0;
-  const int vlane = lane * 16;
-  auto rdA = [&](int j, int fi) -> u32x4 {           // fragment fi of slab rd_g + j (j, fi static)
+  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {   // fragment fi of slab rd_g + j
+    constexpr int j = decltype(j_tag)::value, fi = decltype(fi_tag)::value;
     int so = rd_slot + j * TL_SLAB;
     so = so >= RING ? so - RING : so;
-    return *reinterpret_cast<const u32x4*>(ring + so + vlane + fi * TL_FRAG);
+    return *reinterpret_cast<const u32x4*>(ring + so + lane * 16 + fi * TL_FRAG);
   };
   // sync before the first read of slab g (reached PF fragments before its boundary)
-  auto sync = [&](int g) {
-    (void)g;
+  // (g is a compile-time constant where it matters: PRE's first NSLOT - 2 slabs, issued before
+  // the residual loads, have those NRR loads behind them in the vmcnt order)
+  auto sync = [&](auto g_tag) {
+    constexpr int g = decltype(g_tag)::value;
     if constexpr (VAR == 1) {
       __builtin_amdgcn_s_barrier();
       return;
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 3)) : "memory");
+    if constexpr (PRE && g >= 0 && g <= TL_NSLOT - 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 3) + NRR) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 3)) : "memory");
     __builtin_amdgcn_s_barrier();
     issue_next();                                    // slab g - 2 + NSLOT into the slot of slab g - 2
   };
 
   u32x4 a[TL_PF];
-#pragma unroll
-  for (int i = 0; i < TL_PF; ++i) a[i] = rdA(0, i);
+  tl_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
+            std::make_integer_sequence<int, TL_PF>{});
 
   // consume NF fragments (whole slabs) of the part starting at slab rd_g: mma(f, A) per
   // fragment, LDS reads PF ahead (into the next part), one sync per slab
-  auto run = [&](auto nf_tag, auto&& mma) {
+  // G0: the part's first launch slab when known at compile time (PRE), else -1
+  auto run = [&](auto nf_tag, auto g0_tag, auto&& mma) {
     constexpr int NF = decltype(nf_tag)::value;
+    constexpr int G0 = decltype(g0_tag)::value;
     static_assert(NF % 16 == 0, "parts are whole slabs");
     tl_unroll([&](auto fc) {
       constexpr int f = decltype(fc)::value;
       const u32x4 cur = a[f % TL_PF];
       if constexpr ((f & 15) == 16 - TL_PF) {
         // fence the scheduler at every slab sync: bounds the register live ranges of the
-        // fully unrolled stream (hipcc otherwise hoists reads across slabs and spills)
+        // fully unrolled stream (hipcc otherwise hoists work across slabs and spills)
         __builtin_amdgcn_sched_barrier(0);
-        sync(rd_g + (f >> 4) + 1);
+        sync(std::integral_constant<int, (G0 < 0 ? -1 : G0 + (f >> 4) + 1)>{});
       }
+      mma(fc, cur);
       // (past the end of the stream this reads stale ring bytes that are never used)
       constexpr int qn = f + TL_PF;
-      a[f % TL_PF] = rdA(qn >> 4, qn & 15);
-      mma(fc, cur);
+      a[f % TL_PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
+      if constexpr (TL_SGB) {
+        // pipeline shape for the scheduler: MFMA f, then the read PF fragments ahead
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
     }, std::make_integer_sequence<int, NF>{});
     rd_g += NF / 16;
     rd_slot += (NF / 16) * TL_SLAB;
@@ -244,33 +272,36 @@ void tail_kernel(TailArgs p) {
   // C operand — explicit zero vectors here get materialised in VGPRs and spilled)
   f32x16 acc[NT];
   if constexpr (PRE) {
-    // PRE: the out-projection accumulates onto (x + b_o), so LN1 reads ao alone
+    // PRE: the out-projection accumulates onto b_o; LN1 adds the residual x (loaded late, see rr)
     f32x16 ao[NT];
 #pragma unroll
     for (int T = 0; T < NT; ++T)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) ao[T][i] = tl_bf(rr[2 * T + (i >> 3)], i & 7) + sv[6 * D + 32 * T + 16 * hh + i];
+      for (int i = 0; i < 16; ++i) ao[T][i] = sv[6 * D + 32 * T + 16 * hh + i];
     // ---- ao += att W_o'^T;  fragment f: k-step f / NT, tile f % NT.  A runtime loop over
     // groups of 4 k-steps (4 NT fragments = whole slabs): the att fragments of the group are
     // xa[0..3], shifted down after each group (a straight-line 288-MFMA body makes hipcc
     // shuffle the accumulators between AGPRs)
     static_assert(KS % 4 == 0 && (4 * NT) % 16 == 0, "groups of 4 k-steps are whole slabs");
-#pragma unroll 1
-    for (int g = 0; g < KS / 4; ++g) {
-      run(std::integral_constant<int, 4 * NT>{}, [&](auto fc, const u32x4& A) {
+    tl_unroll([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      run(std::integral_constant<int, 4 * NT>{}, std::integral_constant<int, g * (NT / 4)>{}, [&](auto fc, const u32x4& A) {
         constexpr int f = decltype(fc)::value;
-        ao[f % NT] = mfma32(A, xa[f / NT], ao[f % NT]);
+        ao[f % NT] = mfma32(A, xa[4 * g + f / NT], ao[f % NT]);
       });
-#pragma unroll
-      for (int k = 0; k + 4 < KS; ++k) xa[k] = xa[k + 4];
-    }
+    }, std::make_integer_sequence<int, KS / 4>{});
     // ---- x1 = LN1(ao) -> xr (B fragments): pass 1 sums v and v^2, pass 2 normalises
     // (v re-read from the AGPR accumulators, never all held in VGPRs)
     float sum = 0.f, sq = 0.f;
 #pragma unroll
     for (int T = 0; T < NT; ++T)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { const float v = ao[T][i]; sum += v; sq = fmaf(v, v, sq); }
+      for (int i = 0; i < 16; ++i) {
+        const float v = ao[T][i] + tl_bf(rr[2 * T + (i >> 3)], i & 7);
+        ao[T][i] = v;
+        sum += v;
+        sq = fmaf(v, v, sq);
+      }
 #pragma unroll
     for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(ao[T]));
     asm volatile("" ::: "memory");
@@ -302,60 +333,76 @@ void tail_kernel(TailArgs p) {
   // its hidden into phase-2 B fragments) is interleaved between them; then phase 2 (W2') of
   // chunk k-1.  Stream order: W1(0), W1(1), W2'(0), W1(2), W2'(1), ..., W2'(N-1).
   float st1 = 0.f, st2 = 0.f;
-  f32x16 hc[2], hn[2];                               // hidden of chunk k-1 (epilogue) / k (phase 1)
+  const uint32_t sv_lane = tl_lds(reinterpret_cast<const char*>(sv)) + 16 * hh;
+  f32x16 h0[2], h1[2];                               // hidden of even / odd chunks (ping-pong)
   u32x4 hf[4];                                       // phase-2 B fragments (k-step 2t + q)
-  auto epi_pair = [&](int m) {                       // hidden values 2m, 2m+1 of hc (m < 16)
+  auto epi_pair = [&](const f32x16 (&hc)[2], int m) {   // hidden values 2m, 2m+1 of hc (m < 16)
     const int t = m >> 3, i = 2 * (m & 7);
     float x0 = hc[t][i], x1 = hc[t][i + 1];
-    x0 = fmaxf(x0, 0.1f * x0);                       // LeakyReLU(0.1)
-    x1 = fmaxf(x1, 0.1f * x1);
+    x0 = tl_lrelu(x0);
+    x1 = tl_lrelu(x1);
     st1 += x0 + x1;
     st2 = fmaf(x0, x0, fmaf(x1, x1, st2));
     hf[2 * t + (i >> 3)][(i & 7) >> 1] = tl_pack2(x0, x1);
   };
   // phase 1 of chunk k into hn: h^T = W1_c x1^T + b1 (fragment f: k-step f / 2, tile f % 2; the
-  // bias is the C operand of the first k-step, hidden unit of acc element i: 8(i/4) + 4hh + i%4)
-  auto phase1 = [&](int k, auto epi_tag) {
+  // bias is the C operand of the first k-step, hidden unit of acc element i: 8(i/4) + 4hh + i%4),
+  // with the epilogue of the previous chunk (hc) interleaved when EPI
+  auto phase1 = [&](int k, f32x16 (&hn)[2], const f32x16 (&hc)[2], auto epi_tag) {
     constexpr bool EPI = decltype(epi_tag)::value;
     const int c = k + rot >= S::NCH ? k + rot - S::NCH : k + rot;
-    const float* b1 = sv + 64 * c + 4 * hh;
+    const uint32_t b1 = sv_lane + 256 * c;          // &sv[64 c + 4 hh]
+    u32x4 bv[8];
+    // bv[r] = floats 32 (r / 4) + 8 (r % 4) .. + 3 of the chunk's bias: reads and their wait in ONE
+    // asm statement (outputs early-clobber: the address stays intact until the last read)
+    asm volatile(
+        "ds_read_b128 %0, %8 offset:0\n ds_read_b128 %1, %8 offset:32\n ds_read_b128 %2, %8 offset:64\n"
+        " ds_read_b128 %3, %8 offset:96\n ds_read_b128 %4, %8 offset:128\n ds_read_b128 %5, %8 offset:160\n"
+        " ds_read_b128 %6, %8 offset:192\n ds_read_b128 %7, %8 offset:224\n s_waitcnt lgkmcnt(0)"
+        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3]), "=&v"(bv[4]), "=&v"(bv[5]), "=&v"(bv[6]), "=&v"(bv[7])
+        : "v"(b1));
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float4 bv = *reinterpret_cast<const float4*>(b1 + 32 * t + 8 * r);
-        hn[t][4 * r] = bv.x; hn[t][4 * r + 1] = bv.y; hn[t][4 * r + 2] = bv.z; hn[t][4 * r + 3] = bv.w;
-      }
-    run(std::integral_constant<int, S::FW1>{}, [&](auto fc, const u32x4& A) {
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hn[t][4 * r + e] = __uint_as_float(bv[4 * t + r][e]);
+    run(std::integral_constant<int, S::FW1>{}, std::integral_constant<int, -1>{}, [&](auto fc, const u32x4& A) {
       constexpr int f = decltype(fc)::value;
       hn[f & 1] = mfma32(A, xr[f >> 1], hn[f & 1]);
       constexpr int SP = S::FW1 / 16;                // 16 epilogue pairs spread over the MFMAs
-      if constexpr (EPI && f % SP == 0) epi_pair(f / SP);
+      if constexpr (EPI && f % SP == 0) epi_pair(hc, f / SP);
     });
   };
   // phase 2 of the chunk whose hidden sits in hf: out^T += W2'_c h_c^T (fragment f: k-step
   // f / NT, output tile f % NT); the first one starts acc with a zero C operand
   auto phase2 = [&](auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
-    run(std::integral_constant<int, S::FW2>{}, [&](auto fc, const u32x4& A) {
+    run(std::integral_constant<int, S::FW2>{}, std::integral_constant<int, -1>{}, [&](auto fc, const u32x4& A) {
       constexpr int f = decltype(fc)::value;
       if constexpr (FIRST && f < NT) acc[f] = mfma32(A, hf[0], f32x16{});
       else acc[f % NT] = mfma32(A, hf[f / NT], acc[f % NT]);
     });
   };
-  phase1(0, std::false_type{});
-  hc[0] = hn[0]; hc[1] = hn[1];
-  phase1(1, std::true_type{});
+  // even chunks in h0, odd in h1: no hidden copies (a loop-carried copy makes hipcc shuffle
+  // the accumulator registers at every back edge)
+  static_assert(S::NCH % 2 == 0 && S::NCH >= 4, "chunk pairs");
+  phase1(0, h0, h1, std::false_type{});
+  phase1(1, h1, h0, std::true_type{});
   phase2(std::true_type{});
-  hc[0] = hn[0]; hc[1] = hn[1];
+  phase1(2, h0, h1, std::true_type{});
+  phase2(std::false_type{});
 #pragma unroll 1
-  for (int k = 2; k < S::NCH; ++k) {
-    phase1(k, std::true_type{});
+  for (int k = 3; k + 1 < S::NCH; k += 2) {
+    phase1(k, h1, h0, std::true_type{});
     phase2(std::false_type{});
-    hc[0] = hn[0]; hc[1] = hn[1];
+    phase1(k + 1, h0, h1, std::true_type{});
+    phase2(std::false_type{});
   }
+  phase1(S::NCH - 1, h1, h0, std::true_type{});
+  phase2(std::false_type{});
 #pragma unroll
-  for (int m = 0; m < 16; ++m) epi_pair(m);
+  for (int m = 0; m < 16; ++m) epi_pair(h1, m);
   phase2(std::false_type{});
 
   // ---- epilogue: out = LN2(x1 + lrelu(rstd_f acc - rstd_f mean_f c1 + b2'))
@@ -372,27 +419,30 @@ void tail_kernel(TailArgs p) {
   const float* c1 = ev + D;
   const float* g2 = ev + 2 * D;
   const float* be2 = ev + 3 * D;
-  // two passes recomputing v from acc (see LN1): sums of v and v^2, then normalise + store
-  auto v2 = [&](int T, int i) {
-    const int ft = 32 * T + 16 * hh + i;
-    float u = hr * acc[T][i] - hr * hm * c1[ft] + b2[ft];
-    u = fmaxf(u, 0.1f * u);
-    return u + tl_bf(xr[2 * T + (i >> 3)], i & 7);
-  };
+  // pass 1: v = x1 + lrelu(rstd_f (acc - mean_f c1) + b2') written back over acc, sums of v and
+  // v^2; pass 2 normalises v in place of acc and stores
   float sum = 0.f, sq = 0.f;
 #pragma unroll
   for (int T = 0; T < NT; ++T)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { const float v = v2(T, i); sum += v; sq = fmaf(v, v, sq); }
+    for (int i = 0; i < 16; ++i) {
+      const int ft = 32 * T + 16 * hh + i;
+      float u = hr * fmaf(-hm, c1[ft], acc[T][i]) + b2[ft];
+      u = tl_lrelu(u);
+      const float v = u + tl_bf(xr[2 * T + (i >> 3)], i & 7);
+      acc[T][i] = v;
+      sum += v;
+      sq = fmaf(v, v, sq);
+    }
 #pragma unroll
   for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(acc[T]));
-#pragma unroll
-  for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(xr[k]));
   asm volatile("" ::: "memory");
   sum += __shfl_xor(sum, 32, 64);
   sq += __shfl_xor(sq, 32, 64);
   const float mean = sum * (1.0f / D);
   const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+  const float nmr = -mean * rstd;
+  auto v2 = [&](int T, int i) { return fmaf(acc[T][i], rstd, nmr); };
   if (row < p.M) {
 #pragma unroll
     for (int T = 0; T < NT; ++T) {
@@ -400,7 +450,7 @@ void tail_kernel(TailArgs p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ft = 32 * T + 16 * hh + i;
-        y[i] = (v2(T, i) - mean) * rstd * g2[ft] + be2[ft];
+        y[i] = fmaf(v2(T, i), g2[ft], be2[ft]);
       }
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2)
@@ -446,7 +496,8 @@ template <int D, bool PRE>
 static int launch_tail(const TailArgs& a, hipStream_t s) {
   const char* ev = getenv("SNVRAG_TAIL_VARIANT");
   const int var = ev ? atoi(ev) : 0;
-  auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, 4, 1> : tail_kernel<D, PRE>;
+  auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
+              : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false> : tail_kernel<D, PRE>;
   constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + 7 * D * 4;     // ring + b1, g1, be1, b_o
   static_assert(7 * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

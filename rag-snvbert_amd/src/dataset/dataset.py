@@ -9,6 +9,7 @@ loud error); ``from_arrays`` takes the same data in memory.
 
 from __future__ import annotations
 
+import math
 from typing import Dict, List, Sequence
 
 import numpy as np
@@ -136,21 +137,102 @@ class TrainDataset(torch.utils.data.Dataset):
 
     @classmethod
     def from_file(cls, vocab, vcfpath, panelpath, freqpath, windowpath, typepath, poppath, pospath):
-        try:
-            import h5py  # noqa: F401
-        except ImportError as e:
-            raise RuntimeError("TrainDataset.from_file needs h5py (not installed here); "
-                               "use from_arrays with in-memory GT/POS") from e
-        import pickle
-        f = h5py.File(vcfpath, "r")
-        gt = f["calldata/GT"][:]
-        gt[gt > 0] = 1
-        pos = f["variants/POS"][:]
-        with open(typepath, "rb") as fh:
-            t2i = pickle.load(fh)
-        with open(poppath, "rb") as fh:
-            p2i = pickle.load(fh)
-        with open(pospath, "rb") as fh:
-            pos2i = pickle.load(fh)
+        gt, pos, t2i, p2i, pos2i = _read_inputs(vcfpath, typepath, poppath, pospath)
         return cls(vocab, gt, pos, PanelData.from_file(panelpath), np.load(freqpath),
                    Window.from_file(windowpath), t2i, p2i, pos2i)
+
+
+def _read_inputs(vcfpath, typepath, poppath, pospath):
+    """GT (ALT > 0 -> 1), POS and the three mapping pickles (dataset.py:190-230, :747-771).
+    The pickles are the reference's own mapping files, opened as the reference does."""
+    try:
+        import h5py
+    except ImportError as e:
+        raise RuntimeError("reading the VCF/H5 inputs needs h5py (not installed here); "
+                           "use from_arrays with in-memory GT/POS") from e
+    import pickle
+    with h5py.File(vcfpath, "r") as f:
+        gt = f["calldata/GT"][:]
+        pos = f["variants/POS"][:]
+    gt[gt > 0] = 1
+    maps = []
+    for path in (typepath, poppath, pospath):
+        with open(path, "rb") as fh:
+            maps.append(pickle.load(fh))
+    return (gt, pos, *maps)
+
+
+INFER_WINDOW_LEN = 1020     # dataset.py:26
+
+
+class InferDataset(torch.utils.data.Dataset):
+    """Imputation featurisation (dataset.py:629-900), vectorised.
+
+    Sites are the panel's full site list ``ori_pos`` (the keys of ``pos_to_idx``, in
+    insertion order); a site absent from the target VCF is ``position_needed`` — its
+    haplotype value is 0 and its mask bit 1 (the sites to impute).  Items run
+    sample-major: ``item = sample * window_count + window`` over fixed windows of
+    ``window_len`` sites (dataset.py:700, :818-825)."""
+    long_fields = ["hap_1", "hap_2", "mask", "sample_idx", "start_idx", "end_idx", "hap1_nomask", "hap2_nomask"]
+    float_fields = ["pos", "af", "af_p", "ref", "het", "hom"]
+
+    def __init__(self, vocab: WordVocab, vcf: np.ndarray, pos: np.ndarray, panel: PanelData, freq: np.ndarray,
+                 type_to_idx: Dict, pop_to_idx: Dict, pos_to_idx: Dict, window_len: int = INFER_WINDOW_LEN):
+        self.vocab, self.vcf, self.pos = vocab, vcf, np.asarray(pos)
+        self.panel, self.freq = panel, freq
+        self.type_to_idx, self.pop_to_idx, self.pos_to_idx = type_to_idx, pop_to_idx, pos_to_idx
+        self.window_len = int(window_len)
+        self.ori_pos = np.array(list(pos_to_idx.keys()))
+        self.position_needed = ~np.isin(self.ori_pos, self.pos, assume_unique=True)
+        self.test_pos_to_idx = {p: i for i, p in enumerate(self.pos)}
+        # vectorised lookups: target-VCF row of every panel site (-1 = absent) and its freq column
+        self._vcf_row = np.full(len(self.ori_pos), -1, np.int64)
+        if len(self.pos):
+            order = np.argsort(self.pos, kind="stable")
+            # last occurrence of a duplicated position, like the reference's dict (dataset.py:692)
+            at = np.clip(np.searchsorted(self.pos[order], self.ori_pos, side="right") - 1, 0, len(self.pos) - 1)
+            hit = self.pos[order][at] == self.ori_pos
+            self._vcf_row[hit] = order[at][hit]
+        self._freq_col = np.fromiter(pos_to_idx.values(), dtype=np.int64, count=len(pos_to_idx))
+        self.window_count = math.ceil(self.ori_pos.shape[0] / self.window_len)
+        self.sample_count = self.vcf.shape[1] * self.window_count
+
+    def __len__(self):
+        return self.sample_count
+
+    def tokenize(self, seq: np.ndarray, mask: np.ndarray = None) -> np.ndarray:
+        return self.vocab.tokenize(seq, mask)
+
+    def window_bounds(self, w: int):
+        start = self.window_len * w
+        return start, min(start + self.window_len, self.ori_pos.shape[0])
+
+    def __getitem__(self, item: int) -> dict:
+        sample_idx, window_idx = item // self.window_count, item % self.window_count
+        start, end = self.window_bounds(window_idx)
+        out = {"sample_idx": [sample_idx], "start_idx": [start], "end_idx": [end]}
+        rows = self._vcf_row[start:end]
+        need = rows < 0
+        h1 = np.where(need, 0, np.asarray(self.vcf[np.maximum(rows, 0), sample_idx, 0])).astype(np.int64)
+        h2 = np.where(need, 0, np.asarray(self.vcf[np.maximum(rows, 0), sample_idx, 1])).astype(np.int64)
+        mask = sequence_padding(need.astype(np.int64), "int")
+        out["mask"] = mask
+        out["hap1_nomask"], out["hap2_nomask"] = h1, h2
+        out["hap_1"] = self.tokenize(h1, mask)
+        out["hap_2"] = self.tokenize(h2, mask)
+        out["pos"] = sequence_padding(position_normalize(self.ori_pos[start:end]), "float")
+        pop_key = self.pop_to_idx[self.panel.pop_list[sample_idx]]
+        cols = self._freq_col[start:end]
+        pad = lambda v: sequence_padding(v, dtype="float")
+        out.update(af=pad(self.freq[AF][GLOBAL][cols]), af_p=pad(self.freq[AF][pop_key][cols]),
+                   ref=pad(self.freq[REF][pop_key][cols]), het=pad(self.freq[HET][pop_key][cols]),
+                   hom=pad(self.freq[HOM][pop_key][cols]))
+        return self.to_tensors(out)
+
+    def to_tensors(self, out: dict) -> dict:
+        return TrainDataset.to_tensors(self, out)
+
+    @classmethod
+    def from_file(cls, vocab, vcfpath, panelpath, freqpath, typepath, poppath, pospath):
+        gt, pos, t2i, p2i, pos2i = _read_inputs(vcfpath, typepath, poppath, pospath)
+        return cls(vocab, gt, pos, PanelData.from_file(panelpath), np.load(freqpath), t2i, p2i, pos2i)

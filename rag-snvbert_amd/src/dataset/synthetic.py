@@ -180,3 +180,49 @@ def make_rag_dataset(n_samples: int = 8, n_sites: int = 512, n_windows: int = 2,
                                          {p: i for i, p in enumerate(POPS)},
                                          {int(p): i for i, p in enumerate(pos)}, ref, pos, name=name)
     return ds, vocab
+
+
+def make_infer_arrays(n_sites: int = 1300, n_samples: int = 3, n_ref_samples: int = 24, missing_rate: float = 0.3,
+                      ref_missing: int = 0, seed: int = 0) -> dict:
+    """In-memory imputation inputs with the reference's file contract (InferDataset.from_file,
+    dataset.py:747-771; the panel of embedding_rag_infer_dataset.py:56-69):
+
+      ori_pos / pos_to_idx  every panel site (Freq.npy columns), sorted positions;
+      pos, vcf              the target VCF: the sites kept with probability 1 - missing_rate,
+                            GT [n_target, n_samples, 2] copied from panel haplotypes + 2 % flips;
+      ref_gt, ref_pos       the reference panel [n_ref_sites, n_ref_samples, 2]; ``ref_missing``
+                            panel sites dropped from it (windows with unmatched sites);
+      freq                  [4, 6, n_sites] (REF, HET, HOM, AF x 5 populations + GLOBAL)."""
+    rng = np.random.default_rng([seed, 0x1F3A])
+    af = rng.beta(0.3, 3.0, n_sites).astype(np.float32)
+    ori_pos = np.sort(rng.choice(np.arange(1, 50 * n_sites), n_sites, replace=False)).astype(np.int64)
+    panel = (rng.random((n_sites, n_ref_samples, 2)) < af[:, None, None]).astype(np.int8)
+    src = rng.integers(0, n_ref_samples, size=(n_samples, 2))
+    full = np.stack([panel[:, src[:, 0], 0], panel[:, src[:, 1], 1]], -1)
+    full = (full ^ (rng.random(full.shape) < 0.02)).astype(np.int8)
+    keep = rng.random(n_sites) >= missing_rate
+    keep[0] = True                                       # a target VCF with at least one site
+    freq = np.zeros((4, 6, n_sites), np.float32)
+    for p in range(6):
+        ap = np.clip(af + (0.05 * rng.standard_normal(n_sites) if p < 5 else 0), 0, 1)
+        freq[0, p], freq[1, p], freq[2, p], freq[3, p] = (1 - ap) ** 2, 2 * ap * (1 - ap), ap ** 2, ap
+    ref_rows = np.arange(n_sites)
+    if ref_missing:
+        drop = rng.choice(np.arange(1, n_sites), ref_missing, replace=False)
+        ref_rows = np.setdiff1d(ref_rows, drop)
+    return dict(ori_pos=ori_pos, pos=ori_pos[keep], vcf=full[keep], freq=freq,
+                pops=[POPS[i % 5] for i in range(n_samples)], pop_to_idx={p: i for i, p in enumerate(POPS)},
+                pos_to_idx={int(p): i for i, p in enumerate(ori_pos)}, ref_gt=panel[ref_rows],
+                ref_pos=ori_pos[ref_rows], source=src)
+
+
+def make_infer_dataset(a: dict = None, index_window_len: int = 510, **kw):
+    """EmbeddingRAGInferDataset over ``make_infer_arrays`` data (or ``a``).  Returns (dataset, vocab)."""
+    from .embedding_rag_infer_dataset import EmbeddingRAGInferDataset
+    from .vocab import WordVocab
+    a = a if a is not None else make_infer_arrays(**kw)
+    vocab = WordVocab(POPS)
+    ds = EmbeddingRAGInferDataset.from_arrays(vocab, a["vcf"], a["pos"], a["pops"], a["freq"], a["pop_to_idx"],
+                                              a["pos_to_idx"], a["ref_gt"], a["ref_pos"],
+                                              index_window_len=index_window_len)
+    return ds, vocab

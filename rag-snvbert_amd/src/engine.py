@@ -191,6 +191,8 @@ class Engine:
                 t["ffn_v"] = K.ffn_vec(t["b1"], b2g, w2g, t["ln2_g"], t["ln2_b"])
                 t["qkv_ws"] = K.wsg_pack(t["w_qkv"])
                 t["o_ws"] = K.ffn_pre_pack(t["w_o"])
+                # the whole block tail (W_o' + W1 + W2') on 32x32 MFMAs (csrc/tail.hip)
+                t["tail_w"] = K.tail_pack(t["w_o"], t["w1"], w2g)
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:

@@ -1,21 +1,23 @@
 """v18 embedding-RAG imputation entry point (reference: src/infer_embedding_rag.py:53-257).
 
-Per batch (window-major order, WindowMajorSampler): retrieval on the HBM token index
-(exact int8-MFMA kNN, no FAISS, no host round trip), the native eval forward, then the
-reference's post-processing on the device (snvrag_infer_post: second softmax of the head
-probabilities, genotype products).  Results stay on the GPU until the end of the run;
-one device->host copy feeds the geometry step ([W, S, L] -> [W*L, S], slice [1, 1+window),
-fit to the variant count — infer_embedding_rag.py:166-203) and the writers.
+Data: ``EmbeddingRAGInferDataset`` (InferDataset items over the panel's full site list;
+the sites absent from the target are masked and imputed).  Per batch (window-major order,
+WindowMajorSampler): retrieval on the HBM token index (exact int8-MFMA kNN, no FAISS, no
+host round trip), the native eval forward, then the reference's post-processing on the
+device (snvrag_infer_post: second softmax of the head probabilities, genotype products).
+Results stay on the GPU until the end of the run; one device->host copy feeds the
+geometry step ([W, S, L] -> [W*L, S], slice [1, 1+window), fit to the panel's site count —
+infer_embedding_rag.py:166-203) and the writers.
 
 Outputs (``--output_path``): ``imputed.npz`` (hap1/hap2 ALT probabilities, GP, mask,
-positions) and ``imputed.vcf`` (GT phased at p > 0.5, DS = p1 + p2, GP = (p00, p01 + p10,
-p11), ``%.3f``).  The reference's VCF call fails with a TypeError, so the
+positions) and ``imputed.vcf`` (the imputed sites = mask of the first sample, as
+infer_embedding_rag.py:237; GT phased argmax, HDS, GP = (p00, p01 + p10, p11), DS,
+``%.3f``).  The reference's VCF call fails with a TypeError, so the
 writer here defines the output instead of mirroring it.
 
-Windows: the reference's query windows are INFER_WINDOW_LEN = 1020 sites while its FAISS
-index windows are 510 (embedding_rag_infer_dataset.py:16), misaligning index and query for
-w > 0.  Here index and query share the dataset's windows (aligned); ``--window_len``
-sets the slice length (1020, the reference's query geometry).
+Windows: query windows are INFER_WINDOW_LEN = 1020 sites; ``--index_window_len`` 510
+(default) reproduces the reference's 510-site index windows and infer masks
+(embedding_rag_infer_dataset.py:16), 1020 aligns them with the query windows.
 """
 
 from __future__ import annotations
@@ -47,11 +49,14 @@ def parse_args(argv=None):
     p.add_argument("--k_retrieve", type=int, default=1)
     p.add_argument("--cuda_devices", type=int, nargs="+", default=None)
     p.add_argument("--window_len", type=int, default=INFER_WINDOW_LEN)
+    p.add_argument("--index_window_len", type=int, default=510,
+                   help="510: the reference's index windows (compat); 1020: aligned with the query windows")
     p.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--synthetic", type=int, default=0, help="samples of in-memory synthetic data")
-    p.add_argument("--synthetic_windows", type=int, default=2)
-    p.add_argument("--synthetic_ref", type=int, default=256)
-    p.add_argument("--mask_rate", type=float, default=None, help="synthetic: fixed mask level 0.1..0.9 (C5 sweep)")
+    p.add_argument("--synthetic_sites", type=int, default=2040, help="synthetic: panel sites")
+    p.add_argument("--synthetic_ref", type=int, default=256, help="synthetic: panel samples")
+    p.add_argument("--mask_rate", type=float, default=0.3,
+                   help="synthetic: fraction of panel sites absent from the target (C5 sweep 0.1..0.9)")
     p.add_argument("--no_vcf", action="store_true")
     return p.parse_args(argv)
 
@@ -112,22 +117,52 @@ def write_vcf(path, chrom, pos, h1, h2, gt, samples, pos_flag=None, ref=None, al
 
 
 def build_dataset(args):
+    from .dataset.embedding_rag_infer_dataset import EmbeddingRAGInferDataset
+    from .dataset.vocab import WordVocab
     if not args.synthetic:
-        raise SystemExit("reading the reference's VCF/H5 inputs needs scikit-allel/h5py, absent in this image; "
-                         "run with --synthetic N (in-memory data with the same file contract)")
-    from .dataset.synthetic import make_rag_dataset
-    ds, vocab = make_rag_dataset(args.synthetic, args.window_len, args.synthetic_windows, args.synthetic_ref,
-                                 seed=11, name="infer")
-    if args.mask_rate is not None:
-        from .dataset.utils import sequence_padding
-        for w in range(ds.window_count):
-            n = ds.window_actual_lens[w]
-            rng = np.random.default_rng(1000 + w)
-            raw = (rng.random(n) < args.mask_rate).astype(np.int64)
-            ds.raw_window_masks[w] = raw
-            ds.window_masks[w] = sequence_padding(raw, "int")
-        ds.fixed_masks = True
-    return ds, vocab
+        from .dataset.dataset import PanelData
+        vocab = WordVocab(list(PanelData.from_file(args.infer_panel).pop_class_dict.keys()))
+        ds = EmbeddingRAGInferDataset.from_file(vocab, args.infer_dataset, args.infer_panel, args.freq_path,
+                                                args.type_path, args.pop_path, args.pos_path,
+                                                ref_vcf_path=args.ref_panel, window_len=args.window_len,
+                                                index_window_len=args.index_window_len)
+        return ds, vocab
+    from .dataset.synthetic import make_infer_arrays, make_infer_dataset
+    a = make_infer_arrays(args.synthetic_sites, args.synthetic, args.synthetic_ref, missing_rate=args.mask_rate,
+                          seed=11)
+    return make_infer_dataset(a, index_window_len=args.index_window_len)
+
+
+def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_len: int = INFER_WINDOW_LEN):
+    """The inference loop (infer_embedding_rag.py:132-157) and geometry (:165-203) over ``ds``
+    with an eval ``model`` on ``dev``.  Returns host arrays h1/h2 [n_sites, S], gt
+    [n_sites, S, 4], mask [n_sites, S], the neighbour indices per sampler row and the time."""
+    from .dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from .dataset.sampler import WindowMajorSampler
+    emb = model.bert.embedding
+    loader = torch.utils.data.DataLoader(ds, batch_size=batch_size, sampler=WindowMajorSampler(ds),
+                                         num_workers=num_workers, collate_fn=embedding_rag_collate_fn)
+    outs = {"h1": [], "h2": [], "gt": [], "mask": [], "idx1": [], "idx2": []}
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for batch in loader:
+            batch = ds.process_batch_retrieval(batch, emb, dev, k)
+            x = {key: (v.to(dev, non_blocking=True) if torch.is_tensor(v) else v) for key, v in batch.items()}
+            out = model(x)
+            p1, p2, gt = postprocess(out[0], out[1])
+            outs["h1"].append(p1)
+            outs["h2"].append(p2)
+            outs["gt"].append(gt)
+            outs["mask"].append(x["mask"])
+            outs["idx1"].append(x["rag_idx_h1"])
+            outs["idx2"].append(x["rag_idx_h2"])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    host = {key: torch.cat(v).cpu().numpy() for key, v in outs.items()}
+    h1, h2, gt, mask = geometry(host["h1"], host["h2"], host["gt"], host["mask"], ds.window_count,
+                                len(ds.ori_pos), window_len)
+    return dict(h1=h1, h2=h2, gt=gt, mask=mask, idx1=host["idx1"], idx2=host["idx2"], seconds=elapsed,
+                masked_snvs=int(host["mask"].sum()) * 2, batch_mask=host["mask"])
 
 
 def infer(argv=None):
@@ -136,8 +171,6 @@ def infer(argv=None):
         raise SystemExit("imputation runs on the MI355X kernels only (no CPU fallback)")
     dev = torch.device(f"cuda:{args.cuda_devices[0] if args.cuda_devices else torch.cuda.current_device()}")
     torch.cuda.set_device(dev)
-    from .dataset.embedding_rag_dataset import embedding_rag_collate_fn
-    from .dataset.sampler import WindowMajorSampler
     from .engine import engine_for
     from .model import build_model
     ds, vocab = build_dataset(args)
@@ -151,44 +184,18 @@ def infer(argv=None):
         model.load_state_dict(sd, strict=True)
     model = model.to(dev).eval()
     engine_for(model).set_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
-    emb = model.bert.embedding
-    loader = torch.utils.data.DataLoader(ds, batch_size=args.infer_batch_size, sampler=WindowMajorSampler(ds),
-                                         num_workers=args.num_workers, collate_fn=embedding_rag_collate_fn)
-    outs = {"h1": [], "h2": [], "gt": [], "mask": []}
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        for batch in loader:
-            if getattr(ds, "fixed_masks", False):     # C5 sweep: the window mask is the query mask
-                w = int(batch["window_idx"][0])
-                m = torch.from_numpy(np.asarray(ds.window_masks[w])).long()
-                batch["mask"] = m.expand_as(batch["hap_1"]).clone()
-                keep = batch["mask"] == 0
-                batch["hap_1"] = torch.where(keep, batch["hap_1"], torch.full_like(batch["hap_1"], 4))
-                batch["hap_2"] = torch.where(keep, batch["hap_2"], torch.full_like(batch["hap_2"], 4))
-            batch = ds.process_batch_retrieval(batch, emb, dev, args.k_retrieve)
-            x = {k: (v.to(dev, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
-            out = model(x)
-            p1, p2, gt = postprocess(out[0], out[1])
-            outs["h1"].append(p1)
-            outs["h2"].append(p2)
-            outs["gt"].append(gt)
-            outs["mask"].append(x["mask"])
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    host = {k: torch.cat(v).cpu().numpy() for k, v in outs.items()}
-    n_windows = ds.window_count
-    n_variants = len(ds.pos)
-    h1, h2, gt, mask = geometry(host["h1"], host["h2"], host["gt"], host["mask"], n_windows, n_variants,
-                                args.window_len)
+    res = run(ds, model, dev, args.infer_batch_size, args.k_retrieve, args.num_workers, args.window_len)
+    h1, h2, gt, mask = res["h1"], res["h2"], res["gt"], res["mask"]
     os.makedirs(args.output_path, exist_ok=True)
     np.savez_compressed(os.path.join(args.output_path, "imputed.npz"), hap1=h1, hap2=h2, gp=gt, mask=mask,
-                        pos=np.asarray(ds.pos))
+                        pos=np.asarray(ds.ori_pos))
     if not args.no_vcf:
         samples = [f"S{i}" for i in range(h1.shape[1])]
-        write_vcf(os.path.join(args.output_path, "imputed.vcf"), args.chrom, ds.pos, h1, h2, gt, samples)
-    masked = int(host["mask"].sum()) * 2
-    print(f"imputed {len(ds)} sample-windows in {elapsed:.2f}s ({masked / elapsed:.0f} masked SNVs/s)", flush=True)
-    return dict(h1=h1, h2=h2, gt=gt, mask=mask, seconds=elapsed, masked_snvs=masked)
+        write_vcf(os.path.join(args.output_path, "imputed.vcf"), args.chrom, ds.ori_pos, h1, h2, gt, samples,
+                  pos_flag=mask[:, 0].astype(bool))
+    print(f"imputed {len(ds)} sample-windows in {res['seconds']:.2f}s "
+          f"({res['masked_snvs'] / res['seconds']:.0f} masked SNVs/s)", flush=True)
+    return res
 
 
 if __name__ == "__main__":

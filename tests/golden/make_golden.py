@@ -290,6 +290,147 @@ def run_norag_case(name, d, layers, heads, B, n_sites, n_ref=8, level=4, seed=0,
     print(f"{name}: digest={digest}")
 
 
+class _FlatL2:
+    """Stand-in for ``faiss.IndexFlatL2`` (faiss is not installed here): the published
+    semantics of that index — exact brute-force k-NN on squared L2 over the added rows —
+    evaluated in float64, ties to the lower row id.  Every search is logged."""
+    log: list = []
+
+    def __init__(self, d):
+        self.d, self.xb = d, np.zeros((0, d), np.float32)
+
+    def add(self, x):
+        self.xb = np.concatenate([self.xb, np.asarray(x, np.float32)])
+
+    def search(self, q, k):
+        xb = self.xb.astype(np.float64)
+        dist = np.stack([((xb - r.astype(np.float64)[None]) ** 2).sum(1) for r in np.asarray(q)])
+        idx = np.arange(xb.shape[0])
+        I = np.stack([np.lexsort((idx, d)) for d in dist])[:, :k].astype(np.int64)
+        _FlatL2.log.append((I, dist))
+        return np.take_along_axis(dist, I, 1).astype(np.float32), I
+
+
+def _faiss_standin():
+    store = {}
+    return SimpleNamespace(IndexFlatL2=_FlatL2, StandardGpuResources=lambda: None,
+                           write_index=lambda index, path: store.__setitem__(path, index),
+                           read_index=lambda path: store[path], index_cpu_to_gpu=lambda res, dev, index: index)
+
+
+def run_infer_case(name, d, layers, heads, n_sites, n_samples, n_ref_samples, k, batch_size, seed=0,
+                   ref_missing=2, compact=False):
+    """The reference imputation path end to end on synthetic arrays: InferDataset
+    (dataset.py:629-900), EmbeddingRAGInferDataset (embedding_rag_infer_dataset.py:20-324:
+    510-site index windows, infer masks, panel embeddings, process_batch_retrieval) with the
+    FAISS stand-in above, WindowMajorSampler + embedding_rag_collate_fn, and the inference
+    loop + geometry statements of infer_embedding_rag.py:129-203 executed as written."""
+    import os
+    import tempfile
+    import time
+    from typing import Dict, List, Optional
+    from torch.utils.data import DataLoader, Dataset
+    torch.set_num_threads(8)
+    vocab = ref_vocab()
+    model, digest = build_model(d, layers, heads, len(vocab), seed)
+    a = synthetic.make_infer_arrays(n_sites, n_samples, n_ref_samples, missing_rate=0.3, ref_missing=ref_missing,
+                                    seed=seed + 5)
+    vpm = SimpleNamespace(sequence_padding=seq_pad, position_normalize=pos_norm)
+    glb = dict(NP_GLB, Dataset=Dataset, math=math, INFER_WINDOW_LEN=1020, REF=0, HET=1, HOM=2, AF=3, GLOBAL=5,
+               VCFProcessingModule=vpm, WordVocab=WordVocabRef)
+    RefInfer = ref_classes("src/dataset/dataset.py", ["InferDataset"], glb)["InferDataset"]
+    glb2 = dict(NP_GLB, InferDataset=RefInfer, faiss=_faiss_standin(), os=os, time=time, tqdm=lambda it, **kw: it,
+                VCFProcessingModule=vpm, INFER_WINDOW_LEN=510, Dict=Dict, List=List, Optional=Optional)
+    RefRAGInfer = ref_classes("src/dataset/embedding_rag_infer_dataset.py", ["EmbeddingRAGInferDataset"],
+                              glb2)["EmbeddingRAGInferDataset"]
+    collate = ref_function("src/dataset/embedding_rag_dataset.py", None, "embedding_rag_collate_fn", NP_GLB)
+
+    class _Infer(RefRAGInfer):                     # the panel arrays instead of an h5/VCF file
+        def _load_ref_data(self, ref_vcf_path):
+            return a["ref_gt"], a["ref_pos"]
+
+    emb = model.bert.embedding
+    panel = SimpleNamespace(pop_list=np.array(a["pops"]))
+    cwd = os.getcwd()
+    _FlatL2.log.clear()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)                              # the reference writes its index dir relative to the CWD
+        try:
+            ds = _Infer(vocab, a["vcf"], a["pos"], panel, a["freq"], {}, a["pop_to_idx"], a["pos_to_idx"],
+                        ref_vcf_path="panel", embedding_layer=emb, build_ref_data=True, build_index=True)
+        finally:
+            os.chdir(cwd)
+        n_index_searches = len(_FlatL2.log)
+        items = [ds[i] for i in range(len(ds))]
+        order = list(iter(WindowMajorSampler(ds)))
+        batches = []
+        loader = DataLoader(ds, batch_size=batch_size, sampler=WindowMajorSampler(ds), collate_fn=collate)
+
+        class _Rec:                                # model(batch) with its outputs kept
+            def __init__(self, m):
+                self.m, self.bert, self.outs = m, m.bert, []
+
+            def __call__(self, b):
+                batches.append({key: (v.clone() if torch.is_tensor(v) else v) for key, v in b.items()})
+                o = self.m(b)
+                self.outs.append(o)
+                return o
+        rec = _Rec(model)
+        text, tree = _source(REF / "src/infer_embedding_rag.py")
+        fn = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "infer")
+        body = [n for n in fn.body if 129 <= n.lineno <= 203]
+        lines = text.splitlines()
+        src = textwrap.dedent("\n".join(lines[body[0].lineno - 1:body[-1].end_lineno]))
+        ns = dict(NP_GLB, infer_data_loader=loader, device=torch.device("cpu"), infer_dataset=ds,
+                  embedding_layer=emb, args=SimpleNamespace(k_retrieve=k), model=rec, tqdm=lambda it, **kw: it,
+                  time=time, INFER_WINDOW_LEN=1020)
+        exec(compile(src, "src/infer_embedding_rag.py:129-203", "exec"), ns)
+    # neighbours per query haplotype, in sampler order (process_batch_retrieval groups each batch by
+    # window in first-appearance order and searches h1 then h2 per group, :256-285)
+    log = _FlatL2.log[n_index_searches:]
+    I1 = np.zeros((len(order), k), np.int64)
+    I2 = np.zeros_like(I1)
+    D1 = np.zeros((len(order), n_ref_samples * 2))
+    D2 = np.zeros_like(D1)
+    row = 0
+    for b in batches:
+        groups = defaultdict(list)
+        for i, w in enumerate(b["window_idx"]):
+            groups[int(w)].append(i)
+        for w, rows in groups.items():
+            (i1, d1), (i2, d2) = log.pop(0), log.pop(0)
+            for j, r in enumerate(rows):
+                I1[row + r], I2[row + r], D1[row + r], D2[row + r] = i1[j], i2[j], d1[j], d2[j]
+        row += len(b["window_idx"])
+    probs1 = np.concatenate([o[0].detach().numpy() for o in rec.outs])
+    probs2 = np.concatenate([o[1].detach().numpy() for o in rec.outs])
+    res = dict(cfg=np.array(json.dumps(dict(d=d, layers=layers, heads=heads, vocab=len(vocab), k=k, seed=seed,
+                                              batch_size=batch_size, n_samples=n_samples, index_window_len=510,
+                                              window_len=1020, sd_digest=digest, pops=a["pops"]))),
+               ori_pos=a["ori_pos"], pos=a["pos"], vcf=a["vcf"], freq=a["freq"], ref_gt=a["ref_gt"],
+               ref_pos=a["ref_pos"], order=np.array(order),
+               infer_masks=np.stack(ds.infer_masks).astype(np.int8),
+               ref_tokens_complete=np.stack(ds.ref_tokens_complete).astype(np.int8),
+               ref_af_windows=np.stack(ds.ref_af_windows).astype(np.float32),
+               I_h1=I1, I_h2=I2, kth_margin_h1=_kth_margin(D1, k), kth_margin_h2=_kth_margin(D2, k),
+               batch_probs_h1=probs1, batch_probs_h2=probs2,
+               hap1=ns["hap1"], hap2=ns["hap2"], gt=ns["gt"], mask=ns["mask"])
+    if compact:
+        # batch-size case: keep the inputs, the neighbours and the imputed haplotype
+        # probabilities (float16); GP follows from them (checked on the full case)
+        for key in ("batch_probs_h1", "batch_probs_h2", "gt", "ref_tokens_complete"):
+            res.pop(key)
+        res["hap1"], res["hap2"] = res["hap1"].astype(np.float16), res["hap2"].astype(np.float16)
+        res["mask"] = res["mask"].astype(np.int8)
+    else:
+        for key in ("hap_1", "hap_2", "mask", "af", "af_p", "pos", "ref", "het", "hom", "window_idx", "sample_idx",
+                    "start_idx", "end_idx"):
+            res[f"item_{key}"] = np.stack([np.asarray(it[key]) for it in items])
+    np.savez_compressed(OUT / f"{name}.npz", **res)
+    print(f"{name}: digest={digest} items={len(items)} windows={ds.window_count} "
+          f"min kth margin h1={res['kth_margin_h1'].min():.3g} h2={res['kth_margin_h2'].min():.3g}")
+
+
 def _kth_margin(dist, k):
     s = np.sort(dist, 1)
     return (s[:, k] - s[:, k - 1]) if s.shape[1] > k else np.full(s.shape[0], np.inf)
@@ -329,7 +470,7 @@ def masks_fixture():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag"]
+    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag", "infer", "infer256"]
     if "data" in which:
         masks_fixture()
     if "tiny" in which:
@@ -341,3 +482,10 @@ if __name__ == "__main__":
         run_case("fwd_full", d=384, layers=12, heads=12, B=2, n_sites=1020, n_ref=64, k=4, seed=2)
     if "norag" in which:
         run_norag_case("fwd_norag", d=128, layers=2, heads=4, B=3, n_sites=128, seed=4)
+    if "infer" in which:
+        run_infer_case("infer_c5", d=64, layers=2, heads=4, n_sites=1300, n_samples=3, n_ref_samples=24, k=2,
+                       batch_size=4, seed=6)
+    if "infer256" in which:
+        # C5 geometry: one batch of 256 sample-windows spanning both windows
+        run_infer_case("infer_c5_b256", d=64, layers=2, heads=4, n_sites=1300, n_samples=128, n_ref_samples=24,
+                       k=2, batch_size=256, seed=7, compact=True)

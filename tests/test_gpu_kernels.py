@@ -348,6 +348,51 @@ def test_block_tail_fused_kernel(D, M):
     assert (out.double() - two.double()).abs().mean() < 5e-3
 
 
+@pytest.mark.parametrize("D,M", [(384, 777), (384, 128 * 3), (128, 300), (256, 1), (256, 129),
+                                 (384, 4 * 1030 + 5), (384, 64 * 1030)])
+def test_tail32_kernel(D, M):
+    """32x32-MFMA block tail (csrc/tail.hip, the engine's default bf16 path): both entry points
+    (snvrag_tail_forward = W_o' + LN1 + FFN + LN2 in place; snvrag_tail_ffn_forward = FFN + LN2)
+    vs float64 torch on the same bf16 operands and vs the 16x16 kernel (csrc/ffn.hip).  Ragged M
+    (row tails of 1, 1 + 128 k, 5) and 515 workgroups (every chunk rotation of the stream)."""
+    g = torch.Generator(device="cpu").manual_seed(7 * D + M)
+    bf, F = torch.bfloat16, torch.nn.functional
+    x = torch.randn(M, D, generator=g).to(DEV, bf)
+    att = (0.5 * torch.randn(M, D, generator=g)).to(DEV, bf)
+    w_o = (torch.randn(D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    b_o = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    g1, be1 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w1 = (torch.randn(4 * D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    w2 = (torch.randn(D, 4 * D, generator=g) / math.sqrt(4 * D)).to(DEV)
+    b1, b2 = torch.randn(4 * D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    gf, bff = (1 + 0.2 * torch.randn(4 * D, generator=g)).to(DEV), (0.1 * torch.randn(4 * D, generator=g)).to(DEV)
+    g2, be2 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w2g, b2g, _ = K().fold_layernorm(w2, b2, gf, bff, bf)
+    vec = K().ffn_vec(b1, b2g, w2g, g2, be2)
+    ts = K().tail_pack(w_o, w1, w2g)
+
+    def ffn_ref(x1):
+        h = F.leaky_relu(x1 @ w1.double().T + b1.double(), 0.1)
+        hn = F.layer_norm(h, (4 * D,), gf.double(), bff.double(), 1e-5)
+        f = F.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
+        return F.layer_norm(x1 + f, (D,), g2.double(), be2.double(), 1e-5)
+
+    x1 = F.layer_norm(x.double() + att.double() @ w_o.double().T + b_o.double(), (D,), g1.double(), be1.double(), 1e-5)
+    ref = ffn_ref(x1)
+    old = K().block_tail_forward(att, x.clone(), K().ffn_pre_pack(w_o), b_o, g1, be1, K().ffn_pack(w1, w2g), vec)
+    # FFN-only entry on the same x (not in place)
+    o2 = K().tail_ffn_forward(x, ts, vec)
+    r2 = ffn_ref(x.double())
+    torch.testing.assert_close(o2.double(), r2, rtol=5e-2, atol=5e-2)
+    assert (o2.double() - r2).abs().mean() < 1e-2
+    out = K().tail_forward(att, x, ts, b_o, g1, be1, vec)
+    assert out.data_ptr() == x.data_ptr()
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.double(), ref, rtol=5e-2, atol=5e-2)
+    assert (out.double() - ref).abs().mean() < 1e-2
+    assert (out.double() - old.double()).abs().mean() < 5e-3
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_encoder_fused_equals_unfused(dt, monkeypatch):
     """Encoder stack with LN fused into GEMM epilogues/prologues == the 8-launch unfused stack."""

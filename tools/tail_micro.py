@@ -88,6 +88,7 @@ for name, fn, fl in (
         ("tail.hip PRE", tail_var(0), fl9),
         ("tail.hip PRE PF=8", tail_var(1), fl9),
         ("tail.hip PRE no-DMA (diag)", tail_var(2), fl9),
+        ("tail.hip PRE no sched groups", tail_var(3), fl9),
         ("ffn.hip FFN only", lambda: K.ffn_forward(c["x"], ws, c["vec"], out=out), fl8),
         ("tail.hip FFN only", lambda: (os.environ.__setitem__("SNVRAG_TAIL_VARIANT", "0"),
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
