@@ -54,6 +54,9 @@ def parse():
                    help="steps of the same batch on the exact-f32 path (bf16-vs-f32 call agreement); 0 = skip")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on host cores (rank 0)")
     p.add_argument("--cpu-panel", type=int, default=65536, help="panel sample for the CPU kNN timing")
+    p.add_argument("--panel", default="sharded", choices=["sharded", "replicated"],
+                   help="N>1: each rank holds 1/N of the panel and serves every rank's queries (SURVEY §8e), "
+                        "or every rank holds the whole panel")
     p.add_argument("--train-steps", type=int, default=3,
                    help="timed DDP training steps at configs[1] (B=24/GPU, window 1020, k=8, 10k-haplotype panel); 0 = skip")
     return p.parse_args()
@@ -88,12 +91,14 @@ def make_queries(args, af_np, seed, rank):
     return alle, src
 
 
-def build_workload(args, dev, vocab, rank=0, seed=1234):
+def build_workload(args, dev, vocab, rank=0, seed=1234, shard=None):
     """configs[2] workload: one window of ``args.window`` sites, an ``args.n_ref``-haplotype panel
-    generated on the device (HBM-resident), ``args.batch`` query samples copied from panel rows with
-    2 % flips, AF-guided masks at ``args.level``.  Shared by the bench and the launch-shape kNN
-    parity test (tests/test_gpu_knn_scale.py)."""
+    generated on the device (HBM-resident; with ``shard`` only this rank's contiguous range of
+    it), ``args.batch`` query samples copied from panel rows with 2 % flips, AF-guided masks at
+    ``args.level``.  Shared by the bench and the launch-shape kNN parity test
+    (tests/test_gpu_knn_scale.py)."""
     from types import SimpleNamespace
+    from src import kernels as K
     from src.dataset import utils as U
     from src.retrieval import PanelIndex
     S, B, L = args.window, args.batch, 1030
@@ -102,7 +107,12 @@ def build_workload(args, dev, vocab, rank=0, seed=1234):
     pos = np.sort(rng.choice(np.arange(1, 50 * S), S, replace=False))
     af_dev = torch.from_numpy(af_np).to(dev)
     ref_af = U.sequence_padding(af_np, "float").astype(np.float32)
-    index = PanelIndex.synthetic(args.n_ref, S, af_dev, torch.from_numpy(ref_af).to(dev), seed)
+    if shard is None:
+        index = PanelIndex.synthetic(args.n_ref, S, af_dev, torch.from_numpy(ref_af).to(dev), seed)
+    else:
+        r0, r1 = shard.bounds(args.n_ref)
+        index = PanelIndex(K.panel_synth(r1 - r0, S, af_dev, seed, row0=r0), S, torch.from_numpy(ref_af).to(dev),
+                           ref_offset=r0, n_total=args.n_ref)
     raw_mask = U.af_guided_mask(af_np, args.level, 0, 0)
     mask = U.sequence_padding(raw_mask, "int")
     alle, src = make_queries(args, af_np, seed, rank)
@@ -116,8 +126,24 @@ def build_workload(args, dev, vocab, rank=0, seed=1234):
     site_mask = torch.from_numpy(raw_mask.astype(np.uint8)).to(dev)
     tok = torch.cat([x["hap_1"], x["hap_2"]]).contiguous()
     return SimpleNamespace(index=index, x=x, site_mask=site_mask, tok=tok, raw_mask=raw_mask, af_np=af_np,
-                           ref_af=ref_af, alle=alle, src=src, S=S, B=B, L=L,
+                           ref_af=ref_af, alle=alle, src=src, S=S, B=B, L=L, shard=shard,
                            masked_per_step=2 * B * int(raw_mask.sum()))
+
+
+def make_search(wl, eng, k):
+    """The exact kNN of the step's 2B query haplotypes -> (idx [2B, k], counts or None).
+    Sharded panel: the collective search of src/retrieval/shards.py (every rank's queries
+    against every shard; the neighbours' alt-allele counts come back all-reduced)."""
+    P = eng.packed()
+    if wl.shard is None:
+        return lambda: (wl.index.search(wl.tok, P.W, wl.site_mask, k)[0], None)
+    from src.retrieval.shards import kernel_ops, sharded_neighbours
+    ops = kernel_ops(wl.index, P.W, wl.site_mask, k)
+
+    def search():
+        idx, _, counts = sharded_neighbours(wl.tok, k, ops, None, wl.shard.group)
+        return idx, counts
+    return search
 
 
 def make_step(wl, eng, k):
@@ -127,11 +153,12 @@ def make_step(wl, eng, k):
     P = eng.packed()
     Ar = eng.af_embedding(torch.from_numpy(wl.ref_af).to(wl.tok.device)[None]).float()[0].contiguous()
     B, L, D = wl.B, wl.L, P.D
+    search = make_search(wl, eng, k)
 
     def step():
-        idx, _ = wl.index.search(wl.tok, P.W, wl.site_mask, k)
+        idx, counts = search()
         block = torch.empty(4 * B, L, D, device=wl.tok.device, dtype=eng.dtype)
-        K.rag_mean(idx, wl.index.codes, wl.S, P.W, P.pe, Ar, L, eng.dtype, out=block[2 * B:])
+        K.rag_mean(idx, wl.index.codes, wl.S, P.W, P.pe, Ar, L, eng.dtype, out=block[2 * B:], counts=counts)
         wl.x["rag_block"] = block
         return eng.forward(wl.x)
     return step
@@ -156,7 +183,11 @@ def main():
     P = eng.packed()
 
     # ---- window, panel (HBM-resident, generated on device), queries ----
-    wl = build_workload(args, dev, vocab, rank)
+    shard = None
+    if world > 1 and args.panel == "sharded":
+        from src.retrieval.shards import PanelShard
+        shard = PanelShard.current()
+    wl = build_workload(args, dev, vocab, rank, shard=shard)
     S, B, L = wl.S, wl.B, wl.L
     index, x, tok, site_mask = wl.index, wl.x, wl.tok, wl.site_mask
     af_np, ref_af, raw_mask = wl.af_np, wl.ref_af, wl.raw_mask
@@ -187,9 +218,10 @@ def main():
     kinds, ms, work = kinds[:n], ms[:n], work[:n]
     # the whole kNN search (LUT + pre-pass + scan + merges + decode) alone, outside the timed region
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    search = make_search(wl, eng, k)
     ev0.record()
     for _ in range(5):
-        index.search(tok, P.W, site_mask, k)
+        search()
     ev1.record()
     torch.cuda.synchronize()
     knn_ms = ev0.elapsed_time(ev1) / 5
@@ -272,7 +304,8 @@ def main():
                                   "above ~150 queries the scan is int8-MFMA/LDS bound, see knn_hbm_probe"),
             "knn_hbm_probe": dict(probe, bound="hbm", peak=HBM_PEAK_GBS),
             "knn_search_ms": round(knn_ms, 4),
-            "knn_search_queries_per_s": round(2 * B / (knn_ms * 1e-3), 1),
+            # (sharded panel: the search serves every rank's queries in that time)
+            "knn_search_queries_per_s": round(2 * B * (world if shard is not None else 1) / (knn_ms * 1e-3), 1),
             "gemm": dict(achieved_tflops=round(gemm["rate"] / 1e12, 2), frac=round(gemm["rate"] / 1e12 / peak_f, 4),
                          ms_per_step=round(gemm["total_ms_per_step"], 3), launches_per_step=gemm["launches_per_step"]),
             "ffn_fused": (dict(achieved_tflops=round(ffn["rate"] / 1e12, 2), frac=round(ffn["rate"] / 1e12 / peak_f, 4),
@@ -294,7 +327,8 @@ def main():
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded AF~Beta(0.3,3) panel + copied queries)",
         "config": {"workload": "configs[2]: v18 embedding-RAG imputation, window=1024 sites (L=1030 tokens), "
                                f"k={k}, {args.n_ref}-haplotype panel resident in HBM, d{args.dims}/L{args.layers}/H{args.heads}",
-                   "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (panel replicated)"},
+                   "global_batch": B * world, "seq_len": L, "parallelism": (f"dp{world} + panel sharded {world}-way" if shard is not None
+                                                  else f"dp{world} (panel replicated)")},
         "roofline": roofline, "cpu_baseline": cpu, **extra, "precision_parity": precision, "train": train,
     }
     print(json.dumps(line))

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 11
+#define SNVRAG_ABI_VERSION 12
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -216,10 +216,28 @@ int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, cons
                     const float* W, const float* pe, const float* Ar,
                     int tok0, int tok1, int sos, int eos, int pad, void* out, void* stream);
 
+/* Sharded panel (replaces the reference's single-process gather of the
+ * neighbours' complete tokens, embedding_rag_dataset.py:404-442 / _infer_dataset.py:287-322):
+ * the neighbour mean needs only the per-site alt-allele COUNT over the k neighbours.
+ * snvrag_neighbor_counts: counts[q][s] = sum_j codes[idx[q][j] - row0][s] over the
+ *   neighbours a shard owns (global idx in [row0, row0 + n_rows)); u8 [nq][ld_out],
+ *   ld and ld_out multiples of 16, ld_out >= ld.  The shards' partials add up (all-reduce).
+ * snvrag_rag_mean_counts: snvrag_rag_mean with those counts ([nq][ld_counts]) in place of
+ *   the panel rows; idx gives the valid-neighbour count per query. */
+int snvrag_neighbor_counts(int64_t nq, int k, const int64_t* idx, const uint8_t* codes, int64_t ld,
+                           int64_t row0, int64_t n_rows, uint8_t* counts, int64_t ld_out, void* stream);
+int snvrag_rag_mean_counts(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                           const uint8_t* counts, int64_t ld_counts, int32_t n_sites,
+                           const float* W, const float* pe, const float* Ar,
+                           int tok0, int tok1, int sos, int eos, int pad, void* out, void* stream);
+
 /* Deterministic synthetic panel on device: code = (u(seed,r,s) < af[s]), u = splitmix64
- * hash (src/dataset/synthetic.py hash_uniform), zero padding to ld. */
+ * hash (src/dataset/synthetic.py hash_uniform), zero padding to ld.  _rows: rows
+ * [row0, row0 + n_rows) of that panel (a shard). */
 int snvrag_panel_synth(uint8_t* codes, int64_t n_ref, int64_t ld, int32_t n_sites,
                        const float* af, uint64_t seed, void* stream);
+int snvrag_panel_synth_rows(uint8_t* codes, int64_t row0, int64_t n_rows, int64_t ld, int32_t n_sites,
+                            const float* af, uint64_t seed, void* stream);
 
 /* ------------------------------------------------------------------------
  * Encoder stack (model/transformer.py:27-30 x n_layers, model/bert.py:213-217),

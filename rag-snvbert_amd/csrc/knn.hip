@@ -399,7 +399,10 @@ __global__ void decode_kernel(const uint64_t* __restrict__ keys, int nq, int k, 
 // (neighbour indices staged in LDS first), so no load waits on another.
 constexpr int RM_P = 8, RM_Q = 16, RM_KMAX = 128;
 
-template <typename T>
+// CNT: `codes` holds per-query alt-allele counts over the k neighbours ([nq][ld], the
+// sharded-panel form, see neighbor_counts_kernel) instead of panel rows indexed by idx;
+// idx still gives the number of valid neighbours.
+template <typename T, bool CNT = false>
 __global__ __launch_bounds__(256) void rag_mean_kernel(int nq, int L, int D, int k, const int64_t* __restrict__ idx,
                                                        const uint8_t* __restrict__ codes, long ld, int n_sites,
                                                        const float* __restrict__ W, const float* __restrict__ pe,
@@ -422,8 +425,9 @@ __global__ __launch_bounds__(256) void rag_mean_kernel(int nq, int L, int D, int
     for (int j = 0; j < k; ++j) {
       const int64_t r = sidx[qq * k + j];
       nv += r >= 0;
-      c += (r >= 0 && site) ? codes[r * ld + (l - 1)] : 0;
+      if constexpr (!CNT) c += (r >= 0 && site) ? codes[r * ld + (l - 1)] : 0;
     }
+    if constexpr (CNT) c = (site && q0 + qq < nq) ? codes[(long)(q0 + qq) * ld + (l - 1)] : 0;
     frac[qq][p] = nv > 0 ? (float)c / (float)nv : 0.f;
     if (p == 0) nvalid[qq] = nv;
   }
@@ -473,8 +477,32 @@ __device__ __forceinline__ double hash_u01(uint64_t seed, uint64_t r, uint64_t c
   return (double)(x >> 40) / (double)(1 << 24);
 }
 
+// Alt-allele counts over the neighbours a panel SHARD owns: counts[q][s] = sum over j of
+// codes[idx[q][j] - row0][s] for the idx[q][j] in [row0, row0 + n_rows) (global indices).
+// One thread per (query, 16-site chunk); the shards' partial counts sum (all-reduce) to the
+// full count, which rag_mean_kernel<T, true> turns into the neighbour mean.
+__global__ __launch_bounds__(256) void neighbor_counts_kernel(int nq, int k, const int64_t* __restrict__ idx,
+                                                              const uint8_t* __restrict__ codes, long ld,
+                                                              long row0, long n_rows, uint8_t* __restrict__ counts,
+                                                              long ld_out) {
+  const long chunks = ld_out / 16;
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)nq * chunks) return;
+  const int q = (int)(id / chunks);
+  const int c0 = (int)(id % chunks) * 16;
+  uint32_t acc[4] = {0, 0, 0, 0};                    // 16 byte counters (k <= 128: no carries)
+  for (int j = 0; j < k; ++j) {
+    const long r = idx[(long)q * k + j] - row0;
+    if (r < 0 || r >= n_rows || c0 >= ld) continue;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(codes + r * ld + c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += v[i];      // codes are 0/1 bytes: packed byte adds
+  }
+  *reinterpret_cast<u32x4*>(counts + (long)q * ld_out + c0) = u32x4{acc[0], acc[1], acc[2], acc[3]};
+}
+
 __global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long ld, int n_sites,
-                                   const float* __restrict__ af, uint64_t seed) {
+                                   const float* __restrict__ af, uint64_t seed, long row0) {
   const long chunks_per_row = ld / 16;
   const long total = n_ref * chunks_per_row;
   for (long id = (long)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (long)gridDim.x * blockDim.x) {
@@ -484,7 +512,7 @@ __global__ void panel_synth_kernel(uint8_t* __restrict__ codes, long n_ref, long
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int s = c0 + j;
-      v[j] = (s < n_sites && hash_u01(seed, (uint64_t)r, (uint64_t)s) < (double)af[s]) ? 1 : 0;
+      v[j] = (s < n_sites && hash_u01(seed, (uint64_t)(r + row0), (uint64_t)s) < (double)af[s]) ? 1 : 0;
     }
     *reinterpret_cast<u32x4*>(codes + r * ld + c0) = *reinterpret_cast<u32x4*>(v);
   }
@@ -968,34 +996,71 @@ extern "C" int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const 
   return 0;
 }
 
-extern "C" int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
-                               const uint8_t* codes, int64_t ld_codes, int32_t n_sites, const float* W,
-                               const float* pe, const float* Ar, int tok0, int tok1, int sos, int eos, int pad,
-                               void* out, void* stream) {
+template <bool CNT>
+static int rag_mean_launch(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                           const uint8_t* codes, int64_t ld_codes, int32_t n_sites, const float* W, const float* pe,
+                           const float* Ar, int tok0, int tok1, int sos, int eos, int pad, void* out, void* stream) {
   SNV_CHECK_ARG(idx && codes && W && pe && out, "null pointer");
   SNV_CHECK_ARG(D % 8 == 0 && n_sites + 2 <= L, "shape");
   if (nq == 0) return 0;
   SNV_CHECK_ARG(k >= 1 && k <= RM_KMAX, "k must be in [1, 128]");
+  SNV_CHECK_ARG(!CNT || ld_codes >= n_sites, "counts row shorter than the window");
   dim3 g((unsigned)cdiv(L, RM_P), (unsigned)cdiv(nq, RM_Q));
   hipStream_t s = as_stream(stream);
   if (dtype_out == SNVRAG_BF16)
-    hipLaunchKernelGGL(rag_mean_kernel<bf16>, g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes, (long)ld_codes,
-                       n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (bf16*)out);
+    hipLaunchKernelGGL((rag_mean_kernel<bf16, CNT>), g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes,
+                       (long)ld_codes, n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (bf16*)out);
   else
-    hipLaunchKernelGGL(rag_mean_kernel<float>, g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes, (long)ld_codes,
-                       n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (float*)out);
+    hipLaunchKernelGGL((rag_mean_kernel<float, CNT>), g, dim3(256), 0, s, (int)nq, (int)L, (int)D, k, idx, codes,
+                       (long)ld_codes, n_sites, W, pe, Ar, tok0, tok1, sos, eos, pad, (float*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_rag_mean(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                               const uint8_t* codes, int64_t ld_codes, int32_t n_sites, const float* W,
+                               const float* pe, const float* Ar, int tok0, int tok1, int sos, int eos, int pad,
+                               void* out, void* stream) {
+  return rag_mean_launch<false>(dtype_out, nq, L, D, k, idx, codes, ld_codes, n_sites, W, pe, Ar, tok0, tok1, sos,
+                                eos, pad, out, stream);
+}
+
+extern "C" int snvrag_rag_mean_counts(int dtype_out, int64_t nq, int64_t L, int64_t D, int k, const int64_t* idx,
+                                      const uint8_t* counts, int64_t ld_counts, int32_t n_sites, const float* W,
+                                      const float* pe, const float* Ar, int tok0, int tok1, int sos, int eos, int pad,
+                                      void* out, void* stream) {
+  return rag_mean_launch<true>(dtype_out, nq, L, D, k, idx, counts, ld_counts, n_sites, W, pe, Ar, tok0, tok1, sos,
+                               eos, pad, out, stream);
+}
+
+extern "C" int snvrag_neighbor_counts(int64_t nq, int k, const int64_t* idx, const uint8_t* codes, int64_t ld,
+                                      int64_t row0, int64_t n_rows, uint8_t* counts, int64_t ld_out, void* stream) {
+  SNV_CHECK_ARG(idx && counts && (codes || n_rows == 0), "null pointer");
+  SNV_CHECK_ARG(k >= 1 && k <= RM_KMAX, "k must be in [1, 128]");
+  SNV_CHECK_ARG(ld % 16 == 0 && ld_out % 16 == 0 && ld_out >= ld && ((uintptr_t)counts % 16) == 0 &&
+                    ((uintptr_t)codes % 16) == 0,
+                "rows must be 16-byte multiples, counts row >= codes row");
+  if (nq == 0) return 0;
+  const long work = nq * (ld_out / 16);
+  hipLaunchKernelGGL(neighbor_counts_kernel, dim3((unsigned)cdiv(work, 256)), dim3(256), 0, as_stream(stream),
+                     (int)nq, k, idx, codes, (long)ld, (long)row0, (long)n_rows, counts, (long)ld_out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_panel_synth_rows(uint8_t* codes, int64_t row0, int64_t n_rows, int64_t ld, int32_t n_sites,
+                                       const float* af, uint64_t seed, void* stream) {
+  SNV_CHECK_ARG(codes && af && ld % 16 == 0 && ld >= n_sites && row0 >= 0, "bad args");
+  if (n_rows == 0) return 0;
+  const long work = n_rows * (ld / 16);
+  const int grid = (int)std::min<long>(cdiv(work, 256), 65536);
+  hipLaunchKernelGGL(panel_synth_kernel, dim3(grid), dim3(256), 0, as_stream(stream), codes, (long)n_rows, (long)ld,
+                     n_sites, af, seed, (long)row0);
   SNV_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" int snvrag_panel_synth(uint8_t* codes, int64_t n_ref, int64_t ld, int32_t n_sites, const float* af,
                                   uint64_t seed, void* stream) {
-  SNV_CHECK_ARG(codes && af && ld % 16 == 0 && ld >= n_sites, "bad args");
-  if (n_ref == 0) return 0;
-  const long work = n_ref * (ld / 16);
-  const int grid = (int)std::min<long>(cdiv(work, 256), 65536);
-  hipLaunchKernelGGL(panel_synth_kernel, dim3(grid), dim3(256), 0, as_stream(stream), codes, (long)n_ref, (long)ld,
-                     n_sites, af, seed);
-  SNV_LAUNCH_CHECK();
-  return 0;
+  return snvrag_panel_synth_rows(codes, 0, n_ref, ld, n_sites, af, seed, stream);
 }

@@ -207,13 +207,16 @@ def focal_loss(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, ga
 
 class _RagMean(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos):
+    def forward(ctx, W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos, counts):
         out = K.rag_mean(idx, codes, n_sites, W.detach().float().contiguous(), pe, Ar.detach().float().contiguous(),
-                         L, torch.bfloat16, tok0=tok0, tok1=tok1, sos=sos, eos=eos)
+                         L, torch.bfloat16, tok0=tok0, tok1=tok1, sos=sos, eos=eos, counts=counts)
         valid = idx >= 0
         nv = valid.sum(1)
-        al = codes[idx.clamp(min=0)][:, :, :n_sites].float() * valid[:, :, None]
-        frac = al.sum(1) / nv.clamp(min=1)[:, None]                         # [nq, n_sites]
+        if counts is not None:
+            al = counts[:, :n_sites].float()
+        else:
+            al = (codes[idx.clamp(min=0)][:, :, :n_sites].float() * valid[:, :, None]).sum(1)
+        frac = al / nv.clamp(min=1)[:, None]                                 # [nq, n_sites]
         ctx.save_for_backward(frac, (nv > 0).float())
         ctx.meta = (n_sites, W.shape, tok0, tok1, sos, eos)
         return out
@@ -232,10 +235,12 @@ class _RagMean(torch.autograd.Function):
             gW[eos] += G[:, n + 1].sum(0)
         # <pad> positions: nn.Embedding(padding_idx=0) accumulates no gradient
         gAr = G.sum(0)
-        return gW, gAr, None, None, None, None, None, None, None, None, None
+        return gW, gAr, None, None, None, None, None, None, None, None, None, None
 
 
 def rag_mean_train(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, codes: torch.Tensor, n_sites: int,
-                   pe: torch.Tensor, L: int, tok0: int = 5, tok1: int = 6, sos: int = 2, eos: int = 3) -> torch.Tensor:
-    """[nq, L, D] bf16 mean of the k neighbours' complete-token embeddings, differentiable in W and Ar."""
-    return _RagMean.apply(W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos)
+                   pe: torch.Tensor, L: int, tok0: int = 5, tok1: int = 6, sos: int = 2, eos: int = 3,
+                   counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[nq, L, D] bf16 mean of the k neighbours' complete-token embeddings, differentiable in W and Ar
+    (``counts``: the neighbours' per-site alt-allele counts, sharded panels)."""
+    return _RagMean.apply(W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos, counts)

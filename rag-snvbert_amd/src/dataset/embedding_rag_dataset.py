@@ -129,11 +129,32 @@ class EmbeddingRAGDataset(TrainDataset):
         return self.to_tensors(out)
 
     # ------------------------------------------------------------- retrieval --
+    panel_shard = None
+
+    def set_panel_shard(self, shard) -> None:
+        """Hold only this rank's contiguous haplotype range of every window's panel
+        (``retrieval.shards.PanelShard``; None = the whole panel).  process_batch_retrieval
+        then runs the collective search — every rank must call it for every batch.
+
+        A query's distances must not depend on which shard scores them, so every rank takes
+        rank 0's window masks here (the construction-time masks come from the unseeded
+        global RNG, embedding_rag_dataset.py:160-170; ``regenerate_masks(seed)`` is seeded
+        and stays identical across ranks)."""
+        self.panel_shard = shard
+        self._index_cache.clear()
+        if shard is not None:
+            import torch.distributed as dist
+            obj = [self.raw_window_masks if shard.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=shard.group)
+            self.raw_window_masks = [np.asarray(m) for m in obj[0]]
+            self.window_masks = [sequence_padding(m, "int") for m in self.raw_window_masks]
+            self.mask_version += 1
+
     def panel_index(self, w: int, device) -> "object":
         from ..retrieval import PanelIndex
         idx = self._index_cache.get(w)
         if idx is None or idx.codes.device != torch.device(device):
-            idx = PanelIndex.from_alleles(self.ref_alleles[w], self.ref_af_windows[w], device)
+            idx = panel_index_of(self.ref_alleles[w], self.ref_af_windows[w], device, self.panel_shard)
             self._index_cache[w] = idx
             while sum(i.nbytes for i in self._index_cache.values()) > self._index_cache_bytes and \
                     len(self._index_cache) > 1:
@@ -155,9 +176,23 @@ class EmbeddingRAGDataset(TrainDataset):
                    ref_gt=ref_gt, ref_pos=ref_pos, embedding_layer=embedding_layer, name=name)
 
 
+def panel_index_of(alleles: np.ndarray, ref_af: np.ndarray, device, shard=None):
+    """PanelIndex of one window's panel, or of this rank's contiguous range of it."""
+    from ..retrieval import PanelIndex
+    if shard is None:
+        return PanelIndex.from_alleles(alleles, ref_af, device)
+    r0, r1 = shard.bounds(alleles.shape[0])
+    return PanelIndex.from_alleles(alleles[r0:r1], ref_af, device, ref_offset=r0, n_total=alleles.shape[0])
+
+
 def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.ndarray],
              dense: bool = False, limbs: int = 2) -> dict:
-    """Shared retrieval body of the train/val and infer datasets (see module docstring)."""
+    """Shared retrieval body of the train/val and infer datasets (see module docstring).
+
+    With ``ds.panel_shard`` set (multi-rank) each rank's index holds its own
+    contiguous haplotype range and every window step runs the collective search of
+    ``retrieval/shards.py`` over the union of the ranks' batch windows; the neighbour
+    means then come from the all-reduced per-site alt-allele counts."""
     from ..engine import engine_for
     from .. import kernels as K
     eng = engine_for(embedding_layer)
@@ -172,12 +207,18 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     groups = defaultdict(list)
     for i, w in enumerate(batch["window_idx"]):
         groups[int(w)].append(i)
+    shard = getattr(ds, "panel_shard", None)
+    windows = list(groups)
+    if shard is not None:
+        from ..retrieval.shards import batch_windows
+        windows = batch_windows(windows, shard.group)
     # eval: the neighbour means land directly in rows [2B:] of the encoder's input block
     block = None if train else eng.input_block(B, L, dev)
     rag_mean = None if train else block[2 * B:]
     rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
     rag_groups = []
-    for w, rows in groups.items():
+    for w in windows:
+        rows = groups.get(w, [])
         index = ds.panel_index(w, dev)
         rows_t = torch.tensor(rows, device=dev, dtype=torch.long)
         tok = torch.cat([h1[rows_t], h2[rows_t]], 0).contiguous()
@@ -188,23 +229,35 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         # windows built from one freq table); otherwise pass both AF embeddings (exact LUT form).
         afw = af[rows_t]
         same = bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw)))
+        counts = None
         with torch.no_grad():
             Ar_emb = eng.af_embedding(ref_af.unsqueeze(0), True).float()[0].contiguous() \
                 if P.af is not None else None
-            Aq = Ar = None
-            if not same and P.af is not None:
-                Aq = eng.af_embedding(afw, True).float().contiguous()
-                Ar = Ar_emb
-            idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
+            if shard is not None:
+                from ..retrieval.shards import any_rank, kernel_ops, sharded_neighbours
+                exact = P.af is not None and any_rank(not same, dev, shard.group)
+                ops = kernel_ops(index, P.W, site_mask, k, limbs,
+                                 aq_fn=lambda a: eng.af_embedding(a, True).float().contiguous(),
+                                 Ar=Ar_emb if exact else None)
+                idx, _, counts = sharded_neighbours(tok, k, ops, torch.cat([afw, afw]) if exact else None,
+                                                    shard.group)
+            else:
+                Aq = Ar = None
+                if not same and P.af is not None:
+                    Aq = eng.af_embedding(afw, True).float().contiguous()
+                    Ar = Ar_emb
+                idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
         nb = len(rows)
+        if nb == 0:
+            continue
         if train:
             # the model re-encodes the neighbours WITH grad (train_forward.neighbour_means)
-            rag_groups.append((rows_t, idx[:nb], idx[nb:], index))
+            rag_groups.append((rows_t, idx[:nb], idx[nb:], index, counts))
         else:
             if nb == B and rows == list(range(B)):      # one window, batch order: no scatter
-                K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, out=rag_mean)
+                K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, out=rag_mean, counts=counts)
             else:
-                means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype)
+                means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, counts=counts)
                 rag_mean[rows_t] = means[:nb]
                 rag_mean[rows_t + B] = means[nb:]
         rag_idx[rows_t] = idx[:nb]

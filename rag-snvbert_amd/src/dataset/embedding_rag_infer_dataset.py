@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from .dataset import INFER_WINDOW_LEN, InferDataset, PanelData
-from .embedding_rag_dataset import retrieve
+from .embedding_rag_dataset import panel_index_of, retrieve
 from .utils import MAX_SEQ_LEN, sequence_padding
 
 REFERENCE_INDEX_WINDOW = 510     # embedding_rag_infer_dataset.py:16
@@ -113,11 +113,17 @@ class EmbeddingRAGInferDataset(InferDataset):
             self.ref_alleles.append(alleles.astype(np.int64))
             self.ref_tokens_complete.append(self.tokenize(alleles, np.zeros(MAX_SEQ_LEN, np.int64)))
 
+    panel_shard = None
+
+    def set_panel_shard(self, shard) -> None:
+        """See EmbeddingRAGDataset.set_panel_shard (the infer masks are deterministic: no sync)."""
+        self.panel_shard = shard
+        self._index_cache.clear()
+
     def panel_index(self, w: int, device) -> "object":
-        from ..retrieval import PanelIndex
         idx = self._index_cache.get(w)
         if idx is None or idx.codes.device != torch.device(device):
-            idx = PanelIndex.from_alleles(self.ref_alleles[w], self.ref_af_windows[w], device)
+            idx = panel_index_of(self.ref_alleles[w], self.ref_af_windows[w], device, self.panel_shard)
             self._index_cache[w] = idx
             while sum(i.nbytes for i in self._index_cache.values()) > self._index_cache_bytes and \
                     len(self._index_cache) > 1:

@@ -363,25 +363,49 @@ def knn_decode(keys: torch.Tensor, exps: Optional[torch.Tensor] = None, consts: 
 
 def rag_mean(idx: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor, pe: torch.Tensor,
              Ar: Optional[torch.Tensor], L: int, dtype: torch.dtype, tok0=5, tok1=6, sos=2, eos=3, pad=0,
-             out: Optional[torch.Tensor] = None):
+             out: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None):
     """[nq, L, D] mean over the k neighbours of their complete-token embeddings; ``out`` (e.g. the
-    rag half of the encoder's input block) is written in place."""
+    rag half of the encoder's input block) is written in place.  ``counts`` (u8 [nq, ld], the
+    per-site alt-allele counts over the neighbours, see ``neighbor_counts``) replaces the panel
+    rows ``codes[idx]`` (sharded panels; ``codes`` is then unused)."""
     nq, k = idx.shape
     D = W.shape[1]
     if out is None:
         out = torch.empty(nq, L, D, device=idx.device, dtype=dtype)
     assert out.dtype == dtype and tuple(out.shape) == (nq, L, D) and out.is_contiguous()
+    if counts is not None:
+        assert counts.dtype == torch.uint8 and counts.shape[0] == nq
+        check(N.lib().snvrag_rag_mean_counts(_dt(dtype), nq, L, D, k, ptr(_c(idx)), ptr(_c(counts)), counts.shape[1],
+                                             n_sites, ptr(_c(W)), ptr(_c(pe)), ptr(Ar), tok0, tok1, sos, eos, pad,
+                                             ptr(out), stream_ptr()), "rag_mean_counts")
+        return out
     check(N.lib().snvrag_rag_mean(_dt(dtype), nq, L, D, k, ptr(_c(idx)), ptr(_c(codes)), codes.shape[1], n_sites,
                                   ptr(_c(W)), ptr(_c(pe)), ptr(Ar), tok0, tok1, sos, eos, pad, ptr(out),
                                   stream_ptr()), "rag_mean")
     return out
 
 
-def panel_synth(n_ref: int, n_sites: int, af: torch.Tensor, seed: int, ld: Optional[int] = None) -> torch.Tensor:
+def neighbor_counts(idx: torch.Tensor, codes: torch.Tensor, row0: int, ld_out: Optional[int] = None,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """u8 [nq, ld_out]: per-site alt-allele counts over the neighbours ``idx`` (global, int64
+    [nq, k]) that fall in this shard's rows [row0, row0 + codes.shape[0])."""
+    nq, k = idx.shape
+    n_rows, ld = codes.shape
+    ld_out = ld_out or ld
+    if out is None:
+        out = torch.empty(nq, ld_out, device=idx.device, dtype=torch.uint8)
+    check(N.lib().snvrag_neighbor_counts(nq, k, ptr(_c(idx)), ptr(_c(codes)), ld, row0, n_rows, ptr(out), ld_out,
+                                         stream_ptr()), "neighbor_counts")
+    return out
+
+
+def panel_synth(n_ref: int, n_sites: int, af: torch.Tensor, seed: int, ld: Optional[int] = None,
+                row0: int = 0) -> torch.Tensor:
+    """Rows [row0, row0 + n_ref) of the hash-generated synthetic panel (u8 [n_ref, ld])."""
     N.require_gpu(af)
     ld = ld or max(256, ((n_sites + 255) // 256) * 256)
     codes = torch.empty(n_ref, ld, device=af.device, dtype=torch.uint8)
-    check(N.lib().snvrag_panel_synth(ptr(codes), n_ref, ld, n_sites, ptr(_c(af)), seed, stream_ptr()),
+    check(N.lib().snvrag_panel_synth_rows(ptr(codes), row0, n_ref, ld, n_sites, ptr(_c(af)), seed, stream_ptr()),
           "panel_synth")
     return codes
 

@@ -53,6 +53,9 @@ def parse_args(argv=None):
     p.add_argument("--synthetic_windows", type=int, default=2)
     p.add_argument("--synthetic_ref", type=int, default=256, help="panel samples (2 haplotypes each)")
     p.add_argument("--max_steps", type=int, default=0)
+    p.add_argument("--panel", default="sharded", choices=["sharded", "replicated"],
+                   help="DDP: each rank holds 1/world of every window's panel and serves every rank's "
+                        "queries (SURVEY §8e), or every rank holds the whole panel")
     p.add_argument("--seed", type=int, default=0)
     return p.parse_args(argv)
 
@@ -76,6 +79,10 @@ def build_data(args, rank: int, world: int):
     if world > 1:
         ts = DistributedWindowSampler(train, rank, world, shuffle=True, seed=42)
         vs = DistributedWindowSampler(val, rank, world, shuffle=False)
+        if args.panel == "sharded":
+            from .retrieval.shards import PanelShard
+            for ds in (train, val):
+                ds.set_panel_shard(PanelShard.current())
     else:
         ts, vs = WindowGroupedSampler(train, shuffle=True, seed=42), WindowGroupedSampler(val, shuffle=False)
     return mk(train, ts, args.train_batch_size), mk(val, vs, args.val_batch_size), vocab

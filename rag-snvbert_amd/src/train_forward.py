@@ -160,11 +160,13 @@ def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
     pe = emb.position.pe[0, :L].float().contiguous()
     rows_out: List[torch.Tensor] = []
     vals: List[torch.Tensor] = []
-    for rows, idx_h1, idx_h2, index in groups:
+    for rows, idx_h1, idx_h2, index, *cnt in groups:
         Ar = af_embedding(emb.af_embedding, index.ref_af.view(1, -1))[0].float() if emb.use_af else \
             torch.zeros(L, D, device=pe.device)
         idx = torch.cat([idx_h1, idx_h2], 0)
-        m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L)
+        # (sharded panel: the all-reduced alt-allele counts of the neighbours, retrieval/shards.py)
+        counts = cnt[0] if cnt else None
+        m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, counts=counts)
         nb = rows.numel()
         rows_out += [rows, rows + B]
         vals += [m[:nb], m[nb:]]

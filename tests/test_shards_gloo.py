@@ -1,8 +1,11 @@
-"""World-size-2 gloo test of the sharded kNN exchange: each rank owns a
-contiguous range of the panel, computes its exact local top-k with GLOBAL indices, the
-partial key lists are all-gathered and merged — the result must equal the single-shard
-canonical top-k bit for bit.  The local top-k and the merge are the oracle's here (CPU);
-on the GPU the same exchange runs with knn_scan/topk_merge over RCCL."""
+"""World-size-2 gloo tests of the sharded retrieval (src/retrieval/shards.py):
+each rank owns a contiguous range of the panel, computes its exact local top-k with GLOBAL
+indices, the partial key lists are all-gathered and merged, and the neighbours' per-site
+alt-allele counts are all-reduced — results must equal the single-shard canonical top-k
+and the full-panel counts bit for bit.  The product plumbing (``sharded_neighbours``,
+``all_gather_rows`` with ragged per-rank query counts, ``batch_windows``) runs as shipped;
+only its compute steps (LUT + scan, merge, decode, counts) are the oracle's on the CPU —
+on the GPU the same plumbing drives knn_scan / topk_merge / neighbor_counts over RCCL."""
 
 import os
 import socket
@@ -74,3 +77,94 @@ def test_sharded_topk_equals_single_shard_world2():
         assert p.exitcode == 0
     for r in range(2):
         np.testing.assert_array_equal(got[r], want)
+
+
+# ---------------------------------------------------------------------------- product plumbing
+def _plumbing_case(seed=5, n_ref=203, n_sites=80, k=6):
+    rng = np.random.default_rng(seed)
+    codes = (rng.random((n_ref, n_sites)) < 0.25).astype(np.uint8)
+    codes[:10] = codes[50:60]                          # ties across the shard boundary
+    W = rng.standard_normal((11, 16)).astype(np.float32)
+    site_mask = (rng.random(n_sites) < 0.3).astype(np.uint8)
+    L = n_sites + 2
+    toks = []
+    for nq in (5, 3):                                  # ragged: rank 0 has 5 queries, rank 1 has 3
+        t = np.zeros((nq, L), np.int64)
+        t[:, 0], t[:, -1] = 2, 3
+        src = codes[rng.integers(0, n_ref, nq)] ^ (rng.random((nq, n_sites)) < 0.05)
+        t[:, 1:-1] = np.where(site_mask[None] == 1, 4, 5 + src)
+        toks.append(t)
+    return codes, W, site_mask, toks, k
+
+
+def _oracle_ops(codes_local, r0, W, site_mask, k):
+    from src.retrieval.shards import ShardOps
+
+    def keys(tok_all, af_all):
+        assert af_all is None
+        dq, e = knn_np.quantize_lut(knn_np.lut_delta(W, tok_all.numpy(), None, site_mask), 2)
+        return torch.from_numpy(_local_keys(codes_local, dq, k, r0).view(np.int64)), torch.from_numpy(e), None
+
+    def merge(g, kk):
+        return torch.from_numpy(knn_np.merge_partials(g.numpy().view(np.uint64), kk).view(np.int64))
+
+    def decode(keys, exps, consts):
+        kk = keys.numpy().view(np.uint64)
+        idx = (kk & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        d = (kk >> np.uint64(32)).astype(np.int64) - (1 << 30)
+        return torch.from_numpy(idx), torch.from_numpy(d.astype(np.float32))
+
+    def counts(idx):
+        i = idx.numpy() - r0
+        own = (i >= 0) & (i < codes_local.shape[0])
+        c = np.zeros((i.shape[0], codes_local.shape[1]), np.uint8)
+        for q in range(i.shape[0]):
+            for j in range(i.shape[1]):
+                if own[q, j]:
+                    c[q] += codes_local[i[q, j]]
+        return torch.from_numpy(c)
+
+    return ShardOps(keys=keys, merge=merge, decode=decode, counts=counts)
+
+
+def _plumbing_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
+        from src.retrieval.shards import PanelShard, batch_windows, sharded_neighbours
+        codes, W, site_mask, toks, k = _plumbing_case()
+        shard = PanelShard.current()
+        r0, r1 = shard.bounds(codes.shape[0])
+        ops = _oracle_ops(codes[r0:r1], r0, W, site_mask, k)
+        idx, d, cnt = sharded_neighbours(torch.from_numpy(toks[rank]), k, ops, None, shard.group)
+        wins = batch_windows([3, 1] if rank == 0 else [1, 4], shard.group)
+        q.put((rank, idx.numpy().copy(), cnt.numpy().copy(), wins))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_sharded_neighbours_product_plumbing_world2():
+    codes, W, site_mask, toks, k = _plumbing_case()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_plumbing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in ps:
+        r, idx, cnt, wins = q.get(timeout=100)
+        got[r] = (idx, cnt, wins)
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    for r in range(2):
+        dq, _ = knn_np.quantize_lut(knn_np.lut_delta(W, toks[r], None, site_mask), 2)
+        want_i, _ = knn_np.knn(codes, dq, k)
+        idx, cnt, wins = got[r]
+        np.testing.assert_array_equal(idx, want_i)
+        np.testing.assert_array_equal(cnt, codes[want_i].sum(1).astype(np.uint8))
+        assert wins == [1, 3, 4]
