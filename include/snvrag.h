@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 12
+#define SNVRAG_ABI_VERSION 13
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -230,6 +230,16 @@ int snvrag_rag_mean_counts(int dtype_out, int64_t nq, int64_t L, int64_t D, int 
                            const uint8_t* counts, int64_t ld_counts, int32_t n_sites,
                            const float* W, const float* pe, const float* Ar,
                            int tok0, int tok1, int sos, int eos, int pad, void* out, void* stream);
+
+/* Raw-genotype window index (build_ref_db_l2.py:15-98: faiss.IndexFlatL2 over each
+ * sample's flattened (window_len, 2) 0/1 genotypes; test_faiss_intersect.py:171-181 the
+ * Hamming twin).  Squared L2 on 0/1 vectors = Hamming distance: rows bit-packed 32
+ * genotypes per word, word-major codes_wm[nw][N]; queries [nq][nw].  Writes
+ * snvrag_hamming_list_count() sorted top-k key lists per query, lists[n_lists][nq][k]
+ * (key = (d + 2^30) << 32 | row), to be merged by snvrag_topk_merge.  k <= 32, nw <= 2048. */
+int snvrag_hamming_lists(int64_t nq, int64_t N, int32_t nw, int k, const uint32_t* codes_wm,
+                         const uint32_t* queries, uint64_t* lists, void* stream);
+int32_t snvrag_hamming_list_count(void);
 
 /* Deterministic synthetic panel on device: code = (u(seed,r,s) < af[s]), u = splitmix64
  * hash (src/dataset/synthetic.py hash_uniform), zero padding to ld.  _rows: rows

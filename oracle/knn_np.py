@@ -118,3 +118,12 @@ def pack_key(d, idx):
     """uint64 key = ((D + 2^30) << 32) | idx (knn.hip ``make_key``); sorts as (D, idx)."""
     return ((np.asarray(d, np.int64) + (1 << 30)).astype(np.uint64) << np.uint64(32)) | \
         np.asarray(idx, np.int64).astype(np.uint64)
+
+
+def raw_genotype_knn(ref_rows, query_rows, k):
+    """ORACLE of the raw-genotype window index (build_ref_db_l2.py:86-89 IndexFlatL2 over the
+    flattened 0/1 genotypes): exact squared L2 = Hamming count, (D, idx)-ascending top-k."""
+    R = np.asarray(ref_rows, np.int64)
+    Q = np.asarray(query_rows, np.int64)
+    D = (Q[:, None, :] != R[None, :, :]).sum(-1)
+    return topk_exact(D, k)

@@ -8,7 +8,8 @@ Drop-in surface:
     (model/bert.py:176-179); here the K-mean is produced directly by the
     ``rag_mean`` kernel as [B, 1, L, D] — the model consumes it identically
     (bert.py:180-182) — and ``rag_idx_h1/h2`` [B, k] carry the neighbour indices.
-    ``dense=True`` restores the [B, k, L, D] layout for callers that need it.
+    ``dense=True`` returns the reference's fp32 [B, k, L, D] neighbour embeddings
+    (eval; the model's mean over k then equals the K-mean path).
   * ``regenerate_masks(seed)``, ``clear_jit_cache()``, ``add_level()``,
     ``window_masks``, ``ref_tokens_complete``, ``ref_af_windows``, ``jit_cache_win_idx``.
 
@@ -217,6 +218,7 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     rag_mean = None if train else block[2 * B:]
     rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
     rag_groups = []
+    dense_out = None
     for w in windows:
         rows = groups.get(w, [])
         index = ds.panel_index(w, dev)
@@ -260,6 +262,18 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                 means = K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, counts=counts)
                 rag_mean[rows_t] = means[:nb]
                 rag_mean[rows_t + B] = means[nb:]
+        if dense and not train:
+            # the reference's [B, k, L, D] fp32 neighbour embeddings (:425-442): every (query,
+            # neighbour) pair as a one-neighbour "mean" in one launch
+            if shard is not None:
+                raise NotImplementedError("dense neighbour embeddings need the neighbours' panel rows; "
+                                          "a sharded panel returns their counts only")
+            if dense_out is None:
+                dense_out = torch.zeros(2 * B, k, L, D, device=dev, dtype=torch.float32)
+            e = K.rag_mean(idx.reshape(-1, 1), index.codes, n, P.W, P.pe, Ar_emb, L, torch.float32)
+            e = e.view(2 * nb, k, L, D)
+            dense_out[rows_t] = e[:nb]
+            dense_out[rows_t + B] = e[nb:]
         rag_idx[rows_t] = idx[:nb]
         rag_idx[rows_t + B] = idx[nb:]
     batch["rag_idx_h1"], batch["rag_idx_h2"] = rag_idx[:B], rag_idx[B:]
@@ -267,10 +281,10 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         batch["rag_groups"] = rag_groups
         return batch
     if dense:
-        raise NotImplementedError("dense [B,k,L,D] neighbour embeddings: use rag_idx_* with "
-                                  "BERTEmbedding on the retrieved complete tokens")
-    batch["rag_emb_h1"] = rag_mean[:B].unsqueeze(1)
-    batch["rag_emb_h2"] = rag_mean[B:].unsqueeze(1)
+        batch["rag_emb_h1"], batch["rag_emb_h2"] = dense_out[:B], dense_out[B:]
+    else:
+        batch["rag_emb_h1"] = rag_mean[:B].unsqueeze(1)
+        batch["rag_emb_h2"] = rag_mean[B:].unsqueeze(1)
     batch["rag_mean"] = rag_mean
     batch["rag_block"] = block
     return batch

@@ -399,6 +399,19 @@ def neighbor_counts(idx: torch.Tensor, codes: torch.Tensor, row0: int, ld_out: O
     return out
 
 
+def hamming_topk(codes_wm: torch.Tensor, queries: torch.Tensor, k: int) -> torch.Tensor:
+    """Exact top-k keys [nq, k] ((d + 2^30) << 32 | row, (d, row) order) of bit-packed 0/1 rows
+    (word-major int32 [nw, N]) for bit-packed queries (int32 [nq, nw]); d = Hamming distance."""
+    nw, n = codes_wm.shape
+    nq = queries.shape[0]
+    assert queries.shape[1] == nw and codes_wm.dtype == torch.int32 and queries.dtype == torch.int32
+    n_lists = int(N.lib().snvrag_hamming_list_count())
+    lists = torch.empty(n_lists, nq, k, device=queries.device, dtype=torch.int64)
+    check(N.lib().snvrag_hamming_lists(nq, n, nw, k, ptr(_c(codes_wm)), ptr(_c(queries)), ptr(lists),
+                                       stream_ptr()), "hamming_lists")
+    return topk_merge(lists, k)
+
+
 def panel_synth(n_ref: int, n_sites: int, af: torch.Tensor, seed: int, ld: Optional[int] = None,
                 row0: int = 0) -> torch.Tensor:
     """Rows [row0, row0 + n_ref) of the hash-generated synthetic panel (u8 [n_ref, ld])."""

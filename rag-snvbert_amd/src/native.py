@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -103,6 +103,8 @@ _SIGS = {
     "snvrag_rag_mean": ([C.c_int, i64, i64, i64, C.c_int, vp, vp, i64, i32, vp, vp, vp, C.c_int, C.c_int,
                          C.c_int, C.c_int, C.c_int, vp, vp], C.c_int),
     "snvrag_panel_synth": ([vp, i64, i64, i32, vp, C.c_uint64, vp], C.c_int),
+    "snvrag_hamming_lists": ([i64, i64, i32, C.c_int, vp, vp, vp, vp], C.c_int),
+    "snvrag_hamming_list_count": ([], i32),
     "snvrag_panel_synth_rows": ([vp, i64, i64, i64, i32, vp, C.c_uint64, vp], C.c_int),
     "snvrag_neighbor_counts": ([i64, C.c_int, vp, vp, i64, i64, i64, vp, i64, vp], C.c_int),
     "snvrag_rag_mean_counts": ([C.c_int, i64, i64, i64, C.c_int, vp, vp, i64, i32, vp, vp, vp, C.c_int, C.c_int,

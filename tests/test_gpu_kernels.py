@@ -515,3 +515,25 @@ def test_weight_streaming_head2(M, Kd):
     logits, probs = K().wsg_head2(x, K().wsg_pack(w), N, b, w2, b2, want_logits=True)
     torch.testing.assert_close(logits, ref_l, rtol=1e-3, atol=2e-3)
     torch.testing.assert_close(probs, torch.softmax(ref_l, -1), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,bits,k,nq", [(5008, 2040, 32, 37), (300, 33, 5, 3), (20, 1020, 32, 4)])
+def test_raw_genotype_index_vs_oracle(n, bits, k, nq):
+    """Raw-genotype window index (csrc/rawdb.hip + topk_merge; build_ref_db_l2.py:86-89 IndexFlatL2
+    semantics): exact (D, row) top-k vs the oracle, incl. duplicated rows (ties), a panel smaller
+    than k (faiss pads with -1) and a row width that is not a multiple of 32 bits."""
+    from oracle import knn_np
+    from src.retrieval.raw_index import RawGenotypeIndex, pack_rows
+    rng = np.random.default_rng(n + bits)
+    R = (rng.random((n, bits)) < 0.2).astype(np.uint8)
+    if n > 40:
+        R[17] = R[5]
+    Q = np.concatenate([R[[5]], (rng.random((nq - 1, bits)) < 0.2).astype(np.uint8)])
+    idx = RawGenotypeIndex(pack_rows(R), bits, DEV)
+    D, I = idx.search(Q, k)
+    oi, od = knn_np.raw_genotype_knn(R, Q, k)
+    kk = min(k, n)
+    np.testing.assert_array_equal(I[:, :kk], oi[:, :kk])
+    np.testing.assert_array_equal(D[:, :kk], od[:, :kk].astype(np.float32))
+    if n < k:
+        assert (I[:, n:] == -1).all() and np.isinf(D[:, n:]).all()
