@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 13
+#define SNVRAG_ABI_VERSION 15
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -280,6 +280,9 @@ typedef struct {
    * the whole block tail runs on the 32x32-MFMA kernel (snvrag_tail_forward); takes
    * precedence over o_ws / ffn_w */
   const void* tail_w;
+  /* optional (bf16, D in {128,256,384}): snvrag_proj_pack of w_qkv (NC = 3) -> the QKV
+   * projection runs on snvrag_proj_forward; takes precedence over qkv_ws */
+  const void* qkv_pw;
 } snvrag_layer_t;
 
 /* ------------------------------------------------------------------------
@@ -327,6 +330,14 @@ int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, const void* 
                         const float* ln1_g, const float* ln1_b, const float* ffn_vec, float eps, void* stream);
 int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
                             const float* ffn_vec, float eps, void* stream);
+/* Projection on the same 32x32-MFMA stream machinery (the QKV projection of
+ * multi_head_attention.py:44-46, bf16): out[M, NC*D] = x[M, D] W^T + bias with W [NC*D, D]
+ * packed once by snvrag_proj_pack (snvrag_proj_pack_bytes(D, NC) bytes); D in {128, 256,
+ * 384}, NC in {1, 3}; bias f32 [NC*D]. */
+size_t snvrag_proj_pack_bytes(int D, int NC);
+int snvrag_proj_pack(int D, int NC, const void* w, void* out, void* stream);
+int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, const void* wstream, const float* bias,
+                        void* out, void* stream);
 
 /* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
  * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either

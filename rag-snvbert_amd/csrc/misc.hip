@@ -18,11 +18,11 @@ static EvLog g_ev;
 
 bool evlog_on() { return g_ev.on && g_ev.n < g_ev.cap; }
 void evlog_begin(hipStream_t s) {
-  if (evlog_on()) hipEventRecord(g_ev.ev[2 * g_ev.n], s);
+  if (evlog_on()) (void)hipEventRecord(g_ev.ev[2 * g_ev.n], s);
 }
 void evlog_end(hipStream_t s, int kind, double work) {
   if (!evlog_on()) return;
-  hipEventRecord(g_ev.ev[2 * g_ev.n + 1], s);
+  (void)hipEventRecord(g_ev.ev[2 * g_ev.n + 1], s);
   g_ev.kind[g_ev.n] = kind;
   g_ev.work[g_ev.n] = work;
   g_ev.n++;
@@ -104,7 +104,7 @@ extern "C" int snvrag_device_info(int device, char* name, int name_len) {
 
 extern "C" int snvrag_evlog_enable(int capacity) {
   if (g_ev.ev) {
-    for (int i = 0; i < 2 * g_ev.cap; ++i) hipEventDestroy(g_ev.ev[i]);
+    for (int i = 0; i < 2 * g_ev.cap; ++i) (void)hipEventDestroy(g_ev.ev[i]);
     delete[] g_ev.ev; delete[] g_ev.kind; delete[] g_ev.work;
     g_ev = EvLog{};
   }

@@ -118,11 +118,15 @@ struct TailArgs {
 // VAR (diagnostics): 0 default; 1 = no weight DMA after the prologue (compute-side ceiling;
 // results are garbage).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
 // SNVRAG_TAIL_VARIANT (launch_tail): 1 = PF 8, 2 = VAR 1, 3 = no schedule groups.
-template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0, bool TL_SGB = true>
+// NC > 0: projection mode (snvrag_proj_forward): out[M, NC*D] = act W^T + b over NC output
+// chunks of D features (the QKV projection: NC = 3), the same stream / ring / read machinery.
+template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0, bool TL_SGB = true, int NC = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void tail_kernel(TailArgs p) {
   using S = TailShape<D>;
   constexpr int NT = S::NT, KS = S::KS;
+  constexpr bool PROJ = NC > 0;
+  static_assert(!(PROJ && PRE), "modes");
   constexpr int NSLAB = (PRE ? S::NPRE : 0) + S::NCH * S::SPC;      // slabs consumed by this launch
   constexpr int RING = TL_NSLOT * TL_SLAB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -139,22 +143,23 @@ void tail_kernel(TailArgs p) {
   // as B fragments (k-step s: features tail_in_feat(s, hh, 0..7)); the residual rows of PRE are
   // loaded after the weight prologue (below) and only needed at LN1, so their HBM burst runs
   // under the out-projection MFMAs
-  for (int i = tid; i < 4 * D; i += 256) sv[i] = p.vec[i];
+  for (int i = tid; i < (PROJ ? NC : 4) * D; i += 256) sv[i] = p.vec[i];
   if constexpr (PRE)
     for (int i = tid; i < D; i += 256) { sv[4 * D + i] = p.g1[i]; sv[5 * D + i] = p.be1[i]; sv[6 * D + i] = p.b_o[i]; }
   u32x4 xr[KS];                                      // x1 B fragments (PRE: produced by LN1)
-  u32x4 xa[PRE ? KS : 1];                            // PRE: att B fragments
+  u32x4 xa[(PRE || PROJ) ? KS : 1];                  // PRE: att B fragments; PROJ: x
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     // (default cache policy: non-temporal activation loads/stores measured 8 % slower)
     const u32x4 v = *reinterpret_cast<const u32x4*>(p.act + rc * D + tail_in_feat(s, hh, 0));
-    if constexpr (PRE) xa[s] = v; else xr[s] = v;
+    if constexpr (PRE || PROJ) xa[s] = v; else xr[s] = v;
   }
 
   // ---- weight stream: buffer_load ... lds with scalar offsets; chunks rotated per workgroup
-  const int rot = (int)(blockIdx.x % S::NCH);
+  const int rot = (int)(blockIdx.x % (PROJ ? NC : S::NCH));
+  constexpr int STREAM_SLABS = PROJ ? NC * S::NPRE : S::NSLAB;
   const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, S::NSLAB * TL_SLAB, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, STREAM_SLABS * TL_SLAB, 0x00020000);
   const int voff = lane * 16;
   // FFN block order (software pipeline, see the chunk loop): with the stream's blocks
   // B(2c) = W1(c), B(2c+1) = W2'(c) (H slabs each) and r = rot, block s of the launch is
@@ -167,6 +172,11 @@ void tail_kernel(TailArgs p) {
   // stream byte offset of launch slab is_i, branch-free (selects only: a branch here splits the
   // unrolled MFMA stream into basic blocks and the register allocator then spills across them)
   auto src_of = [&](int i) -> int {
+    if constexpr (PROJ) {                            // chunks rot, rot + 1, ... (mod NC), NPRE slabs each
+      const int cc = i / S::NPRE, j = i - cc * S::NPRE;
+      const int c = (rot + cc) % NC;
+      return (c * S::NPRE + j) * TL_SLAB;
+    }
     constexpr int NP = PRE ? S::NPRE : 0;
     const int q = i - NP > 0 ? i - NP : 0;
     const int s = q / H, j = q - s * H;              // FFN block, slab within it
@@ -208,9 +218,9 @@ void tail_kernel(TailArgs p) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 2) + NRR) : "memory");
   __syncthreads();                                   // slab 0, the activations + the vector tables visible
 
-  // read side: rd_g = launch slab of the current part start, rd_slot its ring slot
-  int rd_g = 0, rd_slot = 0;
-  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {   // fragment fi of slab rd_g + j
+  // read side: rd_slot = ring slot of the current part's first slab
+  int rd_slot = 0;
+  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {   // fragment fi of the part's slab j
     constexpr int j = decltype(j_tag)::value, fi = decltype(fi_tag)::value;
     int so = rd_slot + j * TL_SLAB;
     so = so >= RING ? so - RING : so;
@@ -237,7 +247,7 @@ void tail_kernel(TailArgs p) {
   tl_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
             std::make_integer_sequence<int, TL_PF>{});
 
-  // consume NF fragments (whole slabs) of the part starting at slab rd_g: mma(f, A) per
+  // consume NF fragments (whole slabs) of the part starting at ring slot rd_slot: mma(f, A) per
   // fragment, LDS reads PF ahead (into the next part), one sync per slab
   // G0: the part's first launch slab when known at compile time (PRE), else -1
   auto run = [&](auto nf_tag, auto g0_tag, auto&& mma) {
@@ -263,7 +273,6 @@ void tail_kernel(TailArgs p) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
     }, std::make_integer_sequence<int, NF>{});
-    rd_g += NF / 16;
     rd_slot += (NF / 16) * TL_SLAB;
     rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
   };
@@ -271,6 +280,68 @@ void tail_kernel(TailArgs p) {
   // (ao: out-projection accumulators; acc: FFN accumulators, born in the first chunk with a zero
   // C operand — explicit zero vectors here get materialised in VGPRs and spilled)
   f32x16 acc[NT];
+  if constexpr (PROJ) {
+    // ---- per output chunk: acc = x W_c^T (zero C operand at k-step 0); + bias -> bf16 in yo.
+    // The NT x 2 stores of chunk c go out PPS per slab during chunk c + 1's stream (bounds-
+    // checked buffer stores: rows >= M fall outside the resource and are dropped): a burst of
+    // stores right before a sync would hold that sync's vmcnt wait until they completed.
+    const uint32_t sv_lane = tl_lds(reinterpret_cast<const char*>(sv)) + 64 * hh;   // &sv[16 hh]
+    const long out_bytes = (long)p.M * NC * D * 2;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.out, (short)0, (int)(out_bytes < 0x7fffffffL ? out_bytes : 0x7fffffffL), 0x00020000);
+    const int row_off = (int)(row * (NC * D) + 16 * hh) * 2;          // bytes; row < 2^31 / (2 NC D)
+    constexpr int PPS = (NT + S::NPRE - 1) / S::NPRE;                 // store pairs per slab
+    u32x4 yo[2 * NT];
+    int yo_off = 0;                                                   // byte offset of yo's chunk
+    auto store_pair = [&](auto t_tag) {
+      constexpr int T = decltype(t_tag)::value;
+      if constexpr (T < NT) {
+        __builtin_amdgcn_raw_buffer_store_b128(yo[2 * T], ors, yo_off + 64 * T, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(yo[2 * T + 1], ors, yo_off + 64 * T + 16, 0, 0);
+      }
+    };
+    auto chunk = [&](int c, auto stores_tag) {
+      constexpr bool STORES = decltype(stores_tag)::value;
+      tl_unroll([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        run(std::integral_constant<int, 4 * NT>{}, std::integral_constant<int, -1>{}, [&](auto fc, const u32x4& A) {
+          constexpr int f = decltype(fc)::value;
+          if constexpr (g == 0 && f < NT) acc[f] = mfma32(A, xa[f / NT], f32x16{});
+          else acc[f % NT] = mfma32(A, xa[4 * g + f / NT], acc[f % NT]);
+          if constexpr (STORES && (f & 15) == 16 - TL_PF) {
+            constexpr int slab = g * (NT / 4) + (f >> 4);
+            tl_unroll([&](auto pc) { store_pair(std::integral_constant<int, slab * PPS + decltype(pc)::value>{}); },
+                      std::make_integer_sequence<int, PPS>{});
+          }
+        });
+      }, std::make_integer_sequence<int, KS / 4>{});
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        // bias of features c D + 32 T + 16 hh + 0..15 (reads + wait in one asm: a compiler LDS
+        // read would wait for the whole in-flight weight stream, see the FFN bias)
+        u32x4 bv[4];
+        asm volatile(
+            "ds_read_b128 %0, %4 offset:0\n ds_read_b128 %1, %4 offset:16\n ds_read_b128 %2, %4 offset:32\n"
+            " ds_read_b128 %3, %4 offset:48\n s_waitcnt lgkmcnt(0)"
+            : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+            : "v"(sv_lane + 4 * (c * D + 32 * T)));
+        float y[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) y[i] = acc[T][i] + __uint_as_float(bv[i >> 2][i & 3]);
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          yo[2 * T + h2] = u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                                 tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+      }
+      yo_off = row_off + c * D * 2;
+    };
+    chunk(rot, std::false_type{});
+#pragma unroll 1
+    for (int cc = 1; cc < NC; ++cc) chunk((rot + cc) % NC, std::true_type{});
+    tl_unroll([&](auto tc) { store_pair(tc); }, std::make_integer_sequence<int, NT>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stream overrun has landed before exit
+    return;
+  }
   if constexpr (PRE) {
     // PRE: the out-projection accumulates onto b_o; LN1 adds the residual x (loaded late, see rr)
     f32x16 ao[NT];
@@ -492,6 +563,31 @@ __global__ void tail_pack_kernel(int D, long n_pieces, const bf16* __restrict__ 
   for (int j = 0; j < 8; ++j) out[p * 8 + j] = v[j];
 }
 
+// Projection stream: per output chunk c (rows c D .. c D + D - 1 of W [NC D, D]), fragments
+// F = s NT + T (k-step s, tile T) like the tail's W_o' part.
+__global__ void proj_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w, bf16* __restrict__ out) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pieces) return;
+  const int NT = D / 32, KS = D / 16, FPRE = NT * KS;
+  const long F = p / 64;
+  const int l = (int)(p % 64), m = l & 31, kh = l >> 5;
+  const int c = (int)(F / FPRE), f = (int)(F % FPRE);
+  const int s = f / NT, T = f % NT;
+  const long n = (long)c * D + tail_out_feat(T, m);
+  for (int j = 0; j < 8; ++j) out[p * 8 + j] = w[n * D + tail_in_feat(s, kh, j)];
+}
+
+template <int D, int NC>
+static int launch_proj(const TailArgs& a, hipStream_t s) {
+  auto kern = tail_kernel<D, false, TL_PF_DEFAULT, 0, true, NC>;
+  constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + NC * D * 4;
+  static_assert(NC * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, TL_ROWS)), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int D, bool PRE>
 static int launch_tail(const TailArgs& a, hipStream_t s) {
   const char* ev = getenv("SNVRAG_TAIL_VARIANT");
@@ -584,4 +680,52 @@ extern "C" int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* o
   const TailArgs a{(int)M, (const bf16*)x1, nullptr, (bf16*)out, (const char*)wstream, ffn_vec, nullptr, nullptr,
                    nullptr, eps};
   return tail_common(M, D, false, a, stream);
+}
+
+static size_t proj_bytes(int D, int NC) {
+  switch (D) {
+    case 128: return (size_t)NC * TailShape<128>::NPRE * TL_SLAB;
+    case 256: return (size_t)NC * TailShape<256>::NPRE * TL_SLAB;
+    case 384: return (size_t)NC * TailShape<384>::NPRE * TL_SLAB;
+    default: return 0;
+  }
+}
+
+extern "C" size_t snvrag_proj_pack_bytes(int D, int NC) { return proj_bytes(D, NC); }
+
+extern "C" int snvrag_proj_pack(int D, int NC, const void* w, void* out, void* stream) {
+  SNV_CHECK_ARG(tail_d_ok(D) && (NC == 1 || NC == 3), "projection needs D in {128, 256, 384}, NC in {1, 3}");
+  SNV_CHECK_ARG(w && out, "null pointer");
+  const long pieces = (long)(proj_bytes(D, NC) / 16);
+  hipLaunchKernelGGL(proj_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
+                     (const bf16*)w, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, const void* wstream, const float* bias,
+                                   void* out, void* stream) {
+  SNV_CHECK_ARG(tail_d_ok(D) && (NC == 1 || NC == 3), "projection needs D in {128, 256, 384}, NC in {1, 3}");
+  SNV_CHECK_ARG(x && wstream && bias && out, "null pointer");
+  SNV_CHECK_ARG(x != out, "x and out must not alias");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wstream % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  const TailArgs a{(int)M, (const bf16*)x, nullptr, (bf16*)out, (const char*)wstream, bias, nullptr, nullptr,
+                   nullptr, 0.f};
+  evlog_begin(s);
+  int rc;
+  switch (D * 8 + NC) {
+    case 128 * 8 + 1: rc = launch_proj<128, 1>(a, s); break;
+    case 128 * 8 + 3: rc = launch_proj<128, 3>(a, s); break;
+    case 256 * 8 + 1: rc = launch_proj<256, 1>(a, s); break;
+    case 256 * 8 + 3: rc = launch_proj<256, 3>(a, s); break;
+    case 384 * 8 + 1: rc = launch_proj<384, 1>(a, s); break;
+    default: rc = launch_proj<384, 3>(a, s); break;
+  }
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)D * D * NC);
+  return 0;
 }

@@ -193,6 +193,8 @@ class Engine:
                 t["o_ws"] = K.ffn_pre_pack(t["w_o"])
                 # the whole block tail (W_o' + W1 + W2') on 32x32 MFMAs (csrc/tail.hip)
                 t["tail_w"] = K.tail_pack(t["w_o"], t["w1"], w2g)
+                # QKV projection on the same 32x32 stream kernel (csrc/tail.hip PROJ mode)
+                t["qkv_pw"] = K.proj_pack(t["w_qkv"])
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:

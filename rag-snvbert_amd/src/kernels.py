@@ -158,6 +158,34 @@ def tail_pack(w_o: torch.Tensor, w1: torch.Tensor, w2g: torch.Tensor) -> torch.T
     return out
 
 
+def proj_pack(w: torch.Tensor) -> torch.Tensor:
+    """Stream of W [NC*D, D] (bf16) for ``proj_forward`` (NC = W.shape[0] // D)."""
+    N.require_gpu(w)
+    n, D = w.shape
+    NC = n // D
+    nbytes = int(N.lib().snvrag_proj_pack_bytes(D, NC))
+    assert nbytes > 0 and NC * D == n, "projection needs D in {128, 256, 384} and NC*D rows"
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    wb = _c(w.to(torch.bfloat16))
+    check(N.lib().snvrag_proj_pack(D, NC, ptr(wb), ptr(out), stream_ptr()), "proj_pack")
+    return out
+
+
+def proj_forward(x: torch.Tensor, wstream: torch.Tensor, bias: torch.Tensor, NC: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out [M, NC*D] = x W^T + bias on the 32x32-MFMA stream kernel (bf16)."""
+    N.require_gpu(x)
+    assert x.dtype == torch.bfloat16
+    D = x.shape[-1]
+    M = x.numel() // D
+    if out is None:
+        out = torch.empty(M, NC * D, device=x.device, dtype=torch.bfloat16)
+    b = _c(bias.float())
+    check(N.lib().snvrag_proj_forward(M, D, NC, ptr(_c(x)), ptr(wstream), ptr(b), ptr(out), stream_ptr()),
+          "proj_forward")
+    return out
+
+
 def tail_forward(att: torch.Tensor, x: torch.Tensor, wstream: torch.Tensor, b_o, ln1_g, ln1_b,
                  ffn_vec: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     """x <- LN2(x1 + FFN(x1)), x1 = LN1(x + att W_o^T + b_o), in place (32x32-MFMA kernel)."""

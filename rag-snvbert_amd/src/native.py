@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 13
+ABI_VERSION = 15
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -70,7 +70,7 @@ class AdamS(C.Structure):
 class LayerW(C.Structure):
     _fields_ = [(n, vp) for n in ("w_qkv", "b_qkv", "w_o", "b_o", "ln1_g", "ln1_b", "w1", "b1",
                                   "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")] + [("q_scale", f32)] + \
-        [("ffn_w", vp), ("ffn_v", vp), ("qkv_ws", vp), ("o_ws", vp), ("tail_w", vp)]
+        [("ffn_w", vp), ("ffn_v", vp), ("qkv_ws", vp), ("o_ws", vp), ("tail_w", vp), ("qkv_pw", vp)]
 
 
 _SIGS = {
@@ -118,6 +118,9 @@ _SIGS = {
     "snvrag_ffn_pre_pack_bytes": ([C.c_int], C.c_size_t),
     "snvrag_ffn_pre_pack": ([C.c_int, vp, vp, vp], C.c_int),
     "snvrag_block_tail_forward": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp], C.c_int),
+    "snvrag_proj_pack_bytes": ([C.c_int, C.c_int], C.c_size_t),
+    "snvrag_proj_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),
+    "snvrag_proj_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_tail_pack_bytes": ([C.c_int], C.c_size_t),
     "snvrag_tail_pack": ([C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_tail_forward": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, f32, vp], C.c_int),

@@ -1,0 +1,24 @@
+"""Run only the bf16 dh=32 attention kernel at the bench shape (512 sequences x 1030 tokens,
+12 heads) — for rocprofv3 PMC passes and timing."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
+from src import kernels as K  # noqa: E402
+
+nseq, L, H, dh = int(os.environ.get("NSEQ", 512)), 1030, 12, 32
+qkv = (torch.randn(nseq * L, 3 * H * dh, device="cuda") * float(os.environ.get("QKV_STD", 0.4))).to(torch.bfloat16)
+out = None
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for i in range(int(os.environ.get("REPS", 3))):
+    if i == 1:
+        a.record()
+    out = K.attention(qkv, nseq, L, H, dh)
+b.record()
+torch.cuda.synchronize()
+n = int(os.environ.get("REPS", 3)) - 1
+if n > 0:
+    ms = a.elapsed_time(b) / n
+    print(f"attention {ms:.4f} ms  {4.0 * L * L * dh * H * nseq / ms / 1e9:.1f} TFLOP/s", flush=True)

@@ -1,0 +1,47 @@
+"""QKV projection on the 32x32 stream kernel (csrc/tail.hip PROJ mode) vs the weight-streaming
+GEMM (csrc/wsgemm.hip) at the bench shape (M = 512 x 1030, D = 384, N = 3D): max |diff| vs an
+fp64 reference on a small M, then launch times (HIP events)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
+from src import kernels as K  # noqa: E402
+
+D, dev, bf = 384, "cuda", torch.bfloat16
+g = torch.Generator(device="cpu").manual_seed(0)
+w = (torch.randn(3 * D, D, generator=g) / D ** 0.5).to(dev, bf)
+b = (0.1 * torch.randn(3 * D, generator=g)).to(dev)
+ws = K.proj_pack(w)
+for M in (777, 128 * 5 + 3):
+    x = torch.randn(M, D, generator=g).to(dev, bf)
+    o = K.proj_forward(x, ws, b, 3)
+    ref = x.double() @ w.double().T + b.double()
+    print(f"M={M} max|err| {(o.double() - ref).abs().max().item():.4f}", flush=True)
+M = 512 * 1030
+x = torch.randn(M, D, device=dev).to(bf)
+out = torch.empty(M, 3 * D, device=dev, dtype=bf)
+wsg = K.wsg_pack(w)
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(e) / reps
+
+
+fl = 2.0 * M * D * 3 * D
+o1 = K.proj_forward(x, ws, b, 3, out=out).clone()
+o2 = K.wsg_linear(x, wsg, 3 * D, b)
+print(f"proj vs wsg max|diff| {(o1.float() - o2.float()).abs().max().item():.4f}", flush=True)
+for name, fn in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out)),
+                 ("wsg (wsgemm.hip)", lambda: K.wsg_linear(x, wsg, 3 * D, b))):
+    ms = timeit(fn)
+    print(f"{name:18s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
