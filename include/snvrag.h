@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 15
+#define SNVRAG_ABI_VERSION 16
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -384,12 +384,16 @@ int snvrag_evlog_read(int* kinds, float* ms, double* work, int max);
  * attention_train_fwd: bf16 qkv [nseq*L, ld_qkv] (q | k | v column blocks) -> out
  *   [nseq*L, ld_out] and lse [nseq][heads][L] f32 (log2 domain: P = exp2(c s - lse),
  *   c = scale*log2 e).  attention_bwd: dout [nseq*L, ld_dout] -> dqkv (same layout as
- *   qkv, bf16); d_ws f32 [nseq*heads*L] scratch (rowsum(dO o O)).  dh in {32, 64}. */
+ *   qkv, bf16); d_ws f32 [nseq*heads*L] scratch (rowsum(dO o O)).  dh in {32, 64}.
+ *   dropout_p > 0: attention-probability dropout (attention.py:28-29) with the counter-based
+ *   keep mask of csrc/attn_common.h (seed; the backward must get the forward's p and seed). */
 int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv, int64_t ld_qkv,
-                               void* out, int64_t ld_out, float* lse, float scale, void* stream);
+                               void* out, int64_t ld_out, float* lse, float scale, float dropout_p,
+                               uint64_t seed, void* stream);
 int snvrag_attention_bwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv, int64_t ld_qkv,
                          const void* out, int64_t ld_out, const void* dout, int64_t ld_dout,
-                         const float* lse, float* d_ws, void* dqkv, int64_t ld_dqkv, float scale, void* stream);
+                         const float* lse, float* d_ws, void* dqkv, int64_t ld_dqkv, float scale,
+                         float dropout_p, uint64_t seed, void* stream);
 /* focal loss over rows with mask[m] != 0: probs [M, C] f32 (the heads' softmax output),
  * labels int64 [M]; loss_sum += weight * sum_m FL_m (caller zeroes it); grad [M, C] =
  * weight * dFL/dprobs (0 on unmasked rows). */

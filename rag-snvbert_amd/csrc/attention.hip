@@ -21,7 +21,8 @@ namespace snvrag {
 template <int DH>
 __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, const bf16* __restrict__ qkv,
                                                      long ld, bf16* __restrict__ out, long ldo,
-                                                     float scale_log2e, int nqb, float* __restrict__ lse) {
+                                                     float scale_log2e, int nqb, float* __restrict__ lse,
+                                                     AttnDrop drop) {
   using C = AttnCfg<DH>;
   __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE];
 
@@ -130,14 +131,28 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, con
     const float alpha = exp2f(m_run - m_new);
     float psum = 0.f;
     bf16x8 pb[2];
+    if (drop.thresh) {
+      // training dropout: the row sum keeps every probability, the PV product the kept ones
+      const uint32_t dbase = drop_base(drop.seed, (uint32_t)sh);
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kt][r] - m_new);
-        psum += p;
-        pb[kt >> 1][(kt & 1) * 4 + r] = (bf16)p;
-      }
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[kt][r] - m_new);
+          psum += p;
+          const int key = kbase + 16 * kt + 4 * lg + r;
+          pb[kt >> 1][(kt & 1) * 4 + r] = (bf16)(p * drop_mul(drop, dbase, (uint32_t)q, (uint32_t)key));
+        }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[kt][r] - m_new);
+          psum += p;
+          pb[kt >> 1][(kt & 1) * 4 + r] = (bf16)p;
+        }
+    }
     psum += __shfl_xor(psum, 16, 64);
     psum += __shfl_xor(psum, 32, 64);
     l_run = l_run * alpha + psum;
@@ -521,7 +536,8 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const long nb = (long)nqb * H * nseq;
     SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
     hipLaunchKernelGGL(attn_fwd_bf16<DH>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, H,
-                       (const bf16*)qkv, ld, (bf16*)out, ldo, scale * 1.4426950408889634f, nqb, nullptr);
+                       (const bf16*)qkv, ld, (bf16*)out, ldo, scale * 1.4426950408889634f, nqb, nullptr,
+                       make_attn_drop(0.f, 0));
   } else {
     hipLaunchKernelGGL(attn_fwd_f32<DH>, dim3(cdiv(L, 64), H, (unsigned)nseq), dim3(64), 0, s,
                        (int)nseq, (int)L, H, (const float*)qkv, ld, (float*)out, ldo, scale);
@@ -548,8 +564,10 @@ extern "C" int snvrag_attention_fallbacks(int reset) {
 // the backward (attention_train.hip) rebuilds P from.
 extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv,
                                           int64_t ld_qkv, void* out, int64_t ld_out, float* lse, float scale,
-                                          void* stream) {
+                                          float dropout_p, uint64_t seed, void* stream) {
   SNV_CHECK_ARG(qkv && out && lse, "null pointer");
+  SNV_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout probability must be in [0, 1)");
+  const AttnDrop drop = make_attn_drop(dropout_p, seed);
   SNV_CHECK_ARG(nseq >= 0 && L > 0 && heads > 0, "bad shape");
   SNV_CHECK_ARG(ld_qkv >= 3L * heads * dh && ld_out >= (long)heads * dh, "leading dims too small");
   SNV_CHECK_ARG(ld_qkv % 8 == 0 && ld_out % 4 == 0, "bf16 alignment");
@@ -562,10 +580,10 @@ extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, in
   evlog_begin(s);
   if (dh == 32)
     hipLaunchKernelGGL(attn_fwd_bf16<32>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
-                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse);
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);
   else if (dh == 64)
     hipLaunchKernelGGL(attn_fwd_bf16<64>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
-                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse);
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);
   else
     return fail(__func__, "training attention supports head dims 32 and 64");
   SNV_LAUNCH_CHECK();

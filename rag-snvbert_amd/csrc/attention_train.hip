@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
                                                    const bf16* __restrict__ dO, long lddo,
                                                    const float* __restrict__ lse, float* __restrict__ Dout,
                                                    bf16* __restrict__ dqkv, long ldd, float c_log2e, float scale,
-                                                   int nqb) {
+                                                   int nqb, AttnDrop drop) {
   using C = AttnCfg<DH>;
   using B = BwdCfg<DH>;
   constexpr int STAGE = 2 * C::KBYTES + C::VBYTES;          // K rows, V rows, K^T
@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
   dq_ += __shfl_xor(dq_, 32, 64);
   const long srow = ((long)seq * H + h) * L;
   const float lse_q = q < L ? lse[srow + q] : 0.f;
+  const uint32_t dbase = drop_base(drop.seed, (uint32_t)sh);
   if (q < L && lg == 0) Dout[srow + q] = dq_;
 
   u32x4 kr[B::NLD], vr[B::NLD];
@@ -178,7 +179,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
       for (int r = 0; r < 4; ++r) {
         const int key = t * 64 + 16 * kt + 4 * lg + r;
         const float p = key < L ? exp2f(s[kt][r] * c_log2e - lse_q) : 0.f;
-        dsb[kt >> 1][(kt & 1) * 4 + r] = (bf16)(p * (dp[kt][r] - dq_));
+        // dropout: dP = (dO V^T) o mask / (1 - p); D_q = rowsum(dO o O) is unchanged (O = P' V)
+        const float dpv = drop.thresh ? dp[kt][r] * drop_mul(drop, dbase, (uint32_t)q, (uint32_t)key) : dp[kt][r];
+        dsb[kt >> 1][(kt & 1) * 4 + r] = (bf16)(p * (dpv - dq_));
       }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
                                                     const bf16* __restrict__ dO, long lddo,
                                                     const float* __restrict__ lse, const float* __restrict__ Dq,
                                                     bf16* __restrict__ dqkv, long ldd, float c_log2e, float scale,
-                                                    int nkb) {
+                                                    int nkb, AttnDrop drop) {
   using C = AttnCfg<DH>;
   using B = BwdCfg<DH>;
   constexpr int STAGE = 2 * C::KBYTES + 2 * C::VBYTES + 2 * 64 * 4;   // Q, dO rows; Q^T, dO^T; lse, D
@@ -221,6 +224,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
   const bf16* dOp = dO + row0 * lddo + h * DH;
   const long srow = ((long)seq * H + h) * L;
   const int key = kb * 64 + wave * 16 + li;
+  const uint32_t dbase = drop_base(drop.seed, (uint32_t)sh);
 
   bf16x8 kf[C::KS], vf[C::KS];
   row_frag<DH>(kf, qkv + row0 * ld + D + h * DH, ld, key, L, lg);
@@ -279,8 +283,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * qt + 4 * lg + r;
         const float p = (t * 64 + ql < L) ? exp2f(s[qt][r] * c_log2e - ls[ql]) : 0.f;
-        pb[qt >> 1][(qt & 1) * 4 + r] = (bf16)p;
-        dsb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * (dp[qt][r] - ls[64 + ql]));
+        // dropout: dV uses the kept, rescaled probabilities; dP is masked the same way
+        const float mk = drop.thresh ? drop_mul(drop, dbase, (uint32_t)(t * 64 + ql), (uint32_t)key) : 1.f;
+        pb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * mk);
+        dsb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * (dp[qt][r] * mk - ls[64 + ql]));
       }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -310,17 +316,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
 
 template <int DH>
 static int launch_bwd(long nseq, long L, int H, const bf16* qkv, long ld, const bf16* O, long ldo, const bf16* dO,
-                      long lddo, const float* lse, float* Dws, bf16* dqkv, long ldd, float scale, hipStream_t s) {
+                      long lddo, const float* lse, float* Dws, bf16* dqkv, long ldd, float scale, AttnDrop drop,
+                      hipStream_t s) {
   const int nb = cdiv(L, 64);
   const long grid = (long)nb * H * nseq;
   SNV_CHECK_ARG(grid < (1L << 31), "grid too large");
   const float cl = scale * 1.4426950408889634f;
   evlog_begin(s);
   hipLaunchKernelGGL(attn_bwd_dq<DH>, dim3((unsigned)grid), dim3(256), 0, s, (int)L, H, qkv, ld, O, ldo, dO, lddo,
-                     lse, Dws, dqkv, ldd, cl, scale, nb);
+                     lse, Dws, dqkv, ldd, cl, scale, nb, drop);
   SNV_LAUNCH_CHECK();
   hipLaunchKernelGGL(attn_bwd_dkv<DH>, dim3((unsigned)grid), dim3(256), 0, s, (int)L, H, qkv, ld, dO, lddo, lse,
-                     (const float*)Dws, dqkv, ldd, cl, scale, nb);
+                     (const float*)Dws, dqkv, ldd, cl, scale, nb, drop);
   SNV_LAUNCH_CHECK();
   // QK^T and dO V^T in both kernels + the dQ, dK, dV products: 7 x 2 L^2 dh per head
   evlog_end(s, EV_ATTN_BWD, 14.0 * nseq * H * (double)L * L * DH);
@@ -334,8 +341,10 @@ using namespace snvrag;
 extern "C" int snvrag_attention_bwd(int64_t nseq, int64_t L, int heads, int dh, const void* qkv, int64_t ld_qkv,
                                     const void* out, int64_t ld_out, const void* dout, int64_t ld_dout,
                                     const float* lse, float* d_ws, void* dqkv, int64_t ld_dqkv, float scale,
-                                    void* stream) {
+                                    float dropout_p, uint64_t seed, void* stream) {
   SNV_CHECK_ARG(qkv && out && dout && lse && d_ws && dqkv, "null pointer");
+  SNV_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "dropout probability must be in [0, 1)");
+  const AttnDrop drop = make_attn_drop(dropout_p, seed);
   SNV_CHECK_ARG(nseq >= 0 && L > 0 && heads > 0, "bad shape");
   SNV_CHECK_ARG(ld_qkv >= 3L * heads * dh && ld_dqkv >= 3L * heads * dh && ld_out >= (long)heads * dh &&
                     ld_dout >= (long)heads * dh, "leading dims too small");
@@ -345,9 +354,9 @@ extern "C" int snvrag_attention_bwd(int64_t nseq, int64_t L, int heads, int dh, 
   const bf16 *q = (const bf16*)qkv, *o = (const bf16*)out, *g = (const bf16*)dout;
   switch (dh) {
     case 32: return launch_bwd<32>(nseq, L, heads, q, ld_qkv, o, ld_out, g, ld_dout, lse, d_ws, (bf16*)dqkv, ld_dqkv,
-                                   scale, s);
+                                   scale, drop, s);
     case 64: return launch_bwd<64>(nseq, L, heads, q, ld_qkv, o, ld_out, g, ld_dout, lse, d_ws, (bf16*)dqkv, ld_dqkv,
-                                   scale, s);
+                                   scale, drop, s);
     default: return fail(__func__, "training attention supports head dims 32 and 64");
   }
 }

@@ -118,7 +118,7 @@ void wsg_kernel(int M, const bf16* __restrict__ A, const char* __restrict__ ws, 
   float keep[EPI == 1 ? NCH : 1][16];
   float po0 = 0.f, po1 = 0.f;                     // EPI 2 partial logits
   int slab = 0;
-#pragma unroll (EPI == 1 ? NCH : 1)
+#pragma unroll EPI == 1 ? NCH : 1
   for (int c0 = 0; c0 < NCH; ++c0) {
     const int c = chunk_of(c0);
     f32x4 h[4];

@@ -165,24 +165,29 @@ def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln) -> torch.T
 
 class _HipAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, nseq, L, heads, dh):
+    def forward(ctx, qkv, nseq, L, heads, dh, p, seed):
         qkv = qkv.contiguous()
-        out, lse = K.attention_train_fwd(qkv, nseq, L, heads, dh)
+        out, lse = K.attention_train_fwd(qkv, nseq, L, heads, dh, p, seed)
         ctx.save_for_backward(qkv, out, lse)
-        ctx.shape = (nseq, L, heads, dh)
+        ctx.shape = (nseq, L, heads, dh, p, seed)
         return out
 
     @staticmethod
     def backward(ctx, gout):
         qkv, out, lse = ctx.saved_tensors
-        nseq, L, heads, dh = ctx.shape
+        nseq, L, heads, dh, p, seed = ctx.shape
         g = gout.to(torch.bfloat16).contiguous()
-        return K.attention_bwd(qkv, out, g, lse, nseq, L, heads, dh), None, None, None, None
+        return K.attention_bwd(qkv, out, g, lse, nseq, L, heads, dh, p, seed), None, None, None, None, None, None
 
 
-def hip_attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int) -> torch.Tensor:
-    """softmax(q k^T / sqrt(dh)) v per (sequence, head); qkv [nseq*L, 3D] bf16 -> [nseq*L, D]."""
-    return _HipAttention.apply(qkv, nseq, L, heads, dh)
+def hip_attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int, dropout_p: float = 0.0,
+                  seed: Optional[int] = None) -> torch.Tensor:
+    """softmax(q k^T / sqrt(dh)) v per (sequence, head); qkv [nseq*L, 3D] bf16 -> [nseq*L, D].
+    ``dropout_p`` > 0: attention-probability dropout (attention.py:28-29); the keep mask is a
+    counter-based hash of ``seed`` (drawn from torch's RNG when None), shared by the backward."""
+    if dropout_p > 0 and seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    return _HipAttention.apply(qkv, nseq, L, heads, dh, float(dropout_p), int(seed or 0))
 
 
 class _FocalLoss(torch.autograd.Function):

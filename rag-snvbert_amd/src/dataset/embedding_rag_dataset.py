@@ -245,10 +245,21 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                                                     shard.group)
             else:
                 Aq = Ar = None
-                if not same and P.af is not None:
+                aq_period = len(rows)
+                p_drop = embedding_layer.dropout.p if train else 0.0
+                if train and p_drop > 0 and len(rows):
+                    # train mode: the reference embeds the queries WITH dropout before the distance
+                    # (:385-386).  u = W[tok] + Aq - Ar must equal drop(e_q) - pe - A_r, so Aq carries
+                    # drop(e_q) - W[tok] - pe per query row (exact-LUT form, fresh torch RNG mask)
+                    Afull = eng.af_embedding(torch.cat([afw, afw]), True).float() if P.af is not None else 0.0
+                    e_q = P.W[tok] + P.pe[:L] + Afull
+                    Aq = (torch.nn.functional.dropout(e_q, p_drop, True) - P.W[tok] - P.pe[:L]).contiguous()
+                    Ar = Ar_emb if Ar_emb is not None else torch.zeros(L, D, device=dev)
+                    aq_period = 2 * len(rows)
+                elif not same and P.af is not None:
                     Aq = eng.af_embedding(afw, True).float().contiguous()
                     Ar = Ar_emb
-                idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=len(rows), Ar=Ar)
+                idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=aq_period, Ar=Ar)
         nb = len(rows)
         if nb == 0:
             continue

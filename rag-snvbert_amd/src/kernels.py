@@ -468,20 +468,23 @@ def selftest_mfma() -> int:
 
 
 # ---------------------------------------------------------------- training --
-def attention_train_fwd(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int):
-    """bf16 attention forward that also returns lse [nseq, heads, L] (log2 domain) for the backward."""
+def attention_train_fwd(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int, dropout_p: float = 0.0,
+                        seed: int = 0):
+    """bf16 attention forward that also returns lse [nseq, heads, L] (log2 domain) for the backward;
+    ``dropout_p`` > 0: attention-probability dropout with the counter-based mask of ``seed``."""
     N.require_gpu(qkv)
     assert qkv.dtype == torch.bfloat16
     D = heads * dh
     out = torch.empty(nseq * L, D, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(nseq, heads, L, device=qkv.device, dtype=torch.float32)
     check(N.lib().snvrag_attention_train_fwd(nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1], ptr(out), D,
-                                             ptr(lse), 1.0 / float(dh) ** 0.5, stream_ptr()), "attention_train_fwd")
+                                             ptr(lse), 1.0 / float(dh) ** 0.5, float(dropout_p), int(seed) & (2 ** 64 - 1),
+                                             stream_ptr()), "attention_train_fwd")
     return out, lse
 
 
 def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, nseq: int, L: int,
-                  heads: int, dh: int) -> torch.Tensor:
+                  heads: int, dh: int, dropout_p: float = 0.0, seed: int = 0) -> torch.Tensor:
     """d(qkv) [nseq*L, 3D] bf16 of the unmasked softmax attention (csrc/attention_train.hip)."""
     N.require_gpu(qkv, out, dout, lse)
     D = heads * dh
@@ -489,7 +492,8 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
     ws = torch.empty(nseq * heads * L, device=qkv.device, dtype=torch.float32)
     check(N.lib().snvrag_attention_bwd(nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1], ptr(_c(out)), out.shape[-1],
                                        ptr(_c(dout)), dout.shape[-1], ptr(_c(lse)), ptr(ws), ptr(dqkv), 3 * D,
-                                       1.0 / float(dh) ** 0.5, stream_ptr()), "attention_bwd")
+                                       1.0 / float(dh) ** 0.5, float(dropout_p), int(seed) & (2 ** 64 - 1),
+                                       stream_ptr()), "attention_bwd")
     return dqkv
 
 

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -125,9 +125,10 @@ _SIGS = {
     "snvrag_tail_pack": ([C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_tail_forward": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, f32, vp], C.c_int),
     "snvrag_tail_ffn_forward": ([i64, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
-    "snvrag_attention_train_fwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, f32, vp], C.c_int),
-    "snvrag_attention_bwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, i64, vp, vp, vp, i64, f32, vp],
-                             C.c_int),
+    "snvrag_attention_train_fwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, f32, f32, C.c_uint64, vp],
+                                   C.c_int),
+    "snvrag_attention_bwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, i64, vp, vp, vp, i64, f32, f32,
+                              C.c_uint64, vp], C.c_int),
     "snvrag_focal_loss": ([i64, C.c_int, vp, vp, vp, f32, f32, vp, vp, vp], C.c_int),
     "snvrag_sqnorm": ([i64, vp, vp, vp], C.c_int),
     "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),

@@ -15,12 +15,15 @@ model/bert.py:148-219:
 Heavy nodes (every Linear with K, N multiples of 8, attention) run on libsnvrag through
 ``autograd_ops``; the small per-site MLPs, LayerNorm, activations and dropout are torch
 elementwise kernels.  Differences from the reference, all in the stochastic parts:
-  * the attention-probability dropout (attention.py:28-29) is not applied;
+  * the attention-probability dropout (attention.py:28-29) draws its keep mask from a
+    counter-based hash (csrc/attn_common.h) rather than torch's generator;
   * EnhancedRareVariantFusion's AF gate (af_adapter) is computed once per sample and
     shared by the h1 and h2 calls (the reference computes it twice with independent
     dropout masks; without dropout the two are identical);
-  * the neighbour mean is taken over the k complete-token embeddings before dropout
-    (the reference drops each neighbour's embedding independently, then averages).
+  * on a sharded panel (retrieval/shards.py) the neighbour mean comes from the all-reduced
+    alt-allele counts, so each neighbour's embedding is not dropped independently (the
+    replicated panel does apply the reference's per-neighbour dropout, ``neighbour_mean_dropout``),
+    and the retrieval query embeddings are not dropped.
 With dropout p = 0 the graph computes the reference's train-mode function exactly
 (up to bf16 rounding) — the gradient parity tests run it that way.
 """
@@ -132,7 +135,8 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     ll = a.linear_layers
     qkv = hip_linear(x.reshape(-1, D), [ll[0].weight, ll[1].weight, ll[2].weight],
                      [ll[0].bias, ll[1].bias, ll[2].bias])
-    att = hip_attention(qkv, nseq, L, a.heads, a.dims)
+    # attention-probability dropout (attention.py:28-29), counter-based mask shared with the backward
+    att = hip_attention(qkv, nseq, L, a.heads, a.dims, a.dropout.p if training else 0.0)
     o = hip_linear(att, a.output_layer.weight, a.output_layer.bias).reshape(x.shape)
     x = _drop(hip_add_layernorm(x, o, blk.input_sublayer.norm), p, training)
     ff = blk.feed_forward
@@ -160,13 +164,17 @@ def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
     pe = emb.position.pe[0, :L].float().contiguous()
     rows_out: List[torch.Tensor] = []
     vals: List[torch.Tensor] = []
+    p = emb.dropout.p if emb.training else 0.0
     for rows, idx_h1, idx_h2, index, *cnt in groups:
         Ar = af_embedding(emb.af_embedding, index.ref_af.view(1, -1))[0].float() if emb.use_af else \
             torch.zeros(L, D, device=pe.device)
         idx = torch.cat([idx_h1, idx_h2], 0)
         # (sharded panel: the all-reduced alt-allele counts of the neighbours, retrieval/shards.py)
         counts = cnt[0] if cnt else None
-        m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, counts=counts)
+        if p > 0 and counts is None:
+            m = neighbour_mean_dropout(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, p)
+        else:
+            m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, counts=counts)
         nb = rows.numel()
         rows_out += [rows, rows + B]
         vals += [m[:nb], m[nb:]]
@@ -175,6 +183,25 @@ def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
     out = torch.empty_like(stacked)
     out[order] = stacked
     return out
+
+
+def neighbour_mean_dropout(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, codes: torch.Tensor, n_sites: int,
+                           pe: torch.Tensor, L: int, p: float, tok0: int = 5, sos: int = 2, eos: int = 3,
+                           pad: int = 0) -> torch.Tensor:
+    """Train-mode neighbour mean with the reference's per-neighbour dropout
+    (embedding_rag_dataset.py:404-417: each retrieved complete-token sequence re-encoded by
+    BERTEmbedding in train mode — its own dropout mask — then bert.py:171-183's mean over k):
+    [nq, L, D] bf16, differentiable in W and Ar."""
+    nq, k = idx.shape
+    tok = torch.full((nq, k, L), pad, device=idx.device, dtype=torch.long)
+    tok[..., 0] = sos
+    if n_sites + 1 < L:
+        tok[..., n_sites + 1] = eos
+    valid = idx >= 0
+    tok[..., 1:1 + n_sites] = tok0 + codes[idx.clamp(min=0)][..., :n_sites].long()
+    e = F.embedding(tok, W, padding_idx=0) + pe[:L] + Ar
+    e = F.dropout(e, p, True) * valid[..., None, None]
+    return (e.sum(1) / valid.sum(1).clamp(min=1)[:, None, None]).to(T)
 
 
 def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:

@@ -1,0 +1,31 @@
+"""Host restatement of the attention-dropout keep mask (csrc/attn_common.h) for the parity tests:
+h(q, k) = fmix32(base + q * 0x9E3779B1 + k * 0x85EBCA77), base = fmix32(lo(seed) ^ fmix32(hi(seed) +
+sh * 0xC2B2AE3D)), keep iff h >= floor(p * 2^32)."""
+import numpy as np
+
+M32 = np.uint64(0xFFFFFFFF)
+
+
+def fmix32(h):
+    h = np.asarray(h, np.uint64) & M32
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & M32
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & M32
+    h ^= h >> np.uint64(16)
+    return h
+
+
+def keep_mask(seed: int, nseq: int, heads: int, L: int, p: float) -> np.ndarray:
+    """bool [nseq, heads, L(q), L(k)]"""
+    thresh = np.uint64(int(p * 4294967296.0))
+    lo, hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    q = np.arange(L, dtype=np.uint64)
+    out = np.zeros((nseq, heads, L, L), bool)
+    for sq in range(nseq):
+        for h in range(heads):
+            sh = np.uint64(sq * heads + h)
+            base = fmix32(lo ^ fmix32((hi + sh * np.uint64(0xC2B2AE3D)) & M32))
+            x = (base + q[:, None] * np.uint64(0x9E3779B1) + q[None, :] * np.uint64(0x85EBCA77)) & M32
+            out[sq, h] = fmix32(x) >= thresh
+    return out

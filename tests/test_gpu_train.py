@@ -57,6 +57,36 @@ def test_attention_backward_vs_torch(nseq, L, H, dh):
         assert err <= 2e-2 * b.abs().max().item() + 1e-3, (name, err, b.abs().max().item())
 
 
+@pytest.mark.parametrize("nseq,L,H,dh,p", [(2, 1030, 2, 32, 0.1), (1, 200, 3, 64, 0.3)])
+def test_attention_dropout_forward_backward_vs_torch(nseq, L, H, dh, p):
+    """Attention-probability dropout (attention.py:28-29): the HIP forward/backward with the
+    counter-based keep mask vs torch autograd of softmax(...) * mask / (1 - p) @ V with the same
+    mask (tests/attn_helpers.py restates the hash); keep rate ~ 1 - p; the seed changes the mask."""
+    from src import kernels as K
+    from attn_helpers import keep_mask
+    g = torch.Generator(device="cpu").manual_seed(L + 7)
+    D = H * dh
+    qkv = (torch.randn(nseq * L, 3 * D, generator=g) * 0.8).to(DEV, torch.bfloat16)
+    dout = torch.randn(nseq * L, D, generator=g).to(DEV, torch.bfloat16)
+    seed = 0x1234567890ABCDEF
+    keep = torch.from_numpy(keep_mask(seed, nseq, H, L, p)).to(DEV)
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    assert (torch.from_numpy(keep_mask(seed + 1, nseq, H, L, p)).to(DEV) != keep).float().mean() > 0.05
+    out, lse = K.attention_train_fwd(qkv, nseq, L, H, dh, p, seed)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    x = ref_in.view(nseq, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    P = torch.softmax((x[0] @ x[1].transpose(-1, -2)) / math.sqrt(dh), -1)
+    ref = ((P * keep / (1 - p)) @ x[2]).permute(0, 2, 1, 3).reshape(nseq * L, D)
+    torch.testing.assert_close(out.float(), ref.detach(), rtol=2e-2, atol=2e-2)
+    ref.backward(dout.float())
+    got = K.attention_bwd(qkv, out, dout, lse, nseq, L, H, dh, p, seed).float()
+    for i, name in enumerate("qkv"):
+        a = got[:, i * D:(i + 1) * D]
+        b = ref_in.grad[:, i * D:(i + 1) * D]
+        err = (a - b).abs().max().item()
+        assert err <= 2e-2 * b.abs().max().item() + 1e-3, (name, err, b.abs().max().item())
+
+
 def test_attention_lse_matches_logsumexp():
     from src import kernels as K
     nseq, L, H, dh = 2, 300, 2, 32
@@ -351,3 +381,57 @@ def test_checkpoint_round_trip(tmp_path):
     torch.testing.assert_close(lb, la, rtol=1e-5, atol=1e-5)
     for pa, pb in zip(a.model.parameters(), b.model.parameters()):
         torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-6)
+
+
+def test_neighbour_mean_dropout_semantics():
+    """Per-neighbour dropout of the re-encoded neighbours (embedding_rag_dataset.py:404-417 +
+    bert.py:171-183): p = 0 equals the counts/codes K-mean; p > 0 is unbiased (average over
+    seeds -> the undropped mean) and differentiable in W and Ar."""
+    from src.train_forward import neighbour_mean_dropout
+    from src.autograd_ops import rag_mean_train
+    rng = np.random.default_rng(0)
+    nq, k, S, L, D = 6, 4, 200, 230, 32
+    codes = torch.from_numpy((rng.random((50, 256)) < 0.3).astype(np.uint8)).to(DEV)
+    idx = torch.from_numpy(rng.integers(0, 50, (nq, k))).to(DEV)
+    idx[0, 3] = -1                                             # a missing neighbour
+    W = torch.randn(12, D, device=DEV, requires_grad=True)
+    Ar = torch.randn(L, D, device=DEV, requires_grad=True)
+    pe = torch.randn(L, D, device=DEV)
+    m0 = neighbour_mean_dropout(W, Ar, idx, codes, S, pe, L, 0.0).float()
+    ref = rag_mean_train(W, Ar, idx, codes, S, pe, L).float()
+    torch.testing.assert_close(m0, ref, rtol=2e-2, atol=2e-2)
+    acc = torch.zeros_like(m0)
+    torch.manual_seed(5)
+    n = 200
+    for _ in range(n):
+        acc += neighbour_mean_dropout(W, Ar, idx, codes, S, pe, L, 0.3).float().detach()
+    assert (acc / n - m0.detach()).abs().mean() < 0.05 * m0.abs().mean()
+    out = neighbour_mean_dropout(W, Ar, idx, codes, S, pe, L, 0.3)
+    out.float().sum().backward()
+    assert W.grad[5].abs().sum() > 0 and W.grad[6].abs().sum() > 0 and W.grad[0].abs().sum() == 0
+    assert Ar.grad.abs().sum() > 0
+
+
+def test_train_mode_retrieval_query_dropout():
+    """Train-mode retrieval embeds the queries with dropout (embedding_rag_dataset.py:385-386):
+    with p = 0 the neighbours equal the eval search; with p = 0.1 they stay valid panel rows and
+    mostly agree with the eval neighbours."""
+    from src.dataset.synthetic import make_rag_dataset
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.model import build_model
+    ds, vocab = make_rag_dataset(n_samples=4, n_sites=300, n_windows=1, n_ref_samples=40, seed=2)
+    torch.manual_seed(0)
+    m = build_model(len(vocab), 64, 1, 4).to(DEV)
+    batch = lambda: embedding_rag_collate_fn([ds[i] for i in range(4)])
+    m.eval()
+    ev = ds.process_batch_retrieval(batch(), m.bert.embedding, DEV, k_retrieve=4)["rag_idx_h1"]
+    m.train()
+    emb = m.bert.embedding
+    emb.dropout.p = 0.0
+    tr0 = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4)["rag_idx_h1"]
+    torch.testing.assert_close(tr0, ev, rtol=0, atol=0)
+    emb.dropout.p = 0.1
+    tr = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4)["rag_idx_h1"]
+    assert ((tr >= 0) & (tr < 80)).all()
+    same = np.mean([len(set(a.tolist()) & set(b.tolist())) / 4 for a, b in zip(tr.cpu(), ev.cpu())])
+    assert same >= 0.5
