@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 16
+#define SNVRAG_ABI_VERSION 17
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -360,6 +360,24 @@ int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const voi
 int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
                      int act, float slope, const float* w_out, const float* b_out, float* logits, float* probs,
                      void* stream);
+
+/* Stream GEMM on 32x32x16 MFMAs (csrc/sgemm.hip), bf16, eval: x [M, D] W^T with W [N, D]
+ * packed once by snvrag_sgemm_pack (snvrag_sgemm_pack_bytes(D, N) bytes; D in {128, 256,
+ * 384}, or 768 for epi 0 with GELU (fusion.py:157 over cat(h, g r)); N % 64 == 0), output tiles streamed outermost so each tile's epilogue runs under the
+ * next tiles' MFMAs.  vec (f32) = [bias N | c1 N, c2 N when r1 | LN: g N, be N | head: w_out
+ * [2, N], b_out 2]; rank terms r1[m % period] c1 + r2[m % period] c2 join the bias (the
+ * cat(x, pos, af) / cat(x, af, af_p) Linear inputs of fusion.py:355-360 and
+ * foundation_model.py:25-33 without widening K); r1 = NULL: none.  epi:
+ *   0  out[M, N] = act(.)                      bf16 (act: NONE / GELU)
+ *   1  probs[M, 2] = softmax(act(.) w_out^T + b_out), logits (nullable) [M, 2] f32
+ *      (foundation_model.py:77-80; N = 4D, act GELU, no rank terms)
+ *   2  out[M, D] = LN(act(.) + x) g + be       bf16 (N = D, act LeakyReLU(slope);
+ *      fusion.py:355-360) */
+size_t snvrag_sgemm_pack_bytes(int D, int N);
+int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
+int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,
+                         const void* wstream, const float* vec, const float* r1, const float* r2,
+                         int64_t period, float eps, void* out, float* probs, float* logits, void* stream);
 
 size_t snvrag_encoder_ws_bytes(int dtype, int64_t nseq, int64_t L, int D, int heads);
 int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D, int heads, int n_layers,

@@ -1,0 +1,447 @@
+// Stream GEMM on 32x32x16 bf16 MFMAs (gfx950) for the K = D projections around the encoder:
+//
+//   ACT   out[M, N] = act(x W^T + b + r1[m] c1 + r2[m] c2)      (bf16)
+//   HEAD2 probs[M, 2] = softmax(act(x W^T + b) w_out^T + b_out)  (the 4D hidden never leaves
+//         the registers)
+//   LN    out[M, D] = LN(act(x W^T + b + r1 c1 + r2 c2) + x)     (N = D)
+//
+// with x [M, D], W [N, D], D in {128, 256, 384} (768: ACT + GELU only), N a multiple of 64.  Reference call sites:
+// fusion.py:355-360 (EmbeddingFusionModule: cat(emb, pos, af) -> Linear -> LeakyReLU + emb ->
+// LayerNorm; the pos / af columns as the rank-2 term), fusion.py:131-141 (af_adapter[0] + GELU),
+// foundation_model.py:64-80 (af_fusion[0] over cat(x, af, af_p) + GELU; net[0] + GELU + net[2]
+// + softmax).
+//
+// The block tail's machinery (tail.hip) with the output tiles OUTERMOST: a workgroup owns 128
+// token rows (4 waves x 32, one wave per SIMD), x stays in VGPRs as B fragments for the whole
+// launch, W streams once per workgroup through an 8-slot ring of 16 KiB LDS slabs by LDS-DMA
+// (buffer_load ... lds, counted vmcnt, one barrier per slab).  The stream is ordered by pairs
+// of 32-feature output tiles and, inside a tile, by k-step, so each tile's accumulator is
+// complete after D / 16 MFMAs: the epilogue of pair P - 1 (bias, rank terms, activation, bf16
+// packing and the stores, or the head's 2-logit dot products) is spread between the MFMAs of
+// pair P (ping-pong accumulators), instead of a VALU block after all tiles.  Only 4 live
+// accumulators (64 registers) instead of N / 32 x 16.  Workgroups start at rotated pairs
+// (blockIdx % pairs) so concurrent workgroups read different stream offsets.
+#include "common.h"
+
+#include <utility>
+
+namespace snvrag {
+
+constexpr int SG_FRAG = 1024;              // one A fragment: 32 W rows x 16 k (bf16)
+constexpr int SG_SLAB = 16 * SG_FRAG;
+constexpr int SG_NSLOT = 8;                // ring slots (128 KiB)
+constexpr int SG_PF = 4;                   // A fragments read ahead
+constexpr int SG_ROWS = 128;
+constexpr int SG_VEC_BYTES = 24 * 1024;    // f32 vector table in LDS
+enum { SG_ACT = 0, SG_HEAD2 = 1, SG_LN = 2 };
+
+// feature permutations shared with tail.hip: MFMA row m of an output tile is feature
+// 16((m/4)%2) + 4(m/8) + m%4, so lane (n, hh) holds features 16hh + i (i < 16) of its tile; the
+// k order of x's B fragments and W's columns: k-step s, lane half kh, element j
+__host__ __device__ constexpr int sg_out_feat(int m) { return 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); }
+__host__ __device__ constexpr int sg_in_feat(int s, int kh, int j) { return 32 * (s >> 1) + 16 * kh + 8 * (s & 1) + j; }
+
+__device__ __forceinline__ f32x16 sg_mfma(const u32x4& a, const u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+typedef __bf16 sg_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float sg_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sg_pack2(float a, float b) {          // one v_cvt_pk_bf16_f32
+  const sg_f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, sg_bf16x2));
+}
+__device__ __forceinline__ uint32_t sg_lds(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// LDS reads of the vector table: the reads and their wait in ONE asm statement (a compiler LDS
+// read here would wait for the whole in-flight weight stream).
+// the 8 x 4 floats of one tile PAIR this lane needs from a table at LDS byte address `a` (its
+// tile-0 features): tile t, quad q at a + 128 t + 16 q; ONE wait for the 8 reads
+__device__ __forceinline__ void sg_vec8(uint32_t a, u32x4 (&v)[8]) {
+  asm volatile(
+      "ds_read_b128 %0, %8 offset:0\n ds_read_b128 %1, %8 offset:16\n ds_read_b128 %2, %8 offset:32\n"
+      " ds_read_b128 %3, %8 offset:48\n ds_read_b128 %4, %8 offset:128\n ds_read_b128 %5, %8 offset:144\n"
+      " ds_read_b128 %6, %8 offset:160\n ds_read_b128 %7, %8 offset:176\n s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(a));
+}
+template <typename Body, int... Is>
+__device__ __forceinline__ void sg_unroll(Body&& body, std::integer_sequence<int, Is...>) {
+  (body(std::integral_constant<int, Is>{}), ...);
+}
+template <int ACT> __device__ __forceinline__ float sg_act(float x, float slope) {
+  if constexpr (ACT == SNVRAG_ACT_GELU) return gelu_bf16(x);
+  else if constexpr (ACT == SNVRAG_ACT_LRELU) return x >= 0.f ? x : x * slope;
+  else if constexpr (ACT == SNVRAG_ACT_SIGMOID) return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+  else return x;
+}
+
+struct SgArgs {
+  int M, N;
+  const bf16* x;            // [M, D]
+  bf16* out;                // [M, N] (ACT, LN)
+  const char* ws;           // stream (snvrag_sgemm_pack)
+  const float* vec;         // [bias N | RANK: c1 N, c2 N | LN: g N, be N | HEAD2: w_out 2N, b_out 2]
+  const float* r1; const float* r2; int period;    // rank terms: row scalars r[m % period]
+  float* probs; float* logits;                     // HEAD2 [M, 2] (logits optional)
+  float slope, eps;
+};
+
+template <int EPI, bool RANK> __host__ __device__ constexpr int sg_nvec(int N) {
+  return N * (1 + (RANK ? 2 : 0) + (EPI == SG_LN ? 2 : 0) + (EPI == SG_HEAD2 ? 2 : 0)) + (EPI == SG_HEAD2 ? 2 : 0);
+}
+
+template <int D, int EPI, int ACT, bool RANK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void sg_kernel(SgArgs p) {
+  constexpr int KS = D / 16, NT = D / 32, FPP = 2 * KS;           // fragments per tile pair
+  static_assert(FPP % 16 == 0, "pairs are whole slabs");
+  constexpr int SPP = FPP / 16;                                    // slabs per pair
+  constexpr int RING = SG_NSLOT * SG_SLAB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  float* sv = reinterpret_cast<float*>(smem + RING);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ln = lane & 31, hh = lane >> 5;
+  const int N = p.N, NP = N / 64;                                  // tile pairs
+  const long row = (long)blockIdx.x * SG_ROWS + wave * 32 + ln;
+  const long rc = row < p.M ? row : (long)p.M - 1;
+
+  // ---- vector table -> LDS, x -> B fragments, rank scalars: all plain loads retire before the
+  // DMA ring starts (its waits are counted)
+  const int nvec = sg_nvec<EPI, RANK>(N);
+  for (int i = tid; i < nvec; i += 256) sv[i] = p.vec[i];
+  u32x4 xa[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+  float r1v = 0.f, r2v = 0.f;
+  if constexpr (RANK) {
+    const long ri = rc % p.period;
+    r1v = p.r1[ri];
+    r2v = p.r2[ri];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- weight stream: slab i of the launch = slab i % SPP of pair (rot + i / SPP) % NP
+  // (LN keeps every tile in a compile-time indexed register array: stream order, no rotation)
+  const int rot = EPI == SG_LN ? 0 : (int)(blockIdx.x % NP);
+  const int nslab = NP * SPP;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, nslab * SG_SLAB, 0x00020000);
+  const int voff = lane * 16;
+  int is_slot = 0, is_i = 0;
+  auto issue_next = [&]() {
+    auto* dst = (__attribute__((address_space(3))) char*)(ring + is_slot + wave * 4 * SG_FRAG);
+    const int pi = is_i / SPP, j = is_i - pi * SPP;
+    int pr = rot + pi;
+    pr = pr % NP;                                   // issues run past the end: the stream wraps
+    const int src = (pr * SPP + j) * SG_SLAB;
+    ++is_i;
+    sg_unroll([&](auto jc) {
+      constexpr int q = decltype(jc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, dst + q * SG_FRAG, 16, voff, src + (wave * 4 + q) * SG_FRAG, 0, 0);
+    }, std::make_integer_sequence<int, 4>{});
+    is_slot = is_slot + SG_SLAB == RING ? 0 : is_slot + SG_SLAB;
+  };
+#pragma unroll
+  for (int g = 0; g < SG_NSLOT - 1; ++g) issue_next();
+  static_assert(4 * (SG_NSLOT - 2) <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 2)) : "memory");
+  __syncthreads();                                   // slab 0 and the vector table visible
+
+  int rd_slot = 0;
+  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {
+    constexpr int j = decltype(j_tag)::value, fi = decltype(fi_tag)::value;
+    int so = rd_slot + j * SG_SLAB;
+    so = so >= RING ? so - RING : so;
+    return *reinterpret_cast<const u32x4*>(ring + so + lane * 16 + fi * SG_FRAG);
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 3)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_next();                                    // into the slot of the slab two behind
+  };
+  u32x4 a[SG_PF];
+  sg_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
+            std::make_integer_sequence<int, SG_PF>{});
+  // consume one tile pair (FPP fragments, whole slabs): mma(f, A) per fragment, LDS reads PF ahead
+  auto run = [&](auto&& mma) {
+    sg_unroll([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      const u32x4 cur = a[f % SG_PF];
+      if constexpr ((f & 15) == 16 - SG_PF) {
+        __builtin_amdgcn_sched_barrier(0);
+        sync();
+      }
+      mma(fc, cur);
+      constexpr int qn = f + SG_PF;
+      a[f % SG_PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }, std::make_integer_sequence<int, FPP>{});
+    rd_slot += SPP * SG_SLAB;
+    rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
+  };
+  const uint32_t sv_lane = sg_lds(sv) + 64 * hh;    // &sv[16 hh]
+  // the pair's epilogue vectors (bias, rank columns, head weights) for this lane's features,
+  // read in blocks of 8 with one wait each — NOT one wait per 4 features in the MFMA stream
+  struct PairVec {
+    u32x4 b[8], c1[8], c2[8];
+  };
+  auto load_vec = [&](int pp, PairVec& v) {
+    const uint32_t a = sv_lane + 4 * 64 * pp;
+    sg_vec8(a, v.b);
+    if constexpr (RANK || EPI == SG_HEAD2) {         // c1 / c2, or the head's w_out rows
+      sg_vec8(a + 4 * N, v.c1);
+      sg_vec8(a + 8 * N, v.c2);
+    }
+  };
+  // y = act(acc + bias + rank) of features 4q .. 4q + 3 (+16 hh) of tile t of the pair
+  auto pre = [&](const f32x16& acc, const PairVec& v, int t, int q, float (&y)[4]) {
+    const int k = 4 * t + q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = acc[4 * q + e] + __uint_as_float(v.b[k][e]);
+      if constexpr (RANK) x = fmaf(r2v, __uint_as_float(v.c2[k][e]), fmaf(r1v, __uint_as_float(v.c1[k][e]), x));
+      y[e] = sg_act<ACT>(x, p.slope);
+    }
+  };
+
+  if constexpr (EPI == SG_LN) {
+    // ---- N = D: every tile kept (v = act(.) + x), then the row LayerNorm
+    f32x16 acc[NT];
+    float sum = 0.f, sq = 0.f;
+    sg_unroll([&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      run([&](auto fc, const u32x4& A) {
+        constexpr int f = decltype(fc)::value, T = 2 * P + f / KS, s = f % KS;
+        if constexpr (s == 0) acc[T] = sg_mfma(A, xa[0], f32x16{});
+        else acc[T] = sg_mfma(A, xa[s], acc[T]);
+      });
+    }, std::make_integer_sequence<int, NT / 2>{});
+    PairVec pv;
+#pragma unroll
+    for (int T = 0; T < NT; ++T)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if ((T & 1) == 0 && q == 0) load_vec(T >> 1, pv);
+        float y[4];
+        pre(acc[T], pv, T & 1, q, y);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * q + e;                   // feature 32T + 16hh + i = x's k-step 2T + i/8, j = i%8
+          const uint32_t w = xa[2 * T + (i >> 3)][(i & 7) >> 1];
+          const float v = y[e] + ((i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16));
+          acc[T][i] = v;
+          sum += v;
+          sq = fmaf(v, v, sq);
+        }
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    const float mean = sum * (1.0f / D);
+    const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stream overrun has landed
+    if (row < p.M) {
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        float y[16];
+        if ((T & 1) == 0) {                          // g, be of the pair's two tiles
+          const uint32_t a = sv_lane + 4 * (32 * T + (RANK ? 3 : 1) * N);
+          sg_vec8(a, pv.b);
+          sg_vec8(a + 4 * N, pv.c1);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = 4 * (T & 1) + q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            y[4 * q + e] = fmaf((acc[T][4 * q + e] - mean) * rstd, __uint_as_float(pv.b[k][e]), __uint_as_float(pv.c1[k][e]));
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          *reinterpret_cast<u32x4*>(p.out + row * D + 32 * T + 16 * hh + 8 * h2) =
+              u32x4{sg_pack2(y[8 * h2], y[8 * h2 + 1]), sg_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                    sg_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), sg_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+      }
+    }
+    return;
+  } else {
+    // ---- ACT / HEAD2: pairs of tiles with ping-pong accumulators; the epilogue of the previous
+    // pair in 8 steps of 4 features (step k: tile k / 4, quad k % 4) between this pair's MFMAs
+    const long out_bytes = EPI == SG_ACT ? (long)p.M * N * 2 : 16;
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.out, (short)0, (int)(out_bytes < 0x7fffffffL ? out_bytes : 0x7fffffffL), 0x00020000);
+    const int row_off = EPI == SG_ACT ? (int)(row * N + 16 * hh) * 2 : 0;   // bytes (row < 2^31 / 2N)
+    float l0 = 0.f, l1 = 0.f;                        // HEAD2 partial logits
+    u32x4 yo;
+    PairVec pv;
+    auto epi_step = [&](const f32x16 (&acc)[2], int pp, int k) {
+      const int t = k >> 2, q = k & 3;
+      const int fb = 32 * (2 * pp + t) + 4 * q;     // this lane's features fb .. fb + 3 (+16 hh)
+      float y[4];
+      pre(acc[t], pv, t, q, y);
+      if constexpr (EPI == SG_ACT) {
+        yo[2 * (q & 1)] = sg_pack2(y[0], y[1]);
+        yo[2 * (q & 1) + 1] = sg_pack2(y[2], y[3]);
+        if (q & 1) __builtin_amdgcn_raw_buffer_store_b128(yo, ors, row_off + 2 * (fb - 4), 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          l0 = fmaf(y[e], __uint_as_float(pv.c1[k][e]), l0);
+          l1 = fmaf(y[e], __uint_as_float(pv.c2[k][e]), l1);
+        }
+      }
+    };
+    constexpr int EVERY = FPP / 8;                   // one epilogue step per EVERY MFMAs
+    auto pair = [&](int P, f32x16 (&an)[2], const f32x16 (&ap)[2], auto prev_tag) {
+      constexpr bool PREV = decltype(prev_tag)::value;
+      const int pp_prev = (rot + P - 1 + NP) % NP;
+      if constexpr (PREV) load_vec(pp_prev, pv);
+      run([&](auto fc, const u32x4& A) {
+        constexpr int f = decltype(fc)::value, t = f / KS, s = f % KS;
+        if constexpr (s == 0) an[t] = sg_mfma(A, xa[0], f32x16{});
+        else an[t] = sg_mfma(A, xa[s], an[t]);
+        if constexpr (PREV && f % EVERY == 0) epi_step(ap, pp_prev, f / EVERY);
+      });
+    };
+    f32x16 e0[2], e1[2];
+    pair(0, e0, e1, std::false_type{});
+    int P = 1;
+#pragma unroll 1
+    for (; P + 1 < NP; P += 2) {
+      pair(P, e1, e0, std::true_type{});
+      pair(P + 1, e0, e1, std::true_type{});
+    }
+    const int pl = (rot + NP - 1) % NP;               // stream index of the last pair
+    if (P < NP) {
+      pair(P, e1, e0, std::true_type{});
+      load_vec(pl, pv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) epi_step(e1, pl, k);
+    } else {
+      load_vec(pl, pv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) epi_step(e0, pl, k);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stores + the stream overrun retired
+    if constexpr (EPI == SG_HEAD2) {
+      l0 += __shfl_xor(l0, 32, 64);
+      l1 += __shfl_xor(l1, 32, 64);
+      if (hh == 0 && row < p.M) {
+        const float2 bo = *reinterpret_cast<const float2*>(p.vec + (RANK ? 5 : 3) * N);
+        l0 += bo.x;
+        l1 += bo.y;
+        const float mx = fmaxf(l0, l1);
+        const float e0v = __expf(l0 - mx), e1v = __expf(l1 - mx), inv = 1.0f / (e0v + e1v);
+        reinterpret_cast<float2*>(p.probs)[row] = make_float2(e0v * inv, e1v * inv);
+        if (p.logits) reinterpret_cast<float2*>(p.logits)[row] = make_float2(l0, l1);
+      }
+    }
+  }
+}
+
+// One thread per 16-byte piece (8 bf16) of the stream: fragment F = T KS + s (output tile T, k-step
+// s), lane l = (m = l % 32, kh = l / 32) holds W[32T + sg_out_feat(m)][sg_in_feat(s, kh, 0 .. 7)].
+__global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w, bf16* __restrict__ out) {
+  const long pc = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pc >= n_pieces) return;
+  const int KS = D / 16;
+  const long F = pc / 64;
+  const int l = (int)(pc % 64), m = l & 31, kh = l >> 5;
+  const long T = F / KS;
+  const int s = (int)(F % KS);
+  const long n = 32 * T + sg_out_feat(m);
+  for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w[n * D + sg_in_feat(s, kh, j)];
+}
+
+template <int D, int EPI, int ACT, bool RANK>
+static int sg_launch(const SgArgs& a, hipStream_t s) {
+  auto kern = sg_kernel<D, EPI, ACT, RANK>;
+  const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
+  static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, SG_ROWS)), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int D>
+static int sg_dispatch(int epi, int act, bool rank, const SgArgs& a, hipStream_t s) {
+  if (epi == SG_HEAD2) {
+    if (act == SNVRAG_ACT_GELU) return sg_launch<D, SG_HEAD2, SNVRAG_ACT_GELU, false>(a, s);
+    return fail("snvrag_sgemm_forward", "head epilogue supports GELU only");
+  }
+  if (epi == SG_LN) {
+    if (act == SNVRAG_ACT_LRELU) {
+      return rank ? sg_launch<D, SG_LN, SNVRAG_ACT_LRELU, true>(a, s) : sg_launch<D, SG_LN, SNVRAG_ACT_LRELU, false>(a, s);
+    }
+    return fail("snvrag_sgemm_forward", "LayerNorm epilogue supports LeakyReLU only");
+  }
+  switch (act) {
+    case SNVRAG_ACT_NONE: return rank ? sg_launch<D, SG_ACT, SNVRAG_ACT_NONE, true>(a, s)
+                                      : sg_launch<D, SG_ACT, SNVRAG_ACT_NONE, false>(a, s);
+    case SNVRAG_ACT_GELU: return rank ? sg_launch<D, SG_ACT, SNVRAG_ACT_GELU, true>(a, s)
+                                      : sg_launch<D, SG_ACT, SNVRAG_ACT_GELU, false>(a, s);
+    default: return fail("snvrag_sgemm_forward", "activation epilogue supports none / GELU");
+  }
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" size_t snvrag_sgemm_pack_bytes(int D, int N) {
+  if (!(D == 128 || D == 256 || D == 384 || D == 768) || N <= 0 || N % 64) return 0;
+  return (size_t)N * D * 2;
+}
+
+extern "C" int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream) {
+  SNV_CHECK_ARG(snvrag_sgemm_pack_bytes(D, N) > 0, "stream GEMM needs D in {128, 256, 384, 768} and N % 64 == 0");
+  SNV_CHECK_ARG(w && out, "null pointer");
+  const long pieces = (long)N * D / 8;
+  hipLaunchKernelGGL(sg_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
+                     (const bf16*)w, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,
+                                    const void* wstream, const float* vec, const float* r1, const float* r2,
+                                    int64_t period, float eps, void* out, float* probs, float* logits,
+                                    void* stream) {
+  SNV_CHECK_ARG(snvrag_sgemm_pack_bytes(D, N) > 0, "stream GEMM needs D in {128, 256, 384, 768} and N % 64 == 0");
+  SNV_CHECK_ARG(epi == SG_ACT || epi == SG_HEAD2 || epi == SG_LN, "bad epilogue");
+  SNV_CHECK_ARG(x && wstream && vec, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  const bool rank = r1 != nullptr;
+  SNV_CHECK_ARG(!rank || (r2 && period > 0), "rank terms need r1, r2 and a period");
+  SNV_CHECK_ARG(epi != SG_HEAD2 || (!rank && N == 4 * D && probs), "head epilogue: no rank terms, N = 4D, probs");
+  SNV_CHECK_ARG(epi != SG_LN || (N == D && out), "LayerNorm epilogue needs N = D and out");
+  SNV_CHECK_ARG(epi != SG_ACT || out, "null output");
+  SNV_CHECK_ARG(epi != SG_ACT || M * N * 2 < (1L << 31), "output exceeds the 2 GiB buffer-store range");
+  const int nvec = rank ? (epi == SG_LN ? sg_nvec<SG_LN, true>(N) : sg_nvec<SG_ACT, true>(N))
+                        : (epi == SG_LN ? sg_nvec<SG_LN, false>(N)
+                                        : epi == SG_HEAD2 ? sg_nvec<SG_HEAD2, false>(N) : sg_nvec<SG_ACT, false>(N));
+  SNV_CHECK_ARG(nvec * 4 <= SG_VEC_BYTES, "vector table exceeds the LDS budget");
+  SNV_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)wstream % 16) == 0 && (!out || ((uintptr_t)out % 16) == 0),
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  const SgArgs a{(int)M, N, (const bf16*)x, (bf16*)out, (const char*)wstream, vec, r1, r2, (int)period,
+                 probs, logits, slope, eps};
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  int rc;
+  switch (D) {
+    case 128: rc = sg_dispatch<128>(epi, act, rank, a, s); break;
+    case 256: rc = sg_dispatch<256>(epi, act, rank, a, s); break;
+    case 384: rc = sg_dispatch<384>(epi, act, rank, a, s); break;
+    default:                                         // K = 2D: the rag fusion's cat(h, g * r) input
+      if (epi != SG_ACT || act != SNVRAG_ACT_GELU || rank)
+        return fail(__func__, "K = 768 supports the GELU activation epilogue only");
+      rc = sg_launch<768, SG_ACT, SNVRAG_ACT_GELU, false>(a, s);
+      break;
+  }
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)N * D);
+  return 0;
+}

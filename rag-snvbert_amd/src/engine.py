@@ -141,6 +141,11 @@ class Engine:
         P.ef = dict(w=cvt(fw[:, :D]), c_pos=fw[:, D].contiguous(), c_af=fw[:, D + 1].contiguous(),
                     b=f32(ef.fusion.bias), g=f32(ef.norm.weight), bb=f32(ef.norm.bias))
         ws_ok = use_ws and D in (128, 256, 384)
+        # stream GEMM (csrc/sgemm.hip, 32x32 MFMAs, tile epilogues under the next tiles' MFMAs)
+        sg_ok = ws_ok and os.environ.get("SNVRAG_NO_SG") is None
+        if sg_ok:
+            P.ef["w_sg"] = K.sgemm_pack(P.ef["w"])
+            P.ef["v_sg"] = K.sgemm_vec(P.ef["b"], P.ef["c_pos"], P.ef["c_af"], ln=(P.ef["g"], P.ef["bb"]))
         # (emb_fusion stays on the row-panel GEMM: at N = K = D over 4B*L rows the
         #  weight-streaming LN epilogue measured 4 % slower)
         pf = ef.pos_feat
@@ -162,7 +167,11 @@ class Engine:
                     f3=cvt(rf.fusion[3].weight), f3b=f32(rf.fusion[3].bias),
                     g=f32(rf.fusion[4].weight), bb=f32(rf.fusion[4].bias),
                     rs=float(rf.res_scale.detach().float().item()))
-        if ws_ok and P.rf["a0"].shape == (4 * D, D):
+        if sg_ok and D == 384 and P.rf["f0"].shape == (4 * D, 2 * D):
+            P.rf["f0_sg"], P.rf["f0_v"] = K.sgemm_pack(P.rf["f0"]), K.sgemm_vec(P.rf["f0b"])
+        if sg_ok and P.rf["a0"].shape == (4 * D, D):
+            P.rf["a0_sg"], P.rf["a0_v"] = K.sgemm_pack(P.rf["a0"]), K.sgemm_vec(P.rf["a0b"])
+        elif ws_ok and P.rf["a0"].shape == (4 * D, D):
             P.rf["a0_ws"] = K.wsg_pack(P.rf["a0"])
         # encoder
         P.layers_t, P.layers = [], []
@@ -206,9 +215,16 @@ class Engine:
                     g=f32(hc.af_fusion[3].weight), bb=f32(hc.af_fusion[3].bias),
                     n0=cvt(hc.net[0].weight), n0b=f32(hc.net[0].bias),
                     n2=f32(hc.net[2].weight), n2b=f32(hc.net[2].bias))
-        if ws_ok and P.hh["w0"].shape == (4 * D, D):
+        if sg_ok and P.hh["w0"].shape == (4 * D, D):
+            P.hh["w0_sg"] = K.sgemm_pack(P.hh["w0"])
+            P.hh["w0_v"] = K.sgemm_vec(P.hh["b0"], P.hh["c_af"], P.hh["c_afp"])
+        elif ws_ok and P.hh["w0"].shape == (4 * D, D):
             P.hh["w0_ws"] = K.wsg_pack(P.hh["w0"])
-        if ws_ok and P.hh["n2"].shape[0] == 2:
+        if sg_ok and P.hh["n2"].shape[0] == 2 and P.hh["n0"].shape == (4 * D, D):
+            # net[0] + GELU + net[2] + softmax on the stream GEMM's head epilogue
+            P.hh["n0_sg"] = K.sgemm_pack(P.hh["n0"])
+            P.hh["n0_v"] = K.sgemm_vec(P.hh["n0b"], head=(P.hh["n2"], P.hh["n2b"]))
+        elif ws_ok and P.hh["n2"].shape[0] == 2:
             # fused net[0] + GELU + net[2] + softmax (csrc/wsgemm.hip, EPI 2)
             P.hh["n0_ws"] = K.wsg_pack(P.hh["n0"])
         gc = fm.gt_classifier
@@ -293,7 +309,10 @@ class Engine:
             hm[2 * B:].copy_(rag)
         pf = K.posfeat(pos, P.pf)                                     # [B, L]
         ef = P.ef
-        if "w_ws" in ef:
+        if "w_sg" in ef:
+            fused = K.sgemm(hm, ef["w_sg"], D, ef["v_sg"], epi=K.SG_LN, act=N.ACT_LRELU, slope=0.1,
+                            rank=(pf, af, BL))
+        elif "w_ws" in ef:
             fused = K.wsg_linear(hm, ef["w_ws"], D, ef["b"], act=N.ACT_LRELU, slope=0.1, resid=hm,
                                  ln=(ef["g"], ef["bb"]), row1=(pf, ef["c_pos"]), row2=(af, ef["c_af"]), row_period=BL)
         else:
@@ -302,13 +321,18 @@ class Engine:
         if rag is not None:
             rf = P.rf
             fa = K.af_gate(af, af_p, P.ag, D, T)                      # [B, L, D]
-            if "a0_ws" in rf:
+            if "a0_sg" in rf:
+                t = K.sgemm(fa, rf["a0_sg"], rf["a0"].shape[0], rf["a0_v"], act=N.ACT_GELU)
+            elif "a0_ws" in rf:
                 t = K.wsg_linear(fa, rf["a0_ws"], rf["a0"].shape[0], rf["a0b"], act=N.ACT_GELU)
             else:
                 t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
             aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
             cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
-            h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
+            if "f0_sg" in rf:
+                h = K.sgemm(cat, rf["f0_sg"], rf["f0"].shape[0], rf["f0_v"], act=N.ACT_GELU)
+            else:
+                h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
             xx = K.linear(h, rf["f3"], rf["f3b"], ln=(rf["g"], rf["bb"]), post_base=fused[:2 * B],
                           post_scale=rf["rs"], post_af=af, post_af_period=BL, post_maf=True)
         else:
@@ -326,14 +350,20 @@ class Engine:
         B, L = o["B"], o["L"]
         BL = B * L
         hh = P.hh
-        if "w0_ws" in hh:
+        if "w0_sg" in hh:
+            h = K.sgemm(o["x_all"], hh["w0_sg"], hh["w0"].shape[0], hh["w0_v"], act=N.ACT_GELU,
+                        rank=(o["af"], o["af_p"], BL))
+        elif "w0_ws" in hh:
             h = K.wsg_linear(o["x_all"], hh["w0_ws"], hh["w0"].shape[0], hh["b0"], act=N.ACT_GELU,
                              row1=(o["af"], hh["c_af"]), row2=(o["af_p"], hh["c_afp"]), row_period=BL)
         else:
             h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
                          row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
         h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
-        if "n0_ws" in hh:
+        if "n0_sg" in hh:
+            logits, probs = K.sgemm(h, hh["n0_sg"], hh["n0"].shape[0], hh["n0_v"], epi=K.SG_HEAD2, act=N.ACT_GELU,
+                                    want_logits=want_logits)
+        elif "n0_ws" in hh:
             logits, probs = K.wsg_head2(h, hh["n0_ws"], hh["n0"].shape[0], hh["n0b"], hh["n2"], hh["n2b"],
                                         act=N.ACT_GELU, want_logits=want_logits)
         else:

@@ -597,6 +597,65 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+SG_ACT, SG_HEAD2, SG_LN = 0, 1, 2
+
+
+def sgemm_pack(w: torch.Tensor) -> torch.Tensor:
+    """Tile-major fragment stream of W [N, D] for the stream GEMM (csrc/sgemm.hip)."""
+    N.require_gpu(w)
+    Nn, D = w.shape
+    nbytes = int(N.lib().snvrag_sgemm_pack_bytes(D, Nn))
+    if nbytes == 0:
+        raise ValueError(f"stream GEMM needs D in (128, 256, 384) and N % 64 == 0, got {tuple(w.shape)}")
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    check(N.lib().snvrag_sgemm_pack(D, Nn, ptr(_c(w.to(torch.bfloat16).contiguous())), ptr(out), stream_ptr()),
+          "sgemm_pack")
+    return out
+
+
+def sgemm_vec(bias: torch.Tensor, c1: Optional[torch.Tensor] = None, c2: Optional[torch.Tensor] = None,
+              ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+              head: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """f32 vector table of :func:`sgemm`: [bias | c1, c2 | ln g, b | head w_out [2, N], b_out [2]]."""
+    parts = [bias]
+    if c1 is not None:
+        parts += [c1, c2]
+    if ln is not None:
+        parts += list(ln)
+    if head is not None:
+        parts += [head[0].reshape(-1), head[1].reshape(-1)]
+    return torch.cat([t.detach().float().reshape(-1) for t in parts]).contiguous()
+
+
+def sgemm(x: torch.Tensor, wstream: torch.Tensor, n_out: int, vec: torch.Tensor, *, epi: int = SG_ACT,
+          act: int = N.ACT_NONE, slope: float = 0.0,
+          rank: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None, eps: float = 1e-5,
+          out: Optional[torch.Tensor] = None, want_logits: bool = False):
+    """Stream GEMM (bf16): SG_ACT -> act(x W^T + b [+ r1 c1 + r2 c2]) [..., n_out] bf16;
+    SG_LN -> LN(act(.) + x) [..., D] bf16; SG_HEAD2 -> (logits or None, probs) [..., 2] f32.
+    ``rank = (r1 f32, r2 f32, period)``: row scalars indexed by row % period."""
+    N.require_gpu(x)
+    assert x.dtype == torch.bfloat16
+    D = x.shape[-1]
+    M = x.numel() // D
+    probs = logits = None
+    if epi == SG_HEAD2:
+        probs = torch.empty(*x.shape[:-1], 2, device=x.device, dtype=torch.float32)
+        logits = torch.empty_like(probs) if want_logits else None
+    elif out is None:
+        out = torch.empty(*x.shape[:-1], n_out, device=x.device, dtype=torch.bfloat16)
+    r1 = r2 = None
+    period = 0
+    if rank is not None:
+        r1, r2 = _c(rank[0].float()), _c(rank[1].float())
+        period = int(rank[2])
+        assert r1.numel() >= period and r2.numel() >= period and period > 0
+    check(N.lib().snvrag_sgemm_forward(M, D, n_out, epi, act, slope, ptr(_c(x)), ptr(wstream), ptr(vec), ptr(r1),
+                                       ptr(r2), period, eps, ptr(out), ptr(probs), ptr(logits), stream_ptr()),
+          "sgemm")
+    return (logits, probs) if epi == SG_HEAD2 else out
+
+
 def wsg_pack(w: torch.Tensor) -> torch.Tensor:
     """Fragment-ordered bf16 weight stream of the weight-streaming GEMM (csrc/wsgemm.hip)."""
     Nn, Kk = w.shape

@@ -517,6 +517,52 @@ def test_weight_streaming_head2(M, Kd):
     torch.testing.assert_close(probs, torch.softmax(ref_l, -1), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,Kd,mode", [(1000, 1152, 384, "plain"), (517, 1536, 384, "gelu"), (77, 512, 128, "gelu"),
+                                        (300, 64, 256, "plain"), (900, 1536, 384, "rank_gelu"),
+                                        (1203, 384, 384, "rank_lrelu_ln"), (260, 128, 128, "rank_lrelu_ln"),
+                                        (129, 256, 256, "lrelu_ln"), (4133, 1536, 384, "head2"),
+                                        (1, 1024, 256, "head2"), (130, 512, 128, "head2"), (999, 1536, 768, "gelu")])
+def test_stream_gemm(M, N, Kd, mode):
+    """snvrag_sgemm_forward (csrc/sgemm.hip: tile-major weight stream, tile epilogues under the next
+    tiles' MFMAs) vs torch fp32 on the same bf16 operands; ragged M, 1..3 pairs per slab cycle,
+    the rotated pair order (blockIdx % pairs) and the three epilogues."""
+    from src import native as NN
+    g = torch.Generator(device="cpu").manual_seed(M + N + Kd)
+    x = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    ws = K().sgemm_pack(w)
+    ref = x.float() @ w.float().t() + b
+    rank, c = None, (None, None)
+    if mode.startswith("rank"):
+        period = (M + 2) // 3
+        r1, r2 = torch.rand(period, generator=g).to(DEV), torch.rand(period, generator=g).to(DEV)
+        c = (torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV))
+        ri = torch.arange(M, device=DEV) % period
+        ref = ref + r1[ri, None] * c[0][None] + r2[ri, None] * c[1][None]
+        rank = (r1, r2, period)
+    if mode == "head2":
+        w2 = (torch.randn(2, N, generator=g) / math.sqrt(N)).to(DEV)
+        b2 = torch.randn(2, generator=g).to(DEV)
+        ref_l = torch.nn.functional.gelu(ref) @ w2.t() + b2
+        logits, probs = K().sgemm(x, ws, N, K().sgemm_vec(b, head=(w2, b2)), epi=K().SG_HEAD2, act=NN.ACT_GELU,
+                                  want_logits=True)
+        torch.testing.assert_close(logits, ref_l, rtol=1e-3, atol=2e-3)
+        torch.testing.assert_close(probs, torch.softmax(ref_l, -1), rtol=1e-3, atol=1e-3)
+        return
+    if mode.endswith("ln"):
+        gm, bt = torch.rand(N, generator=g).to(DEV) + 0.5, torch.randn(N, generator=g).to(DEV)
+        ref = torch.nn.functional.layer_norm(torch.nn.functional.leaky_relu(ref, 0.1) + x.float(), (N,), gm, bt, 1e-5)
+        out = K().sgemm(x, ws, N, K().sgemm_vec(b, *c, ln=(gm, bt)), epi=K().SG_LN, act=NN.ACT_LRELU, slope=0.1,
+                        rank=rank)
+    else:
+        act = NN.ACT_GELU if "gelu" in mode else NN.ACT_NONE
+        if act == NN.ACT_GELU:
+            ref = torch.nn.functional.gelu(ref)
+        out = K().sgemm(x, ws, N, K().sgemm_vec(b, *c), act=act, rank=rank)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("n,bits,k,nq", [(5008, 2040, 32, 37), (300, 33, 5, 3), (20, 1020, 32, 4)])
 def test_raw_genotype_index_vs_oracle(n, bits, k, nq):
     """Raw-genotype window index (csrc/rawdb.hip + topk_merge; build_ref_db_l2.py:86-89 IndexFlatL2
