@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 17
+#define SNVRAG_ABI_VERSION 18
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -283,6 +283,10 @@ typedef struct {
   /* optional (bf16, D in {128,256,384}): snvrag_proj_pack of w_qkv (NC = 3) -> the QKV
    * projection runs on snvrag_proj_forward; takes precedence over qkv_ws */
   const void* qkv_pw;
+  /* optional (bf16, D in {128,256,384}): snvrag_sgemm_pack of w_qkv -> the QKV projection runs on
+   * the stream GEMM (snvrag_sgemm_forward, epi 0); takes precedence over qkv_pw while
+   * M * 3D * 2 bytes < 2^31 */
+  const void* qkv_sg;
 } snvrag_layer_t;
 
 /* ------------------------------------------------------------------------

@@ -80,7 +80,10 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       snvrag_epilogue_t e{};
       int rc;
       e.bias = ly.b_qkv;
-      if (dtype == SNVRAG_BF16 && ly.qkv_pw && !getenv("SNVRAG_NO_PROJ"))
+      if (dtype == SNVRAG_BF16 && ly.qkv_sg && M * 3 * D * 2 < (1L << 31))
+        rc = snvrag_sgemm_forward(M, (int)D, (int)(3 * D), 0, SNVRAG_ACT_NONE, 0.f, xc, ly.qkv_sg, ly.b_qkv, nullptr,
+                                  nullptr, 0, 0.f, qkv, nullptr, nullptr, stream);
+      else if (dtype == SNVRAG_BF16 && ly.qkv_pw && !getenv("SNVRAG_NO_PROJ"))
         rc = snvrag_proj_forward(M, D, 3, xc, ly.qkv_pw, ly.b_qkv, qkv, stream);
       else if (dtype == SNVRAG_BF16 && ly.qkv_ws && !getenv("SNVRAG_NO_WSG"))
         rc = snvrag_wsg_forward(M, 3 * D, D, xc, ly.qkv_ws, ly.b_qkv, SNVRAG_ACT_NONE, 0.f, nullptr, 0, nullptr,

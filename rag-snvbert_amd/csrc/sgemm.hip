@@ -31,7 +31,6 @@ constexpr int SG_FRAG = 1024;              // one A fragment: 32 W rows x 16 k (
 constexpr int SG_SLAB = 16 * SG_FRAG;
 constexpr int SG_NSLOT = 8;                // ring slots (128 KiB)
 constexpr int SG_PF = 4;                   // A fragments read ahead
-constexpr int SG_ROWS = 128;
 constexpr int SG_VEC_BYTES = 24 * 1024;    // f32 vector table in LDS
 enum { SG_ACT = 0, SG_HEAD2 = 1, SG_LN = 2 };
 
@@ -91,12 +90,16 @@ template <int EPI, bool RANK> __host__ __device__ constexpr int sg_nvec(int N) {
   return N * (1 + (RANK ? 2 : 0) + (EPI == SG_LN ? 2 : 0) + (EPI == SG_HEAD2 ? 2 : 0)) + (EPI == SG_HEAD2 ? 2 : 0);
 }
 
-template <int D, int EPI, int ACT, bool RANK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void sg_kernel(SgArgs p) {
+// WAVES = 4: 128 rows per workgroup, one wave per SIMD (512 registers); WAVES = 8: 256 rows, two
+// waves per SIMD (256 registers each) — every streamed weight byte feeds twice the rows.
+template <int D, int EPI, int ACT, bool RANK, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
+void sg_kernel(SgArgs p) {
   constexpr int KS = D / 16, NT = D / 32, FPP = 2 * KS;           // fragments per tile pair
   static_assert(FPP % 16 == 0, "pairs are whole slabs");
   constexpr int SPP = FPP / 16;                                    // slabs per pair
   constexpr int RING = SG_NSLOT * SG_SLAB;
+  constexpr int NTH = 64 * WAVES, ROWS = 32 * WAVES, PPW = 16 / WAVES;   // pieces per wave per slab
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;
   float* sv = reinterpret_cast<float*>(smem + RING);
@@ -104,13 +107,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, lane = tid & 63;
   const int ln = lane & 31, hh = lane >> 5;
   const int N = p.N, NP = N / 64;                                  // tile pairs
-  const long row = (long)blockIdx.x * SG_ROWS + wave * 32 + ln;
+  const long row = (long)blockIdx.x * ROWS + wave * 32 + ln;
   const long rc = row < p.M ? row : (long)p.M - 1;
 
   // ---- vector table -> LDS, x -> B fragments, rank scalars: all plain loads retire before the
   // DMA ring starts (its waits are counted)
   const int nvec = sg_nvec<EPI, RANK>(N);
-  for (int i = tid; i < nvec; i += 256) sv[i] = p.vec[i];
+  for (int i = tid; i < nvec; i += NTH) sv[i] = p.vec[i];
   u32x4 xa[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int voff = lane * 16;
   int is_slot = 0, is_i = 0;
   auto issue_next = [&]() {
-    auto* dst = (__attribute__((address_space(3))) char*)(ring + is_slot + wave * 4 * SG_FRAG);
+    auto* dst = (__attribute__((address_space(3))) char*)(ring + is_slot + wave * PPW * SG_FRAG);
     const int pi = is_i / SPP, j = is_i - pi * SPP;
     int pr = rot + pi;
     pr = pr % NP;                                   // issues run past the end: the stream wraps
@@ -138,14 +141,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ++is_i;
     sg_unroll([&](auto jc) {
       constexpr int q = decltype(jc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, dst + q * SG_FRAG, 16, voff, src + (wave * 4 + q) * SG_FRAG, 0, 0);
-    }, std::make_integer_sequence<int, 4>{});
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, dst + q * SG_FRAG, 16, voff, src + (wave * PPW + q) * SG_FRAG, 0, 0);
+    }, std::make_integer_sequence<int, PPW>{});
     is_slot = is_slot + SG_SLAB == RING ? 0 : is_slot + SG_SLAB;
   };
 #pragma unroll
   for (int g = 0; g < SG_NSLOT - 1; ++g) issue_next();
-  static_assert(4 * (SG_NSLOT - 2) <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 2)) : "memory");
+  static_assert(PPW * (SG_NSLOT - 2) <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (SG_NSLOT - 2)) : "memory");
   __syncthreads();                                   // slab 0 and the vector table visible
 
   int rd_slot = 0;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     return *reinterpret_cast<const u32x4*>(ring + so + lane * 16 + fi * SG_FRAG);
   };
   auto sync = [&]() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 3)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW * (SG_NSLOT - 3)) : "memory");
     __builtin_amdgcn_s_barrier();
     issue_next();                                    // into the slot of the slab two behind
   };
@@ -184,26 +187,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint32_t sv_lane = sg_lds(sv) + 64 * hh;    // &sv[16 hh]
   // the pair's epilogue vectors (bias, rank columns, head weights) for this lane's features,
   // read in blocks of 8 with one wait each — NOT one wait per 4 features in the MFMA stream
+  // b = bias + r1 c1 + r2 c2 (r1, r2: this lane's row scalars, so the rank terms fold into the
+  // pair's bias once); c1 / c2 keep the head's w_out rows (HEAD2) or the LN g / be (LN, at the end)
   struct PairVec {
-    u32x4 b[8], c1[8], c2[8];
+    u32x4 b[8], c1[EPI == SG_ACT ? 1 : 8], c2[EPI == SG_ACT ? 1 : 8];
   };
   auto load_vec = [&](int pp, PairVec& v) {
     const uint32_t a = sv_lane + 4 * 64 * pp;
     sg_vec8(a, v.b);
-    if constexpr (RANK || EPI == SG_HEAD2) {         // c1 / c2, or the head's w_out rows
+    if constexpr (RANK) {
+      u32x4 c[8];
+      sg_vec8(a + 4 * N, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v.b[k][e] = __float_as_uint(fmaf(r1v, __uint_as_float(c[k][e]), __uint_as_float(v.b[k][e])));
+      sg_vec8(a + 8 * N, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v.b[k][e] = __float_as_uint(fmaf(r2v, __uint_as_float(c[k][e]), __uint_as_float(v.b[k][e])));
+    }
+    if constexpr (EPI == SG_HEAD2) {                 // the head's w_out rows
       sg_vec8(a + 4 * N, v.c1);
       sg_vec8(a + 8 * N, v.c2);
     }
   };
-  // y = act(acc + bias + rank) of features 4q .. 4q + 3 (+16 hh) of tile t of the pair
+  // y = act(acc + bias (+ rank)) of features 4q .. 4q + 3 (+16 hh) of tile t of the pair
   auto pre = [&](const f32x16& acc, const PairVec& v, int t, int q, float (&y)[4]) {
     const int k = 4 * t + q;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x = acc[4 * q + e] + __uint_as_float(v.b[k][e]);
-      if constexpr (RANK) x = fmaf(r2v, __uint_as_float(v.c2[k][e]), fmaf(r1v, __uint_as_float(v.c1[k][e]), x));
-      y[e] = sg_act<ACT>(x, p.slope);
-    }
+    for (int e = 0; e < 4; ++e) y[e] = sg_act<ACT>(acc[4 * q + e] + __uint_as_float(v.b[k][e]), p.slope);
   };
 
   if constexpr (EPI == SG_LN) {
@@ -354,13 +368,13 @@ __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w,
   for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w[n * D + sg_in_feat(s, kh, j)];
 }
 
-template <int D, int EPI, int ACT, bool RANK>
+template <int D, int EPI, int ACT, bool RANK, int WAVES = 4>
 static int sg_launch(const SgArgs& a, hipStream_t s) {
-  auto kern = sg_kernel<D, EPI, ACT, RANK>;
+  auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES>;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, SG_ROWS)), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 32 * WAVES)), dim3(64 * WAVES), lds, s, a);
   SNV_LAUNCH_CHECK();
   return 0;
 }
@@ -376,6 +390,14 @@ static int sg_dispatch(int epi, int act, bool rank, const SgArgs& a, hipStream_t
       return rank ? sg_launch<D, SG_LN, SNVRAG_ACT_LRELU, true>(a, s) : sg_launch<D, SG_LN, SNVRAG_ACT_LRELU, false>(a, s);
     }
     return fail("snvrag_sgemm_forward", "LayerNorm epilogue supports LeakyReLU only");
+  }
+  if constexpr (D == 384) {
+    // 8 waves (256 rows per workgroup) for the projections: 15-22 % faster than 4
+    // (tools/proj_micro.py); SNVRAG_SG_WAVES4 forces 4 (A/B)
+    static const bool w8 = getenv("SNVRAG_SG_WAVES4") == nullptr;
+    // (the rank and head variants need more than 256 registers: 4 waves)
+    if (w8 && !rank && act == SNVRAG_ACT_NONE) return sg_launch<D, SG_ACT, SNVRAG_ACT_NONE, false, 8>(a, s);
+    if (w8 && !rank && act == SNVRAG_ACT_GELU) return sg_launch<D, SG_ACT, SNVRAG_ACT_GELU, false, 8>(a, s);
   }
   switch (act) {
     case SNVRAG_ACT_NONE: return rank ? sg_launch<D, SG_ACT, SNVRAG_ACT_NONE, true>(a, s)

@@ -204,6 +204,9 @@ class Engine:
                 t["tail_w"] = K.tail_pack(t["w_o"], t["w1"], w2g)
                 # QKV projection on the same 32x32 stream kernel (csrc/tail.hip PROJ mode)
                 t["qkv_pw"] = K.proj_pack(t["w_qkv"])
+                if os.environ.get("SNVRAG_NO_SG") is None:
+                    # ... and on the stream GEMM (csrc/sgemm.hip, 8 waves), which the engine prefers
+                    t["qkv_sg"] = K.sgemm_pack(t["w_qkv"])
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -70,7 +70,7 @@ class AdamS(C.Structure):
 class LayerW(C.Structure):
     _fields_ = [(n, vp) for n in ("w_qkv", "b_qkv", "w_o", "b_o", "ln1_g", "ln1_b", "w1", "b1",
                                   "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")] + [("q_scale", f32)] + \
-        [("ffn_w", vp), ("ffn_v", vp), ("qkv_ws", vp), ("o_ws", vp), ("tail_w", vp), ("qkv_pw", vp)]
+        [("ffn_w", vp), ("ffn_v", vp), ("qkv_ws", vp), ("o_ws", vp), ("tail_w", vp), ("qkv_pw", vp), ("qkv_sg", vp)]
 
 
 _SIGS = {

@@ -1,6 +1,7 @@
 """QKV projection on the 32x32 stream kernel (csrc/tail.hip PROJ mode) vs the weight-streaming
-GEMM (csrc/wsgemm.hip) at the bench shape (M = 512 x 1030, D = 384, N = 3D): max |diff| vs an
-fp64 reference on a small M, then launch times (HIP events)."""
+GEMM (csrc/wsgemm.hip) and the stream GEMM (csrc/sgemm.hip, 4 and 8 waves) at the bench shape
+(M = 512 x 1030, D = 384, N = 3D), plus the D -> 4D GELU projection on the stream GEMM: max |diff|
+vs an fp64 reference on a small M, then launch times (HIP events)."""
 import os
 import sys
 
@@ -41,7 +42,28 @@ fl = 2.0 * M * D * 3 * D
 o1 = K.proj_forward(x, ws, b, 3, out=out).clone()
 o2 = K.wsg_linear(x, wsg, 3 * D, b)
 print(f"proj vs wsg max|diff| {(o1.float() - o2.float()).abs().max().item():.4f}", flush=True)
-for name, fn in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out)),
-                 ("wsg (wsgemm.hip)", lambda: K.wsg_linear(x, wsg, 3 * D, b))):
+sgw, sgv = K.sgemm_pack(w), K.sgemm_vec(b)
+o3 = K.sgemm(x, sgw, 3 * D, sgv)
+print(f"proj vs sgemm max|diff| {(o1.float() - o3.float()).abs().max().item():.4f}", flush=True)
+w4 = (torch.randn(4 * D, D, generator=g) / D ** 0.5).to(dev, bf)
+b4 = (0.1 * torch.randn(4 * D, generator=g)).to(dev)
+sg4, sv4 = K.sgemm_pack(w4), K.sgemm_vec(b4)
+out4 = torch.empty(M, 4 * D, device=dev, dtype=bf)
+
+
+def env(k, v):
+    if v is None:
+        os.environ.pop(k, None)
+    else:
+        os.environ[k] = v
+
+
+for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out), None, fl),
+                       ("wsg (wsgemm.hip)", lambda: K.wsg_linear(x, wsg, 3 * D, b), None, fl),
+                       ("sgemm", lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out), None, fl),
+                       ("gelu 4D", lambda: K.sgemm(x, sg4, 4 * D, sv4, act=1, out=out4), None, fl * 4 / 3)):
+    env("SNVRAG_SG_WAVES4", e) if e else None
     ms = timeit(fn)
-    print(f"{name:18s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
+    print(f"{name:18s} {ms:.4f} ms  {f / ms / 1e9:.1f} TFLOP/s", flush=True)
+# the wave-count switch is read once per process: run again with SNVRAG_SG_WAVES4=1 for 4 waves
+print("(4-wave variant)" if os.environ.get("SNVRAG_SG_WAVES4") else "(8-wave variant)", flush=True)
