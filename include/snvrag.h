@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 18
+#define SNVRAG_ABI_VERSION 19
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -377,6 +377,12 @@ int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void*
  *      (foundation_model.py:77-80; N = 4D, act GELU, no rank terms)
  *   2  out[M, D] = LN(act(.) + x) g + be       bf16 (N = D, act LeakyReLU(slope);
  *      fusion.py:355-360) */
+/* The same with a concatenated input built in registers (fusion.py:157, rag_fusion's
+ * cat(h, aw * h_rag) -> Linear(2D, 4D) -> GELU, without materialising the [M, 2D] cat):
+ * out[M, N] = GELU([q | bf16(x2 * g2[m % period2])] W^T + b), q and x2 [M, Dh], g2 [period2, Dh]
+ * (bf16), W [N, 2 Dh] packed with snvrag_sgemm_pack(2 Dh, N, ...), vec = bias [N]; Dh = 384. */
+int snvrag_sgemm_cat_forward(int64_t M, int Dh, int N, const void* q, const void* x2, const void* g2,
+                             int64_t period2, const void* wstream, const float* vec, void* out, void* stream);
 size_t snvrag_sgemm_pack_bytes(int D, int N);
 int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
 int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,

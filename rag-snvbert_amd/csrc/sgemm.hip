@@ -84,6 +84,9 @@ struct SgArgs {
   const float* r1; const float* r2; int period;    // rank terms: row scalars r[m % period]
   float* probs; float* logits;                     // HEAD2 [M, 2] (logits optional)
   float slope, eps;
+  // CAT: x = [q | bf16(x2 * g2[m % period2])], q = `x` and x2 [M, D/2], g2 [period2, D/2] (fusion.py:157:
+  // cat(h, aw * h_rag) built in registers)
+  const bf16* x2; const bf16* g2; int period2;
 };
 
 template <int EPI, bool RANK> __host__ __device__ constexpr int sg_nvec(int N) {
@@ -92,7 +95,7 @@ template <int EPI, bool RANK> __host__ __device__ constexpr int sg_nvec(int N) {
 
 // WAVES = 4: 128 rows per workgroup, one wave per SIMD (512 registers); WAVES = 8: 256 rows, two
 // waves per SIMD (256 registers each) — every streamed weight byte feeds twice the rows.
-template <int D, int EPI, int ACT, bool RANK, int WAVES = 4>
+template <int D, int EPI, int ACT, bool RANK, int WAVES = 4, bool CAT = false>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
 void sg_kernel(SgArgs p) {
   constexpr int KS = D / 16, NT = D / 32, FPP = 2 * KS;           // fragments per tile pair
@@ -115,8 +118,25 @@ void sg_kernel(SgArgs p) {
   const int nvec = sg_nvec<EPI, RANK>(N);
   for (int i = tid; i < nvec; i += NTH) sv[i] = p.vec[i];
   u32x4 xa[KS];
+  if constexpr (CAT) {
+    constexpr int DH = D / 2;
+    const long rg = rc % p.period2;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+    for (int s = 0; s < KS / 2; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * DH + sg_in_feat(s, hh, 0));
+#pragma unroll
+    for (int s = KS / 2; s < KS; ++s) {
+      const int f = sg_in_feat(s, hh, 0) - DH;
+      const u32x4 r = *reinterpret_cast<const u32x4*>(p.x2 + rc * DH + f);
+      const u32x4 g = *reinterpret_cast<const u32x4*>(p.g2 + rg * DH + f);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)           // bf16(r * g) per element, as rag_concat rounds it
+        xa[s][w] = sg_pack2(__uint_as_float(r[w] << 16) * __uint_as_float(g[w] << 16),
+                            __uint_as_float(r[w] & 0xffff0000u) * __uint_as_float(g[w] & 0xffff0000u));
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+  }
   float r1v = 0.f, r2v = 0.f;
   if constexpr (RANK) {
     const long ri = rc % p.period;
@@ -368,9 +388,9 @@ __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w,
   for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w[n * D + sg_in_feat(s, kh, j)];
 }
 
-template <int D, int EPI, int ACT, bool RANK, int WAVES = 4>
+template <int D, int EPI, int ACT, bool RANK, int WAVES = 4, bool CAT = false>
 static int sg_launch(const SgArgs& a, hipStream_t s) {
-  auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES>;
+  auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES, CAT>;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -449,7 +469,7 @@ extern "C" int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, f
                 "pointers must be 16-byte aligned");
   if (M == 0) return 0;
   const SgArgs a{(int)M, N, (const bf16*)x, (bf16*)out, (const char*)wstream, vec, r1, r2, (int)period,
-                 probs, logits, slope, eps};
+                 probs, logits, slope, eps, nullptr, nullptr, 0};
   hipStream_t s = as_stream(stream);
   evlog_begin(s);
   int rc;
@@ -465,5 +485,26 @@ extern "C" int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, f
   }
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)N * D);
+  return 0;
+}
+
+extern "C" int snvrag_sgemm_cat_forward(int64_t M, int Dh, int N, const void* q, const void* x2, const void* g2,
+                                        int64_t period2, const void* wstream, const float* vec, void* out,
+                                        void* stream) {
+  SNV_CHECK_ARG(Dh == 384 && N > 0 && N % 64 == 0, "concatenated-input GEMM needs D/2 = 384 and N % 64 == 0");
+  SNV_CHECK_ARG(q && x2 && g2 && wstream && vec && out, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31) && period2 > 0 && M * N * 2 < (1L << 31), "bad M / period");
+  SNV_CHECK_ARG(N * 4 <= SG_VEC_BYTES, "vector table exceeds the LDS budget");
+  SNV_CHECK_ARG(((uintptr_t)q % 16) == 0 && ((uintptr_t)x2 % 16) == 0 && ((uintptr_t)g2 % 16) == 0 &&
+                    ((uintptr_t)wstream % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  const SgArgs a{(int)M, N, (const bf16*)q, (bf16*)out, (const char*)wstream, vec, nullptr, nullptr, 0,
+                 nullptr, nullptr, 0.f, 0.f, (const bf16*)x2, (const bf16*)g2, (int)period2};
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  const int rc = sg_launch<768, SG_ACT, SNVRAG_ACT_GELU, false, 4, true>(a, s);
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)N * 2 * Dh);
   return 0;
 }

@@ -331,10 +331,11 @@ class Engine:
             else:
                 t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
             aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
-            cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
             if "f0_sg" in rf:
-                h = K.sgemm(cat, rf["f0_sg"], rf["f0"].shape[0], rf["f0_v"], act=N.ACT_GELU)
+                # cat(h, aw * h_rag) built in the GEMM's registers (no [2B, L, 2D] tensor)
+                h = K.sgemm_cat(fused[:2 * B], fused[2 * B:], aw, BL, rf["f0_sg"], rf["f0"].shape[0], rf["f0_v"])
             else:
+                cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
                 h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
             xx = K.linear(h, rf["f3"], rf["f3b"], ln=(rf["g"], rf["bb"]), post_base=fused[:2 * B],
                           post_scale=rf["rs"], post_af=af, post_af_period=BL, post_maf=True)

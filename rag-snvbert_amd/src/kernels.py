@@ -656,6 +656,21 @@ def sgemm(x: torch.Tensor, wstream: torch.Tensor, n_out: int, vec: torch.Tensor,
     return (logits, probs) if epi == SG_HEAD2 else out
 
 
+def sgemm_cat(q: torch.Tensor, x2: torch.Tensor, g2: torch.Tensor, period: int, wstream: torch.Tensor, n_out: int,
+              vec: torch.Tensor) -> torch.Tensor:
+    """GELU([q | bf16(x2 * g2[m % period])] W^T + b) [..., n_out] (bf16; the rag fusion's
+    cat(h, aw * h_rag) input of fusion.py:157 built in registers); W packed by sgemm_pack."""
+    N.require_gpu(q, x2, g2)
+    Dh = q.shape[-1]
+    M = q.numel() // Dh
+    assert q.dtype == x2.dtype == g2.dtype == torch.bfloat16 and x2.numel() == q.numel()
+    assert g2.numel() >= period * Dh
+    out = torch.empty(*q.shape[:-1], n_out, device=q.device, dtype=torch.bfloat16)
+    check(N.lib().snvrag_sgemm_cat_forward(M, Dh, n_out, ptr(_c(q)), ptr(_c(x2)), ptr(_c(g2)), period, ptr(wstream),
+                                           ptr(vec), ptr(out), stream_ptr()), "sgemm_cat")
+    return out
+
+
 def wsg_pack(w: torch.Tensor) -> torch.Tensor:
     """Fragment-ordered bf16 weight stream of the weight-streaming GEMM (csrc/wsgemm.hip)."""
     Nn, Kk = w.shape

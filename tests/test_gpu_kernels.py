@@ -563,6 +563,28 @@ def test_stream_gemm(M, N, Kd, mode):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,period", [(1000, 1000), (2060, 1030), (77, 33)])
+def test_stream_gemm_concatenated_input(M, period):
+    """snvrag_sgemm_cat_forward (rag fusion: cat(h, aw * h_rag) -> Linear(2D, 4D) -> GELU, the cat built
+    in registers) == rag_concat + the stream GEMM on the materialised cat (bit-identical: the same
+    bf16 rounding of aw * h_rag, the same weight stream) and vs torch fp32."""
+    from src import native as NN
+    g = torch.Generator(device="cpu").manual_seed(M + period)
+    D, N = 384, 1536
+    q = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+    r = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+    aw = torch.rand(period, D, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, 2 * D, generator=g) / math.sqrt(2 * D)).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    ws, vec = K().sgemm_pack(w), K().sgemm_vec(b)
+    out = K().sgemm_cat(q, r, aw, period, ws, N, vec)
+    cat = K().rag_concat(q, r, aw, period)
+    ref = K().sgemm(cat, ws, N, vec, act=NN.ACT_GELU)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    ref32 = torch.nn.functional.gelu(cat.float() @ w.float().t() + b)
+    torch.testing.assert_close(out.float(), ref32, rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("n,bits,k,nq", [(5008, 2040, 32, 37), (300, 33, 5, 3), (20, 1020, 32, 4)])
 def test_raw_genotype_index_vs_oracle(n, bits, k, nq):
     """Raw-genotype window index (csrc/rawdb.hip + topk_merge; build_ref_db_l2.py:86-89 IndexFlatL2
