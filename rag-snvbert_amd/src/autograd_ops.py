@@ -79,6 +79,36 @@ def register_mirror(p: torch.Tensor, view: torch.Tensor) -> None:
     _MIRROR[id(p)] = (weakref.ref(p), view)
 
 
+class _TinyVocabEmbedding(torch.autograd.Function):
+    """W[tok] (F.embedding with padding_idx) for a vocabulary of a few rows: the weight gradient
+    is one one-hot GEMM (onehot(tok)^T grad, reads grad once) instead of embedding_dense_backward's
+    sort + segment scatter, which took ~6 ms per call on the 4e5 re-encoded neighbour tokens
+    (embedding_rag_dataset.py:404-417) into the 10-row token table."""
+
+    @staticmethod
+    def forward(ctx, tok, W, padding_idx):
+        ctx.save_for_backward(tok)
+        ctx.V, ctx.padding_idx, ctx.wdtype = W.shape[0], padding_idx, W.dtype
+        return torch.nn.functional.embedding(tok, W, padding_idx=padding_idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (tok,) = ctx.saved_tensors
+        D = g.shape[-1]
+        oh = torch.nn.functional.one_hot(tok.reshape(-1), ctx.V).to(torch.float32)
+        gW = oh.t() @ g.reshape(-1, D).float()
+        if ctx.padding_idx is not None:
+            gW[ctx.padding_idx] = 0
+        return None, gW.to(ctx.wdtype), None
+
+
+def tiny_embedding(tok: torch.Tensor, W: torch.Tensor, padding_idx: Optional[int] = 0) -> torch.Tensor:
+    """F.embedding(tok, W, padding_idx) with the one-hot-GEMM weight gradient (small vocabularies)."""
+    if not (W.requires_grad and torch.is_grad_enabled()):
+        return torch.nn.functional.embedding(tok, W, padding_idx=padding_idx)
+    return _TinyVocabEmbedding.apply(tok, W, padding_idx)
+
+
 class _HipLinear(torch.autograd.Function):
     """y = x [W_1; ..; W_n]^T + [b_1; ..; b_n]: one GEMM over weights concatenated along the
     output dim (the q/k/v Linear layers of multi_head_attention.py:44 as one N = 3D GEMM)."""

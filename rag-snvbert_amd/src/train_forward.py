@@ -36,7 +36,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train
+from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train, tiny_embedding
 
 T = torch.bfloat16
 
@@ -199,7 +199,7 @@ def neighbour_mean_dropout(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor,
         tok[..., n_sites + 1] = eos
     valid = idx >= 0
     tok[..., 1:1 + n_sites] = tok0 + codes[idx.clamp(min=0)][..., :n_sites].long()
-    e = F.embedding(tok, W, padding_idx=0) + pe[:L] + Ar
+    e = tiny_embedding(tok, W, 0) + pe[:L] + Ar
     e = F.dropout(e, p, True) * valid[..., None, None]
     return (e.sum(1) / valid.sum(1).clamp(min=1)[:, None, None]).to(T)
 
@@ -219,7 +219,7 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     D = emb.embed_size
     # 1. query embeddings (embedding/bert.py:63-75); h1 and h2 stacked
     tok = torch.cat([h1, h2], 0)
-    e = F.embedding(tok, emb.tokenizer.weight, padding_idx=0) + emb.position.pe[:, :L]
+    e = tiny_embedding(tok, emb.tokenizer.weight, 0) + emb.position.pe[:, :L]
     if emb.use_af:
         e = e + af_embedding(emb.af_embedding, af).float().repeat(2, 1, 1)
     h_raw = _drop(e.to(T), p, training)                                          # [2B, L, D]
