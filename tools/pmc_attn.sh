@@ -11,7 +11,7 @@ P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 tools/attn_only.py \
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 ${PMC_TOOL:-tools/attn_only.py} \
     > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 tools/pmc_kernel.py ${KFILT:-attn} $OUT/p1 $OUT/p2
