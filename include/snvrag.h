@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 19
+#define SNVRAG_ABI_VERSION 20
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -383,6 +383,16 @@ int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void*
  * (bf16), W [N, 2 Dh] packed with snvrag_sgemm_pack(2 Dh, N, ...), vec = bias [N]; Dh = 384. */
 int snvrag_sgemm_cat_forward(int64_t M, int Dh, int N, const void* q, const void* x2, const void* g2,
                              int64_t period2, const void* wstream, const float* vec, void* out, void* stream);
+/* Two projections in one launch with the [M, 4D] hidden on chip (fusion.py:131-141 af_adapter,
+ * foundation_model.py:25-33 af_fusion), bf16, eval, D = 384:
+ *   out[M, D] = EPI2(GELU(x W1^T + b1 [+ r1[m % period] c1 + r2[m % period] c2]) W2^T + b2)
+ * epi2: 0 sigmoid, 1 LayerNorm (g, be).  W1 [4D, D], W2 [D, 4D] packed once by snvrag_mlp_pack
+ * (snvrag_mlp_pack_bytes(D) bytes); vec (f32) = [b1 4D | c1 4D, c2 4D when r1 | b2 D | g D, be D
+ * when epi2 = 1]. */
+size_t snvrag_mlp_pack_bytes(int D);
+int snvrag_mlp_pack(int D, const void* w1, const void* w2, void* out, void* stream);
+int snvrag_mlp_forward(int64_t M, int D, int epi2, const void* x, const void* wstream, const float* vec,
+                       const float* r1, const float* r2, int64_t period, float eps, void* out, void* stream);
 size_t snvrag_sgemm_pack_bytes(int D, int N);
 int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
 int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,

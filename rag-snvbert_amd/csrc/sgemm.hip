@@ -374,6 +374,258 @@ void sg_kernel(SgArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------- MLP --
+// Two projections in one launch, the 4D hidden kept on chip (fusion.py:131-141 af_adapter:
+// Linear(D, 4D) -> GELU -> Linear(4D, D) -> Sigmoid; foundation_model.py:25-33 af_fusion:
+// Linear(D + 2, 4D) over cat(x, af, af_p) -> GELU -> Linear(4D, D) -> LayerNorm):
+//   out[M, D] = EPI2(GELU(x W1^T + b1 [+ r1 c1 + r2 c2]) W2^T + b2),  EPI2 = sigmoid | LN.
+// The stream GEMM above for W1 (hidden tile pairs, 64 units), whose pair epilogue (bias, rank,
+// GELU, bf16 packing) now produces the B fragments of W2's k-steps over those 64 units (the k
+// order baked into W2's columns at pack time), so phase 2 accumulates all D outputs (12 f32
+// tiles, 192 registers) pair by pair.  Per pair: 48 W1 fragments (the previous pair's epilogue
+// spread between them), then the previous pair's 48 W2 fragments.  4 waves x 32 rows.
+template <int D, bool RANK, int EPI2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_kernel(SgArgs p) {
+  constexpr int KS = D / 16, NT = D / 32, F1 = 2 * KS, F2 = 4 * NT, FPP = F1 + F2;
+  static_assert(F1 % 16 == 0 && F2 % 16 == 0, "parts are whole slabs");
+  constexpr int SPP = FPP / 16;
+  constexpr int RING = SG_NSLOT * SG_SLAB;
+  constexpr int H = 4 * D, NP = H / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  float* sv = reinterpret_cast<float*>(smem + RING);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ln = lane & 31, hh = lane >> 5;
+  const long row = (long)blockIdx.x * 128 + wave * 32 + ln;
+  const long rc = row < p.M ? row : (long)p.M - 1;
+  // vector table [b1 H | RANK: c1 H, c2 H | b2 D | LN: g D, be D]
+  constexpr int OB2 = H * (RANK ? 3 : 1);
+  const int nvec = OB2 + D * (EPI2 == 1 ? 3 : 1);
+  for (int i = tid; i < nvec; i += 256) sv[i] = p.vec[i];
+  u32x4 xa[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+  float r1v = 0.f, r2v = 0.f;
+  if constexpr (RANK) {
+    const long ri = rc % p.period;
+    r1v = p.r1[ri];
+    r2v = p.r2[ri];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int rot = (int)(blockIdx.x % NP);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, NP * SPP * SG_SLAB, 0x00020000);
+  const int voff = lane * 16;
+  int is_slot = 0, is_i = 0;
+  // consumption order of the stream's blocks B(2P) = W1(P), B(2P + 1) = W2(P) (HS slabs each):
+  // W1(r), W1(r+1), W2(r), W1(r+2), W2(r+1), ..., W1(r+NP-1), W2(r+NP-2), W2(r+NP-1) (mod NP) —
+  // launch block b: 0 -> B(2r); odd b < 2NP-1 -> B(2r+b+1); even b >= 2 -> B(2r+b-1); 2NP-1 -> B(2r+b)
+  constexpr int HS = F1 / 16;
+  static_assert(F1 == F2, "equal W1 / W2 blocks per pair");
+  auto issue_next = [&]() {
+    auto* dst = (__attribute__((address_space(3))) char*)(ring + is_slot + wave * 4 * SG_FRAG);
+    const int b = is_i / HS, j = is_i - b * HS;
+    int m = 2 * rot + b + ((b == 0 || b == 2 * NP - 1) ? 0 : (b & 1) ? 1 : -1);
+    m %= 2 * NP;                                     // (issues past the end wrap: addresses stay valid)
+    const int src = (m * HS + j) * SG_SLAB;
+    ++is_i;
+    sg_unroll([&](auto jc) {
+      constexpr int q = decltype(jc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, dst + q * SG_FRAG, 16, voff, src + (wave * 4 + q) * SG_FRAG, 0, 0);
+    }, std::make_integer_sequence<int, 4>{});
+    is_slot = is_slot + SG_SLAB == RING ? 0 : is_slot + SG_SLAB;
+  };
+#pragma unroll
+  for (int g = 0; g < SG_NSLOT - 1; ++g) issue_next();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 2)) : "memory");
+  __syncthreads();
+
+  int rd_slot = 0;
+  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {
+    constexpr int j = decltype(j_tag)::value, fi = decltype(fi_tag)::value;
+    int so = rd_slot + j * SG_SLAB;
+    so = so >= RING ? so - RING : so;
+    return *reinterpret_cast<const u32x4*>(ring + so + lane * 16 + fi * SG_FRAG);
+  };
+  auto sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (SG_NSLOT - 3)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_next();
+  };
+  u32x4 a[SG_PF];
+  sg_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
+            std::make_integer_sequence<int, SG_PF>{});
+  auto run = [&](auto nf_tag, auto&& mma) {
+    constexpr int NF = decltype(nf_tag)::value;
+    sg_unroll([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      const u32x4 cur = a[f % SG_PF];
+      if constexpr ((f & 15) == 16 - SG_PF) {
+        __builtin_amdgcn_sched_barrier(0);
+        sync();
+      }
+      mma(fc, cur);
+      constexpr int qn = f + SG_PF;
+      a[f % SG_PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }, std::make_integer_sequence<int, NF>{});
+    rd_slot += (NF / 16) * SG_SLAB;
+    rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
+  };
+  const uint32_t sv_lane = sg_lds(sv) + 64 * hh;
+  u32x4 pb[8];                                       // the pair's b1 (+ rank) for this lane's 32 units
+  auto load_b1 = [&](int pp) {
+    const uint32_t ad = sv_lane + 4 * 64 * pp;
+    sg_vec8(ad, pb);
+    if constexpr (RANK) {
+      u32x4 c[8];
+      sg_vec8(ad + 4 * H, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pb[k][e] = __float_as_uint(fmaf(r1v, __uint_as_float(c[k][e]), __uint_as_float(pb[k][e])));
+      sg_vec8(ad + 8 * H, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pb[k][e] = __float_as_uint(fmaf(r2v, __uint_as_float(c[k][e]), __uint_as_float(pb[k][e])));
+    }
+  };
+  u32x4 hf[4];                                       // phase-2 B fragments of the epilogued pair
+  // step k (0..7): units 4(k%4) .. +3 of tile k/4 -> GELU -> bf16 into hf[2(k/4) + (k%4)/2]
+  auto epi_step = [&](const f32x16 (&e)[2], int k) {
+    const int t = k >> 2, q = k & 3;
+    float y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = gelu_bf16(e[t][4 * q + j] + __uint_as_float(pb[k][j]));
+    hf[2 * t + (q >> 1)][2 * (q & 1)] = sg_pack2(y[0], y[1]);
+    hf[2 * t + (q >> 1)][2 * (q & 1) + 1] = sg_pack2(y[2], y[3]);
+  };
+  constexpr int EVERY = F1 / 8;
+  auto phase1 = [&](f32x16 (&en)[2], const f32x16 (&ep)[2], auto prev_tag) {
+    constexpr bool PREV = decltype(prev_tag)::value;
+    run(std::integral_constant<int, F1>{}, [&](auto fc, const u32x4& A) {
+      constexpr int f = decltype(fc)::value, t = f / KS, s = f % KS;
+      if constexpr (s == 0) en[t] = sg_mfma(A, xa[0], f32x16{});
+      else en[t] = sg_mfma(A, xa[s], en[t]);
+      if constexpr (PREV && f % EVERY == 0) epi_step(ep, f / EVERY);
+    });
+  };
+  f32x16 acc[NT];
+  auto phase2 = [&](auto first_tag) {                // fragment f: k-step f / NT, output tile f % NT
+    constexpr bool FIRST = decltype(first_tag)::value;
+    run(std::integral_constant<int, F2>{}, [&](auto fc, const u32x4& A) {
+      constexpr int f = decltype(fc)::value;
+      if constexpr (FIRST && f < NT) acc[f] = sg_mfma(A, hf[0], f32x16{});
+      else acc[f % NT] = sg_mfma(A, hf[f / NT], acc[f % NT]);
+    });
+  };
+  f32x16 e0[2], e1[2];
+  phase1(e0, e1, std::false_type{});
+  load_b1(rot);
+  phase1(e1, e0, std::true_type{});
+  phase2(std::true_type{});
+  int P = 2;
+#pragma unroll 1
+  for (; P + 1 < NP; P += 2) {
+    load_b1((rot + P - 1) % NP);
+    phase1(e0, e1, std::true_type{});
+    phase2(std::false_type{});
+    load_b1((rot + P) % NP);
+    phase1(e1, e0, std::true_type{});
+    phase2(std::false_type{});
+  }
+  static_assert(NP % 2 == 0, "pairs of hidden tile pairs");
+  load_b1((rot + NP - 1) % NP);                      // the last pair (in e1)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) epi_step(e1, k);
+  phase2(std::false_type{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stream overrun has landed
+
+  // ---- out = EPI2(acc + b2): sigmoid, or LayerNorm over the D outputs of the row
+  float sum = 0.f, sq = 0.f;
+#pragma unroll
+  for (int T = 0; T < NT; T += 2) {
+    u32x4 vb[8];
+    sg_vec8(sv_lane + 4 * (OB2 + 32 * T), vb);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int tt = i >> 4, ii = i & 15;
+      float v = acc[T + tt][ii] + __uint_as_float(vb[4 * tt + (ii >> 2)][ii & 3]);
+      if constexpr (EPI2 == 0) v = __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+      acc[T + tt][ii] = v;
+      sum += v;
+      sq = fmaf(v, v, sq);
+    }
+  }
+  float mean = 0.f, rstd = 1.f;
+  if constexpr (EPI2 == 1) {
+    sum += __shfl_xor(sum, 32, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    mean = sum * (1.0f / D);
+    rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+  }
+  if (row < p.M) {
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float y[16];
+      if constexpr (EPI2 == 1) {
+        u32x4 g[8], be[8];
+        sg_vec8(sv_lane + 4 * (OB2 + D + 32 * (T & ~1)), g);
+        sg_vec8(sv_lane + 4 * (OB2 + 2 * D + 32 * (T & ~1)), be);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int k = 4 * (T & 1) + (i >> 2);
+          y[i] = fmaf((acc[T][i] - mean) * rstd, __uint_as_float(g[k][i & 3]), __uint_as_float(be[k][i & 3]));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) y[i] = acc[T][i];
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        *reinterpret_cast<u32x4*>(p.out + row * D + 32 * T + 16 * hh + 8 * h2) =
+            u32x4{sg_pack2(y[8 * h2], y[8 * h2 + 1]), sg_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                  sg_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), sg_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+    }
+  }
+}
+
+// MLP stream: per hidden pair P: W1 rows 64P .. 64P + 63 as in sg_pack (F = t KS + s), then
+// W2's 64 columns of the pair: fragment F2 = q NT + T, lane (m, kh) holds
+// W2[32T + sg_out_feat(m)][64P + sg_in_feat(q, kh, 0 .. 7)].
+__global__ void mlp_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w1, const bf16* __restrict__ w2,
+                                bf16* __restrict__ out) {
+  const long pc = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pc >= n_pieces) return;
+  const int KS = D / 16, NT = D / 32, F1 = 2 * KS, FPP = F1 + 4 * NT;
+  const long F = pc / 64;
+  const int l = (int)(pc % 64), m = l & 31, kh = l >> 5;
+  const long P = F / FPP;
+  const int f = (int)(F % FPP);
+  if (f < F1) {
+    const int t = f / KS, s = f % KS;
+    const long n = 64 * P + 32 * t + sg_out_feat(m);
+    for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w1[n * D + sg_in_feat(s, kh, j)];
+  } else {
+    const int f2 = f - F1, q = f2 / NT, T = f2 % NT;
+    const long n = 32 * T + sg_out_feat(m);
+    for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w2[n * 4 * D + 64 * P + sg_in_feat(q, kh, j)];
+  }
+}
+
+template <int D, bool RANK, int EPI2>
+static int mlp_launch(const SgArgs& a, hipStream_t s) {
+  auto kern = mlp_kernel<D, RANK, EPI2>;
+  const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 128)), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 // One thread per 16-byte piece (8 bf16) of the stream: fragment F = T KS + s (output tile T, k-step
 // s), lane l = (m = l % 32, kh = l / 32) holds W[32T + sg_out_feat(m)][sg_in_feat(s, kh, 0 .. 7)].
 __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w, bf16* __restrict__ out) {
@@ -506,5 +758,42 @@ extern "C" int snvrag_sgemm_cat_forward(int64_t M, int Dh, int N, const void* q,
   const int rc = sg_launch<768, SG_ACT, SNVRAG_ACT_GELU, false, 4, true>(a, s);
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)N * 2 * Dh);
+  return 0;
+}
+
+extern "C" size_t snvrag_mlp_pack_bytes(int D) {
+  return D == 384 ? (size_t)2 * 4 * D * D * 2 : 0;
+}
+
+extern "C" int snvrag_mlp_pack(int D, const void* w1, const void* w2, void* out, void* stream) {
+  SNV_CHECK_ARG(snvrag_mlp_pack_bytes(D) > 0, "MLP stream needs D = 384");
+  SNV_CHECK_ARG(w1 && w2 && out, "null pointer");
+  const long pieces = (long)snvrag_mlp_pack_bytes(D) / 16;
+  hipLaunchKernelGGL(mlp_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
+                     (const bf16*)w1, (const bf16*)w2, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_mlp_forward(int64_t M, int D, int epi2, const void* x, const void* wstream, const float* vec,
+                                  const float* r1, const float* r2, int64_t period, float eps, void* out,
+                                  void* stream) {
+  SNV_CHECK_ARG(D == 384, "MLP kernel needs D = 384");
+  SNV_CHECK_ARG(epi2 == 0 || epi2 == 1, "epi2: 0 sigmoid, 1 LayerNorm");
+  SNV_CHECK_ARG(x && wstream && vec && out, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  const bool rank = r1 != nullptr;
+  SNV_CHECK_ARG(!rank || (r2 && period > 0), "rank terms need r1, r2 and a period");
+  SNV_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)wstream % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "pointers must be 16-byte aligned");
+  if (M == 0) return 0;
+  const SgArgs a{(int)M, D, (const bf16*)x, (bf16*)out, (const char*)wstream, vec, r1, r2, (int)period,
+                 nullptr, nullptr, 0.f, eps, nullptr, nullptr, 0};
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  const int rc = epi2 == 0 ? (rank ? mlp_launch<384, true, 0>(a, s) : mlp_launch<384, false, 0>(a, s))
+                           : (rank ? mlp_launch<384, true, 1>(a, s) : mlp_launch<384, false, 1>(a, s));
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)D * 4 * D * 2);
   return 0;
 }

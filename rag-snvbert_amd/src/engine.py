@@ -169,7 +169,12 @@ class Engine:
                     rs=float(rf.res_scale.detach().float().item()))
         if sg_ok and D == 384 and P.rf["f0"].shape == (4 * D, 2 * D):
             P.rf["f0_sg"], P.rf["f0_v"] = K.sgemm_pack(P.rf["f0"]), K.sgemm_vec(P.rf["f0b"])
-        if sg_ok and P.rf["a0"].shape == (4 * D, D):
+        mlp_ok = sg_ok and D == 384 and os.environ.get("SNVRAG_NO_MLP") is None
+        if mlp_ok and P.rf["a0"].shape == (4 * D, D) and P.rf["a3"].shape == (D, 4 * D):
+            # af_adapter: Linear -> GELU -> Linear -> Sigmoid in one launch, hidden on chip
+            P.rf["a_mlp"] = K.mlp_pack(P.rf["a0"], P.rf["a3"])
+            P.rf["a_mlp_v"] = K.sgemm_vec(torch.cat([P.rf["a0b"], P.rf["a3b"]]))
+        elif sg_ok and P.rf["a0"].shape == (4 * D, D):
             P.rf["a0_sg"], P.rf["a0_v"] = K.sgemm_pack(P.rf["a0"]), K.sgemm_vec(P.rf["a0b"])
         elif ws_ok and P.rf["a0"].shape == (4 * D, D):
             P.rf["a0_ws"] = K.wsg_pack(P.rf["a0"])
@@ -218,7 +223,12 @@ class Engine:
                     g=f32(hc.af_fusion[3].weight), bb=f32(hc.af_fusion[3].bias),
                     n0=cvt(hc.net[0].weight), n0b=f32(hc.net[0].bias),
                     n2=f32(hc.net[2].weight), n2b=f32(hc.net[2].bias))
-        if sg_ok and P.hh["w0"].shape == (4 * D, D):
+        if sg_ok and D == 384 and os.environ.get("SNVRAG_NO_MLP") is None and P.hh["w2"].shape == (D, 4 * D):
+            # af_fusion: Linear over cat(x, af, af_p) -> GELU -> Linear -> LayerNorm in one launch
+            P.hh["f_mlp"] = K.mlp_pack(P.hh["w0"], P.hh["w2"])
+            P.hh["f_mlp_v"] = torch.cat([P.hh["b0"], P.hh["c_af"], P.hh["c_afp"], P.hh["b2"], P.hh["g"],
+                                         P.hh["bb"]]).float().contiguous()
+        elif sg_ok and P.hh["w0"].shape == (4 * D, D):
             P.hh["w0_sg"] = K.sgemm_pack(P.hh["w0"])
             P.hh["w0_v"] = K.sgemm_vec(P.hh["b0"], P.hh["c_af"], P.hh["c_afp"])
         elif ws_ok and P.hh["w0"].shape == (4 * D, D):
@@ -324,13 +334,16 @@ class Engine:
         if rag is not None:
             rf = P.rf
             fa = K.af_gate(af, af_p, P.ag, D, T)                      # [B, L, D]
-            if "a0_sg" in rf:
-                t = K.sgemm(fa, rf["a0_sg"], rf["a0"].shape[0], rf["a0_v"], act=N.ACT_GELU)
-            elif "a0_ws" in rf:
-                t = K.wsg_linear(fa, rf["a0_ws"], rf["a0"].shape[0], rf["a0b"], act=N.ACT_GELU)
+            if "a_mlp" in rf:
+                aw = K.mlp(fa, rf["a_mlp"], rf["a_mlp_v"], epi2=0)
             else:
-                t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
-            aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
+                if "a0_sg" in rf:
+                    t = K.sgemm(fa, rf["a0_sg"], rf["a0"].shape[0], rf["a0_v"], act=N.ACT_GELU)
+                elif "a0_ws" in rf:
+                    t = K.wsg_linear(fa, rf["a0_ws"], rf["a0"].shape[0], rf["a0b"], act=N.ACT_GELU)
+                else:
+                    t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
+                aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
             if "f0_sg" in rf:
                 # cat(h, aw * h_rag) built in the GEMM's registers (no [2B, L, 2D] tensor)
                 h = K.sgemm_cat(fused[:2 * B], fused[2 * B:], aw, BL, rf["f0_sg"], rf["f0"].shape[0], rf["f0_v"])
@@ -354,16 +367,19 @@ class Engine:
         B, L = o["B"], o["L"]
         BL = B * L
         hh = P.hh
-        if "w0_sg" in hh:
-            h = K.sgemm(o["x_all"], hh["w0_sg"], hh["w0"].shape[0], hh["w0_v"], act=N.ACT_GELU,
-                        rank=(o["af"], o["af_p"], BL))
-        elif "w0_ws" in hh:
-            h = K.wsg_linear(o["x_all"], hh["w0_ws"], hh["w0"].shape[0], hh["b0"], act=N.ACT_GELU,
-                             row1=(o["af"], hh["c_af"]), row2=(o["af_p"], hh["c_afp"]), row_period=BL)
+        if "f_mlp" in hh:
+            h = K.mlp(o["x_all"], hh["f_mlp"], hh["f_mlp_v"], epi2=1, rank=(o["af"], o["af_p"], BL))
         else:
-            h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
-                         row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
-        h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
+            if "w0_sg" in hh:
+                h = K.sgemm(o["x_all"], hh["w0_sg"], hh["w0"].shape[0], hh["w0_v"], act=N.ACT_GELU,
+                            rank=(o["af"], o["af_p"], BL))
+            elif "w0_ws" in hh:
+                h = K.wsg_linear(o["x_all"], hh["w0_ws"], hh["w0"].shape[0], hh["b0"], act=N.ACT_GELU,
+                                 row1=(o["af"], hh["c_af"]), row2=(o["af_p"], hh["c_afp"]), row_period=BL)
+            else:
+                h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
+                             row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
+            h = K.linear(h, hh["w2"], hh["b2"], ln=(hh["g"], hh["bb"]))
         if "n0_sg" in hh:
             logits, probs = K.sgemm(h, hh["n0_sg"], hh["n0"].shape[0], hh["n0_v"], epi=K.SG_HEAD2, act=N.ACT_GELU,
                                     want_logits=want_logits)

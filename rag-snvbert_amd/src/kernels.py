@@ -656,6 +656,37 @@ def sgemm(x: torch.Tensor, wstream: torch.Tensor, n_out: int, vec: torch.Tensor,
     return (logits, probs) if epi == SG_HEAD2 else out
 
 
+def mlp_pack(w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """Stream of the fused MLP kernel (csrc/sgemm.hip mlp_kernel): W1 [4D, D], W2 [D, 4D] (bf16)."""
+    N.require_gpu(w1, w2)
+    D = w1.shape[1]
+    nbytes = int(N.lib().snvrag_mlp_pack_bytes(D))
+    if nbytes == 0 or tuple(w1.shape) != (4 * D, D) or tuple(w2.shape) != (D, 4 * D):
+        raise ValueError(f"MLP stream needs W1 [4D, D], W2 [D, 4D] with D = 384, got {tuple(w1.shape)}, {tuple(w2.shape)}")
+    out = torch.empty(nbytes, device=w1.device, dtype=torch.uint8)
+    check(N.lib().snvrag_mlp_pack(D, ptr(_c(w1.to(torch.bfloat16).contiguous())),
+                                  ptr(_c(w2.to(torch.bfloat16).contiguous())), ptr(out), stream_ptr()), "mlp_pack")
+    return out
+
+
+def mlp(x: torch.Tensor, wstream: torch.Tensor, vec: torch.Tensor, *, epi2: int,
+        rank: Optional[Tuple[torch.Tensor, torch.Tensor, int]] = None, eps: float = 1e-5) -> torch.Tensor:
+    """EPI2(GELU(x W1^T + b1 [+ rank]) W2^T + b2) [..., D] bf16 in one launch; epi2 0 = sigmoid,
+    1 = LayerNorm; vec = [b1 | c1, c2 | b2 | g, be] (f32)."""
+    N.require_gpu(x)
+    assert x.dtype == torch.bfloat16
+    D = x.shape[-1]
+    M = x.numel() // D
+    out = torch.empty_like(x)
+    r1 = r2 = None
+    period = 0
+    if rank is not None:
+        r1, r2, period = _c(rank[0].float()), _c(rank[1].float()), int(rank[2])
+    check(N.lib().snvrag_mlp_forward(M, D, epi2, ptr(_c(x)), ptr(wstream), ptr(vec), ptr(r1), ptr(r2), period, eps,
+                                     ptr(out), stream_ptr()), "mlp")
+    return out
+
+
 def sgemm_cat(q: torch.Tensor, x2: torch.Tensor, g2: torch.Tensor, period: int, wstream: torch.Tensor, n_out: int,
               vec: torch.Tensor) -> torch.Tensor:
     """GELU([q | bf16(x2 * g2[m % period])] W^T + b) [..., n_out] (bf16; the rag fusion's

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -134,6 +134,9 @@ _SIGS = {
     "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),
     "snvrag_confusion": ([i64, C.c_int, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_infer_post": ([i64, vp, vp, vp, vp, vp, vp], C.c_int),
+    "snvrag_mlp_pack_bytes": ([C.c_int], sz),
+    "snvrag_mlp_pack": ([C.c_int, vp, vp, vp, vp], C.c_int),
+    "snvrag_mlp_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, i64, f32, vp, vp], C.c_int),
     "snvrag_sgemm_cat_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, i64, vp, vp, vp, vp], C.c_int),
     "snvrag_sgemm_pack_bytes": ([C.c_int, C.c_int], sz),
     "snvrag_sgemm_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),

@@ -563,6 +563,43 @@ def test_stream_gemm(M, N, Kd, mode):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,mode", [(1000, "sigmoid"), (4133, "rank_ln"), (77, "ln"), (300, "rank_sigmoid")])
+def test_fused_mlp(M, mode):
+    """snvrag_mlp_forward (two projections, the 4D hidden on chip: af_adapter / af_fusion) vs torch fp32 of
+    the same bf16 weights, with the hidden rounded to bf16 as the kernel's phase-2 operand is."""
+    from src import native as NN  # noqa: F401
+    g = torch.Generator(device="cpu").manual_seed(M)
+    D, H = 384, 1536
+    x = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+    w1 = (torch.randn(H, D, generator=g) / math.sqrt(D)).to(DEV, torch.bfloat16)
+    w2 = (torch.randn(D, H, generator=g) / math.sqrt(H)).to(DEV, torch.bfloat16)
+    b1, b2 = torch.randn(H, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    parts, rank = [b1], None
+    h = x.float() @ w1.float().t() + b1
+    if mode.startswith("rank"):
+        period = (M + 2) // 3
+        r1, r2 = torch.rand(period, generator=g).to(DEV), torch.rand(period, generator=g).to(DEV)
+        c1, c2 = torch.randn(H, generator=g).to(DEV), torch.randn(H, generator=g).to(DEV)
+        ri = torch.arange(M, device=DEV) % period
+        h = h + r1[ri, None] * c1[None] + r2[ri, None] * c2[None]
+        parts += [c1, c2]
+        rank = (r1, r2, period)
+    h = torch.nn.functional.gelu(h).to(torch.bfloat16).float()
+    y = h @ w2.float().t() + b2
+    parts.append(b2)
+    if mode.endswith("ln"):
+        gm, bt = torch.rand(D, generator=g).to(DEV) + 0.5, torch.randn(D, generator=g).to(DEV)
+        ref = torch.nn.functional.layer_norm(y, (D,), gm, bt, 1e-5)
+        parts += [gm, bt]
+        epi2 = 1
+    else:
+        ref = torch.sigmoid(y)
+        epi2 = 0
+    vec = torch.cat([t.float().reshape(-1) for t in parts]).contiguous()
+    out = K().mlp(x, K().mlp_pack(w1, w2), vec, epi2=epi2, rank=rank)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("M,period", [(1000, 1000), (2060, 1030), (77, 33)])
 def test_stream_gemm_concatenated_input(M, period):
     """snvrag_sgemm_cat_forward (rag fusion: cat(h, aw * h_rag) -> Linear(2D, 4D) -> GELU, the cat built
