@@ -229,9 +229,19 @@ struct State {
   f32x4 negm[2];     // [qt]: -m_q broadcast (MFMA C operand)
 };
 
-template <int NKT, bool MASK, bool FIRST>
+// Training (TRAIN): Q is unscaled (no bf16 rounding of Q * scale, so the backward's recomputed
+// P = exp2(c s - lse) matches), the shift m_q is in unscaled score units and p = exp2(c (s - m_q));
+// with dropout the PV operand is bf16(p * keep / (1 - p_drop)) while the row sum keeps every p.
+struct Train {
+  float c;            // scale * log2(e)
+  AttnDrop drop;
+  uint32_t dbase;     // drop_base(seed, seq * H + h)
+  int q0;             // the wave's first query
+};
+
+template <int NKT, bool MASK, bool FIRST, bool TRAIN = false>
 __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
-                                     State& st, int li, int lg) {
+                                     State& st, int li, int lg, const Train& tr = Train{}) {
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4 s[NKT][2];
 #pragma unroll
@@ -268,6 +278,7 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
   }
   constexpr int NCB = (NKT + 1) / 2;
   bf16x8 pb[NCB][2];
+  bf16x8 pd[TRAIN ? NCB : 1][2];                 // TRAIN: the dropped-out PV operand
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
@@ -275,7 +286,16 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int kt = 2 * cb + (j >> 2);
-        pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
+        if constexpr (TRAIN) {
+          const float p = kt < NKT ? __builtin_amdgcn_exp2f(tr.c * s[kt < NKT ? kt : 0][qt][j & 3]) : 0.f;
+          pb[cb][qt][j] = (bf16)p;
+          const float dm = tr.drop.thresh ? drop_mul(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
+                                                     (uint32_t)(kbase + 16 * kt + 4 * lg + (j & 3)))
+                                          : 1.f;
+          pd[cb][qt][j] = (bf16)(p * dm);
+        } else {
+          pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
+        }
       }
   const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
@@ -286,27 +306,32 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
       const int k0 = 32 * cb + 4 * lg + tq;
       const bf16x8 vf = cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[cb][qt], st.o[e][qt], 0, 0, 0);
+      for (int qt = 0; qt < 2; ++qt)
+        st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, TRAIN ? pd[TRAIN ? cb : 0][qt] : pb[cb][qt],
+                                                               st.o[e][qt], 0, 0, 0);
     }
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) st.ls[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[cb][qt], st.ls[qt], 0, 0, 0);
   }
 }
 
-template <bool FIRST>
+template <bool FIRST, bool TRAIN = false>
 __device__ __forceinline__ void tile_any(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
-                                         State& st, int li, int lg) {
+                                         State& st, int li, int lg, const Train& tr = Train{}) {
   const int rem = L - kbase;
-  if (rem >= KT) tile<4, false, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
-  else if (rem <= 16) tile<1, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
-  else if (rem <= 32) tile<2, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
-  else tile<4, true, FIRST>(Kt, Vt, kbase, L, qf, st, li, lg);
+  if (rem >= KT) tile<4, false, FIRST, TRAIN>(Kt, Vt, kbase, L, qf, st, li, lg, tr);
+  else if (rem <= 16) tile<1, true, FIRST, TRAIN>(Kt, Vt, kbase, L, qf, st, li, lg, tr);
+  else if (rem <= 32) tile<2, true, FIRST, TRAIN>(Kt, Vt, kbase, L, qf, st, li, lg, tr);
+  else tile<4, true, FIRST, TRAIN>(Kt, Vt, kbase, L, qf, st, li, lg, tr);
 }
 
 // Exact online-max softmax for one wave's 32 queries, K/V read from global memory
 // (16 keys per step).  Only runs when the fixed-shift pass overflowed.
+// (TRAIN: scores scaled by tr.c here, dropout on the PV operand; st.negm returns -m / c so that
+// the caller's lse = -c negm + log2 l holds for both paths)
+template <bool TRAIN = false>
 __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, long ld, int L, const bf16x8 (&qf)[2],
-                                           State& st, int li, int lg) {
+                                           State& st, int li, int lg, const Train& tr = Train{}) {
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -325,6 +350,7 @@ __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, lo
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       f32x4 sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt], zero, 0, 0, 0);
+      if constexpr (TRAIN) sc *= tr.c;
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -338,9 +364,15 @@ __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, lo
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bf16 pr = (bf16)exp2f(sc[r] - mn);
-        pb[r] = pr;
+        const float pf = exp2f(sc[r] - mn);
+        const bf16 pr = (bf16)pf;
         ps += (float)pr;
+        if constexpr (TRAIN)
+          pb[r] = tr.drop.thresh ? (bf16)(pf * drop_mul(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
+                                                        (uint32_t)(k0 + 4 * lg + r)))
+                                 : pr;
+        else
+          pb[r] = pr;
       }
       ps += __shfl_xor(ps, 16, 64);
       ps += __shfl_xor(ps, 32, 64);
@@ -351,14 +383,21 @@ __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, lo
     }
   }
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) st.ls[qt] = f32x4{l[qt], l[qt], l[qt], l[qt]};
+  for (int qt = 0; qt < 2; ++qt) {
+    st.ls[qt] = f32x4{l[qt], l[qt], l[qt], l[qt]};
+    const float nm = TRAIN ? -m[qt] / tr.c : -m[qt];
+    st.negm[qt] = f32x4{nm, nm, nm, nm};
+  }
 }
 }  // namespace a32
 
-template <bool PRESCALED>
+// TRAIN (training forward, snvrag_attention_train_fwd): Q unscaled, lse [nseq, H, L] written
+// (log2 domain: lse = c m + log2 l), attention-probability dropout on the PV operand.
+template <bool PRESCALED, bool TRAIN = false>
 __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                    bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
-                                                   int* __restrict__ n_fallback) {
+                                                   int* __restrict__ n_fallback, float* __restrict__ lse = nullptr,
+                                                   AttnDrop drop = AttnDrop{}) {
   using namespace a32;
   __shared__ __attribute__((aligned(16))) char smem[2][2 * TB];
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -380,7 +419,7 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + 16 * qt + li;
     bf16x8 v = q < L ? *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + 8 * lg) : bf16x8{};
-    if constexpr (!PRESCALED) {
+    if constexpr (!PRESCALED && !TRAIN) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * scale_log2e);
     }
@@ -412,6 +451,8 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
     st.o[0][qt] = st.o[1][qt] = st.ls[qt] = zero;
     st.negm[qt] = zero;
   }
+  Train tr{};
+  if constexpr (TRAIN) tr = Train{scale_log2e, drop, drop.thresh ? drop_base(drop.seed, (uint32_t)sh) : 0u, q0};
   const int ntile = (L + KT - 1) / KT;
   A32_LOAD(0);
   A32_STORE(0);
@@ -421,8 +462,8 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
     if (more) A32_LOAD(t + 1);
     if (active) {
       const char* Kt = smem[t & 1];
-      if (t == 0) tile_any<true>(Kt, Kt + TB, 0, L, qf, st, li, lg);
-      else tile_any<false>(Kt, Kt + TB, t * KT, L, qf, st, li, lg);
+      if (t == 0) tile_any<true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+      else tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
     }
     if (more) A32_STORE((t + 1) & 1);
     __syncthreads();
@@ -443,13 +484,16 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
   }
   if (__ballot(bad)) {
     if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
-    attn32_online(Kp, Vp, ld, L, qf, st, li, lg);
+    attn32_online<TRAIN>(Kp, Vp, ld, L, qf, st, li, lg, tr);
   }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + 16 * qt + li;
     if (q >= L) continue;
     const float inv = 1.0f / st.ls[qt][0];
+    if constexpr (TRAIN) {
+      if (lg == 0) lse[((long)seq * H + h) * L + q] = -scale_log2e * st.negm[qt][0] + log2f(st.ls[qt][0]);
+    }
     bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * 32;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -578,7 +622,16 @@ extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, in
   SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
   const float sl2 = scale * 1.4426950408889634f;
   evlog_begin(s);
-  if (dh == 32)
+  if (dh == 32 && !getenv("SNVRAG_ATTN_TRAIN_V1")) {
+    // the inference kernel's structure (fixed shift, ones-MFMA row sums, 32 queries per wave) with
+    // unscaled Q, lse and dropout (attn32_bf16<false, true>)
+    const int nqb3 = cdiv(L, a32::QPB);
+    const long nb3 = (long)nqb3 * heads * nseq;
+    SNV_CHECK_ARG(nb3 < (1L << 31), "grid too large");
+    hipLaunchKernelGGL((attn32_bf16<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
+                       lse, drop);
+  } else if (dh == 32)
     hipLaunchKernelGGL(attn_fwd_bf16<32>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
                        (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);
   else if (dh == 64)
