@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--panel", default="sharded", choices=["sharded", "replicated"],
                    help="N>1: each rank holds 1/N of the panel and serves every rank's queries (SURVEY §8e), "
                         "or every rank holds the whole panel")
+    p.add_argument("--c2-n", type=int, default=10_000,
+                   help="SURVEY §8d C2 embedding-space cross-check: panel haplotypes embedded (bf16 [N, 1030*D]); 0 = skip")
     p.add_argument("--train-steps", type=int, default=3,
                    help="timed DDP training steps at configs[1] (B=24/GPU, window 1020, k=8, 10k-haplotype panel); 0 = skip")
     return p.parse_args()
@@ -248,6 +250,7 @@ def main():
         probes.append(pr)
     probe = dict(probes[-1], per_queries=[{kq: p[kq] for kq in ("queries", "avg_launch_ms", "achieved_gbs", "frac")}
                                           for p in probes])
+    c2 = knn_c2(args, wl, eng, k) if (args.c2_n > 0 and rank == 0 and dtype == torch.bfloat16) else None
     # precision leg: the same batch through the exact-f32 path, whose logits
     # carry the 1e-3 parity bar; report how often the bf16 run's imputed calls agree with it
     precision = precision_leg(args, wl, eng, k, out) if (args.f32_leg and dtype == torch.bfloat16) else None
@@ -303,6 +306,7 @@ def main():
                              note="all queries in one pass over the panel (XCD co-scheduled query groups); "
                                   "above ~150 queries the scan is int8-MFMA/LDS bound, see knn_hbm_probe"),
             "knn_hbm_probe": dict(probe, bound="hbm", peak=HBM_PEAK_GBS),
+            "knn_c2_embedding_space": c2,
             "knn_search_ms": round(knn_ms, 4),
             # (sharded panel: the search serves every rank's queries in that time)
             "knn_search_queries_per_s": round(2 * B * (world if shard is not None else 1) / (knn_ms * 1e-3), 1),
@@ -420,6 +424,88 @@ def train_bench(args, world, rank, dev):
             "n_gpus": world, "loss": round(float(loss), 3),
             "note": "DDP: bucketed async all-reduce of the flat f32 gradient buffer over RCCL; "
                     "reference banner: 115 ms/batch at B=24 on an unstated GPU (BASELINE.md)"}
+
+
+def knn_c2(args, wl, eng, k):
+    """SURVEY §8d C2 embedding-space mode (cross-check of the token index): the reference's
+    literal retrieval — bf16 window embeddings of the first ``args.c2_n`` panel haplotypes,
+    [N, 1030 * D], exact L2 + top-k (csrc/knn_emb.hip distance GEMM, HBM-bound) — timed at
+    Bq in {48, 96}; its neighbours checked against the token index's exact distances; and the
+    reference-equivalent CPU cost (torch.cdist + topk over a panel sample, the v18 training
+    path's own call) on the host cores."""
+    from src import kernels as K
+    from src import native as N
+    from src.dataset import utils as U
+    from src.retrieval import EmbeddingIndex, PanelIndex, panel_tokens
+    P = eng.packed()
+    dev = wl.tok.device
+    n, L, D, S = min(args.c2_n, wl.index.n_ref), wl.L, P.D, wl.S
+    codes = wl.index.codes[:n]
+    Ar = eng.af_embedding(torch.from_numpy(wl.ref_af).to(dev)[None]).float()[0].contiguous()
+    mask = U.sequence_padding(wl.raw_mask, "int")
+    tr = panel_tokens(codes, S, mask, L)
+    eidx = EmbeddingIndex.build(tr, P.W, P.pe, Ar)
+    lib, cap = N.lib(), 256
+    out = dict(mode="embedding-space exact L2 (reference-literal cdist / IndexFlatL2 over bf16 [N, L*D])",
+               panel_haplotypes=n, dims=L * D, index_bytes=int(eidx.E.numel() * 2), bound="hbm", peak=HBM_PEAK_GBS,
+               per_queries=[])
+    for bq in (48, 96):
+        Q = eidx.embed_queries(wl.tok[:bq], P.W, P.pe, Ar)
+        qn = K.knn_emb_norms(Q)
+        K.knn_emb_dist(eidx.E, Q, eidx.norms, qn)
+        lib.snvrag_evlog_enable(cap)
+        for _ in range(5):
+            K.knn_emb_dist(eidx.E, Q, eidx.norms, qn)
+        torch.cuda.synchronize()
+        kk, mm, ww = np.zeros(cap, np.int32), np.zeros(cap, np.float32), np.zeros(cap, np.float64)
+        n2 = lib.snvrag_evlog_read(kk.ctypes.data, mm.ctypes.data, ww.ctypes.data, cap)
+        lib.snvrag_evlog_enable(0)
+        sel = kk[:n2] == 4
+        ms, by = float(mm[:n2][sel].mean()), float(ww[:n2][sel].mean())
+        gbs = by / (ms * 1e-3) / 1e9
+        out["per_queries"].append(dict(queries=bq, avg_launch_ms=round(ms, 4), bytes_per_launch=by,
+                                       achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4)))
+    # cross-check at Bq = 96 against the token index over the same sub-panel: exact distances
+    # (float64 sums of ||W[a] - W[b]||^2 over token positions) of both neighbour lists
+    d_e, idx_e = eidx.search(Q, k)
+    pidx = PanelIndex(codes, S, wl.index.ref_af)
+    idx_t, _ = pidx.search(wl.tok[:96], P.W, wl.site_mask, k)
+    W64 = P.W.double()
+    T = ((W64[:, None] - W64[None]) ** 2).sum(-1)
+    tq = wl.tok[:96]
+
+    def exact(ix):
+        tr_sel = tr[ix]                                              # [Bq, k, L]
+        return T[tq[:, None, :].expand_as(tr_sel), tr_sel].sum(-1)
+    de, dt = exact(idx_e), exact(idx_t)
+    kth = dt[:, -1:]
+    out["cross_check"] = dict(
+        queries=96, k=k,
+        neighbours_within_exact_kth=round(float((de <= kth + 1.0).double().mean()), 6),
+        same_exact_distance_multiset=bool(torch.allclose(de.sort(1).values, dt, rtol=0, atol=1.0)),
+        index_overlap=round(float(sum(len(set(a) & set(b)) for a, b in zip(idx_e.tolist(), idx_t.tolist()))
+                                  / idx_t.numel()), 4),
+        max_rel_dist_err=round(float(((d_e.double() - de).abs() / de.clamp_min(1.0)).max()), 6),
+        note="distance ties are broken by bf16 rounding in embedding space and by index in the token index, "
+             "so index sets may differ at tied k-th distances; the exact-distance multisets must not")
+    # reference-equivalent CPU: torch.cdist + topk (embedding_rag_dataset.py:390-402) on a sample
+    threads = torch.get_num_threads()
+    m = min(n, 512)
+    Ec = eidx.E[:m].float().cpu()
+    Qc = Q[:48].float().cpu()
+    t0 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t0 < 3.0:
+        torch.topk(torch.cdist(Qc, Ec), min(k, m), dim=1, largest=False)
+        reps += 1
+    t_cpu = (time.perf_counter() - t0) / reps * (n / m)
+    out["cpu_reference_equivalent"] = dict(
+        queries=48, seconds_per_query_batch=round(t_cpu, 3), cores=threads, kind="reference-equivalent",
+        sample=f"torch.cdist + topk of 48 f32 queries vs {m} panel rows x {L * D} dims, scaled x{n / m:.1f} to {n}")
+    out["gpu_vs_cpu_at_48"] = round(t_cpu / (out["per_queries"][0]["avg_launch_ms"] * 1e-3), 1)
+    del eidx
+    torch.cuda.empty_cache()
+    return out
 
 
 def pmc_traffic(kernel_name):

@@ -389,6 +389,44 @@ def knn_decode(keys: torch.Tensor, exps: Optional[torch.Tensor] = None, consts: 
     return idx, dist
 
 
+def knn_emb_norms(E: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
+    """Squared L2 norms (f32) of the bf16 rows of E [N, K] — computed once when the embedding
+    index is built (the stored-norm half of IndexFlatL2's ||q||^2 + ||r||^2 - 2 q.r)."""
+    out = torch.empty(E.shape[0], device=E.device, dtype=torch.float32)
+    for i in range(0, E.shape[0], chunk):
+        out[i:i + chunk] = E[i:i + chunk].float().pow(2).sum(1)
+    return out
+
+
+def knn_emb_dist(E: torch.Tensor, Q: torch.Tensor, rn: torch.Tensor, qn: Optional[torch.Tensor] = None,
+                 splits: Optional[int] = None) -> torch.Tensor:
+    """Exact squared-L2 distances [Bq, N] between bf16 query rows Q [Bq, K] and the panel's
+    flattened window embeddings E [N, K] (csrc/knn_emb.hip; the reference's cdist over
+    [N, L * D], embedding_rag_dataset.py:390-402)."""
+    assert E.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16 and E.shape[1] == Q.shape[1]
+    n, kk = E.shape
+    bq = Q.shape[0]
+    assert 0 < bq <= 128 and kk % 64 == 0
+    if splits is None:
+        splits = int(N.lib().snvrag_knn_emb_splits(n, kk, bq))
+    if qn is None:
+        qn = knn_emb_norms(Q)
+    ws = torch.empty(int(N.lib().snvrag_knn_emb_ws_bytes(n, bq, splits)) // 4, device=E.device, dtype=torch.float32)
+    check(N.lib().snvrag_knn_emb_scan(ptr(_c(E)), n, kk, ptr(_c(Q)), bq, splits, ptr(ws), stream_ptr()),
+          "knn_emb_scan")
+    dist = torch.empty(bq, n, device=E.device, dtype=torch.float32)
+    check(N.lib().snvrag_knn_emb_finish(ptr(ws), splits, bq, n, ptr(_c(qn.float())), ptr(_c(rn.float())), ptr(dist),
+                                        stream_ptr()), "knn_emb_finish")
+    return dist
+
+
+def knn_emb_search(E: torch.Tensor, Q: torch.Tensor, k: int, rn: torch.Tensor, qn: Optional[torch.Tensor] = None):
+    """(dist [Bq, k], idx [Bq, k]) — the k nearest panel rows in embedding space, ascending
+    (torch.topk(largest=False) of embedding_rag_dataset.py:401 over the distance row)."""
+    d = knn_emb_dist(E, Q, rn, qn)
+    return torch.topk(d, k, dim=1, largest=False, sorted=True)
+
+
 def rag_mean(idx: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor, pe: torch.Tensor,
              Ar: Optional[torch.Tensor], L: int, dtype: torch.dtype, tok0=5, tok1=6, sos=2, eos=3, pad=0,
              out: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None):
