@@ -137,11 +137,15 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int nseq, int L, int H, con
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[kt][r] - m_new);
-          psum += p;
-          const int key = kbase + 16 * kt + 4 * lg + r;
-          pb[kt >> 1][(kt & 1) * 4 + r] = (bf16)(p * drop_mul(drop, dbase, (uint32_t)q, (uint32_t)key));
+        for (int r = 0; r < 4; r += 2) {
+          float dm[2];
+          drop_mul2(drop, dbase, (uint32_t)q, (uint32_t)(kbase + 16 * kt + 4 * lg + r), dm[0], dm[1]);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float p = exp2f(s[kt][r + e] - m_new);
+            psum += p;
+            pb[kt >> 1][(kt & 1) * 4 + r + e] = (bf16)(p * dm[e]);
+          }
         }
     } else {
 #pragma unroll
@@ -279,6 +283,7 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
   constexpr int NCB = (NKT + 1) / 2;
   bf16x8 pb[NCB][2];
   bf16x8 pd[TRAIN ? NCB : 1][2];                 // TRAIN: the dropped-out PV operand
+  float dmp[2] = {1.f, 1.f};                     // TRAIN: dropout multipliers of a key pair
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
@@ -289,10 +294,15 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
         if constexpr (TRAIN) {
           const float p = kt < NKT ? __builtin_amdgcn_exp2f(tr.c * s[kt < NKT ? kt : 0][qt][j & 3]) : 0.f;
           pb[cb][qt][j] = (bf16)p;
-          const float dm = tr.drop.thresh ? drop_mul(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
-                                                     (uint32_t)(kbase + 16 * kt + 4 * lg + (j & 3)))
-                                          : 1.f;
-          pd[cb][qt][j] = (bf16)(p * dm);
+          // keys 2i, 2i + 1 share one hash: computed at the even j, used at both
+          if ((j & 1) == 0) {
+            if (tr.drop.thresh)
+              drop_mul2(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
+                        (uint32_t)(kbase + 16 * kt + 4 * lg + (j & 3)), dmp[0], dmp[1]);
+            else
+              dmp[0] = dmp[1] = 1.f;
+          }
+          pd[cb][qt][j] = (bf16)(p * dmp[j & 1]);
         } else {
           pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
         }
@@ -362,15 +372,20 @@ __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, lo
       const float mn = fmaxf(m[qt], mx), alpha = exp2f(m[qt] - mn);
       bf16x8 pb{};
       float ps = 0.f;
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if constexpr (TRAIN) {
+        if (tr.drop.thresh) {
+          drop_mul2(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li), (uint32_t)(k0 + 4 * lg), dm[0], dm[1]);
+          drop_mul2(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li), (uint32_t)(k0 + 4 * lg + 2), dm[2], dm[3]);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float pf = exp2f(sc[r] - mn);
         const bf16 pr = (bf16)pf;
         ps += (float)pr;
         if constexpr (TRAIN)
-          pb[r] = tr.drop.thresh ? (bf16)(pf * drop_mul(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
-                                                        (uint32_t)(k0 + 4 * lg + r)))
-                                 : pr;
+          pb[r] = tr.drop.thresh ? (bf16)(pf * dm[r]) : pr;
         else
           pb[r] = pr;
       }

@@ -176,12 +176,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = t * 64 + 16 * kt + 4 * lg + r;
-        const float p = key < L ? exp2f(s[kt][r] * c_log2e - lse_q) : 0.f;
-        // dropout: dP = (dO V^T) o mask / (1 - p); D_q = rowsum(dO o O) is unchanged (O = P' V)
-        const float dpv = drop.thresh ? dp[kt][r] * drop_mul(drop, dbase, (uint32_t)q, (uint32_t)key) : dp[kt][r];
-        dsb[kt >> 1][(kt & 1) * 4 + r] = (bf16)(p * (dpv - dq_));
+      for (int r = 0; r < 4; r += 2) {
+        float dm[2] = {1.f, 1.f};
+        if (drop.thresh) drop_mul2(drop, dbase, (uint32_t)q, (uint32_t)(t * 64 + 16 * kt + 4 * lg + r), dm[0], dm[1]);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int key = t * 64 + 16 * kt + 4 * lg + r + e;
+          const float p = key < L ? exp2f(s[kt][r + e] * c_log2e - lse_q) : 0.f;
+          // dropout: dP = (dO V^T) o mask / (1 - p); D_q = rowsum(dO o O) is unchanged (O = P' V)
+          const float dpv = dp[kt][r + e] * dm[e];
+          dsb[kt >> 1][(kt & 1) * 4 + r + e] = (bf16)(p * (dpv - dq_));
+        }
       }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -277,6 +282,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
       }
     }
     bf16x8 pb[2], dsb[2];
+    // dropout multipliers: the keys of a hash pair sit in lanes li, li ^ 1 with the same 16
+    // queries, so each lane hashes half of them (r in {0,1} even lanes, {2,3} odd lanes) and
+    // swaps with its neighbour (DPP quad_perm [1,0,3,2]); it then takes its key's 16-bit half
+    float mkv[4][4];
+    if (drop.thresh) {
+      const bool odd = li & 1;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int r_mine = odd ? 2 + rr : rr;
+          const uint32_t hm = drop_hash(dbase, (uint32_t)(t * 64 + 16 * qt + 4 * lg + r_mine), (uint32_t)key >> 1);
+          const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+          const uint32_t h_lo = odd ? ho : hm, h_hi = odd ? hm : ho;       // hashes of r = rr, 2 + rr
+          mkv[qt][rr] = (odd ? h_lo >> 16 : h_lo & 0xFFFFu) >= drop.thresh ? drop.scale : 0.f;
+          mkv[qt][2 + rr] = (odd ? h_hi >> 16 : h_hi & 0xFFFFu) >= drop.thresh ? drop.scale : 0.f;
+        }
+    }
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
@@ -284,7 +307,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
         const int ql = 16 * qt + 4 * lg + r;
         const float p = (t * 64 + ql < L) ? exp2f(s[qt][r] * c_log2e - ls[ql]) : 0.f;
         // dropout: dV uses the kept, rescaled probabilities; dP is masked the same way
-        const float mk = drop.thresh ? drop_mul(drop, dbase, (uint32_t)(t * 64 + ql), (uint32_t)key) : 1.f;
+        const float mk = drop.thresh ? mkv[qt][r] : 1.f;
         pb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * mk);
         dsb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * (dp[qt][r] * mk - ls[64 + ql]));
       }

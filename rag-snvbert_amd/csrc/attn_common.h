@@ -29,10 +29,13 @@ __device__ __forceinline__ int k_off(int key, int chunk) {
 }
 
 // Attention-probability dropout (model/attention/attention.py:28-29) with a counter-based
-// RNG, so the forward and both backward kernels regenerate the same keep mask:
-//   h(q, k) = fmix32(base + q * 0x9E3779B1 + k * 0x85EBCA77),
+// RNG, so the forward and both backward kernels regenerate the same keep mask.  One hash
+// serves a key PAIR (2j, 2j + 1), 16 bits each — the mask costs half the integer multiplies
+// of a hash per probability in the kernels whose lanes hold consecutive keys:
+//   h(q, j) = fmix32(base + q * 0x9E3779B1 + j * 0x85EBCA77),
 //   base    = fmix32(lo(seed) ^ fmix32(hi(seed) + sh * 0xC2B2AE3D)),   sh = seq * heads + head
-// keep iff h >= thresh (thresh = p * 2^32); kept probabilities are scaled by 1 / (1 - p).
+// keep (q, k) iff half (k & 1) of h(q, k >> 1) >= thresh (thresh = round(p * 2^16), so the
+// drop probability is p to within 2^-17); kept probabilities are scaled by 1 / (1 - p).
 // thresh == 0: no dropout.  (tests/attn_helpers.py restates it for the parity tests.)
 struct AttnDrop {
   uint32_t thresh;
@@ -50,13 +53,25 @@ __host__ __device__ inline uint32_t drop_fmix32(uint32_t h) {
 __host__ __device__ inline uint32_t drop_base(uint64_t seed, uint32_t sh) {
   return drop_fmix32((uint32_t)seed ^ drop_fmix32((uint32_t)(seed >> 32) + sh * 0xC2B2AE3Du));
 }
+__device__ __forceinline__ uint32_t drop_hash(uint32_t base, uint32_t q, uint32_t pair) {
+  return drop_fmix32(base + q * 0x9E3779B1u + pair * 0x85EBCA77u);
+}
 // dropout multiplier of probability (q, k): 0 or 1 / (1 - p)
 __device__ __forceinline__ float drop_mul(const AttnDrop& d, uint32_t base, uint32_t q, uint32_t k) {
-  return drop_fmix32(base + q * 0x9E3779B1u + k * 0x85EBCA77u) >= d.thresh ? d.scale : 0.f;
+  const uint32_t h = drop_hash(base, q, k >> 1);
+  return ((k & 1u) ? h >> 16 : h & 0xFFFFu) >= d.thresh ? d.scale : 0.f;
+}
+// multipliers of (q, k) and (q, k + 1) for even k: one hash
+__device__ __forceinline__ void drop_mul2(const AttnDrop& d, uint32_t base, uint32_t q, uint32_t k, float& m0,
+                                          float& m1) {
+  const uint32_t h = drop_hash(base, q, k >> 1);
+  m0 = (h & 0xFFFFu) >= d.thresh ? d.scale : 0.f;
+  m1 = (h >> 16) >= d.thresh ? d.scale : 0.f;
 }
 static inline AttnDrop make_attn_drop(float p, uint64_t seed) {
   AttnDrop d;
-  d.thresh = p > 0.f ? (uint32_t)((double)p * 4294967296.0) : 0u;
+  const double t = (double)p * 65536.0 + 0.5;
+  d.thresh = p > 0.f ? (t < 1.0 ? 1u : (uint32_t)t) : 0u;
   d.scale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
   d.seed = seed;
   return d;

@@ -1,6 +1,7 @@
 """Host restatement of the attention-dropout keep mask (csrc/attn_common.h) for the parity tests:
-h(q, k) = fmix32(base + q * 0x9E3779B1 + k * 0x85EBCA77), base = fmix32(lo(seed) ^ fmix32(hi(seed) +
-sh * 0xC2B2AE3D)), keep iff h >= floor(p * 2^32)."""
+h(q, j) = fmix32(base + q * 0x9E3779B1 + j * 0x85EBCA77), base = fmix32(lo(seed) ^ fmix32(hi(seed) +
+sh * 0xC2B2AE3D)); key k uses 16-bit half (k & 1) of h(q, k >> 1); keep iff that half >=
+round(p * 2^16) (at least 1 when p > 0)."""
 import numpy as np
 
 M32 = np.uint64(0xFFFFFFFF)
@@ -18,7 +19,7 @@ def fmix32(h):
 
 def keep_mask(seed: int, nseq: int, heads: int, L: int, p: float) -> np.ndarray:
     """bool [nseq, heads, L(q), L(k)]"""
-    thresh = np.uint64(int(p * 4294967296.0))
+    thresh = np.uint64(max(1, int(p * 65536.0 + 0.5))) if p > 0 else np.uint64(0)
     lo, hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
     q = np.arange(L, dtype=np.uint64)
     out = np.zeros((nseq, heads, L, L), bool)
@@ -26,6 +27,8 @@ def keep_mask(seed: int, nseq: int, heads: int, L: int, p: float) -> np.ndarray:
         for h in range(heads):
             sh = np.uint64(sq * heads + h)
             base = fmix32(lo ^ fmix32((hi + sh * np.uint64(0xC2B2AE3D)) & M32))
-            x = (base + q[:, None] * np.uint64(0x9E3779B1) + q[None, :] * np.uint64(0x85EBCA77)) & M32
-            out[sq, h] = fmix32(x) >= thresh
+            x = (base + q[:, None] * np.uint64(0x9E3779B1) + (q[None, :] >> np.uint64(1)) * np.uint64(0x85EBCA77)) & M32
+            hh = fmix32(x)
+            half = np.where((q[None, :] & np.uint64(1)) == 1, hh >> np.uint64(16), hh & np.uint64(0xFFFF))
+            out[sq, h] = half >= thresh
     return out

@@ -72,6 +72,9 @@ def test_attention_dropout_forward_backward_vs_torch(nseq, L, H, dh, p):
     keep = torch.from_numpy(keep_mask(seed, nseq, H, L, p)).to(DEV)
     assert abs(keep.float().mean().item() - (1 - p)) < 0.01
     assert (torch.from_numpy(keep_mask(seed + 1, nseq, H, L, p)).to(DEV) != keep).float().mean() > 0.05
+    # the two keys of a hash pair (16-bit halves of one hash) drop independently
+    kp = keep.view(nseq, H, L, L // 2, 2)
+    assert abs((~kp[..., 0] & ~kp[..., 1]).float().mean().item() - p * p) < 0.01
     out, lse = K.attention_train_fwd(qkv, nseq, L, H, dh, p, seed)
     ref_in = qkv.float().clone().requires_grad_(True)
     x = ref_in.view(nseq, L, 3, H, dh).permute(2, 0, 3, 1, 4)
