@@ -502,6 +502,7 @@ def knn_c2(args, wl, eng, k):
     out["cpu_reference_equivalent"] = dict(
         queries=48, seconds_per_query_batch=round(t_cpu, 3), cores=threads, kind="reference-equivalent",
         sample=f"torch.cdist + topk of 48 f32 queries vs {m} panel rows x {L * D} dims, scaled x{n / m:.1f} to {n}")
+    out["traffic"] = pmc_traffic("knn_emb_dot_kernel")
     out["gpu_vs_cpu_at_48"] = round(t_cpu / (out["per_queries"][0]["avg_launch_ms"] * 1e-3), 1)
     del eidx
     torch.cuda.empty_cache()
@@ -512,7 +513,8 @@ def pmc_traffic(kernel_name):
     """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes run by tools/pmc.sh
     on this bench, committed as profiles/pmc_traffic.json), launch-weighted over the kernel class."""
     f = REPO / "profiles" / "pmc_traffic.json"
-    cls = {"rows_gemm_kernel": "gemm", "tail_kernel": "ffn", "ffn_kernel": "ffn", "attn32_bf16": "attention"}
+    cls = {"rows_gemm_kernel": "gemm", "tail_kernel": "ffn", "ffn_kernel": "ffn", "attn32_bf16": "attention",
+           "knn_emb_dot_kernel": "knn_emb"}
     key = next((v for k, v in cls.items() if kernel_name.startswith(k)), None)
     if key is None or not f.exists():
         return None
