@@ -38,7 +38,8 @@ def _f64_dist(Q, E):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,Kd,Bq,splits", [(1000, 64 * 7, 1, None), (333, 1030 * 32, 33, None), (2049, 4096, 64, 5),
-                                            (700, 64 * 101, 96, None), (129, 640, 128, 1), (64, 64, 48, 3)])
+                                            (700, 64 * 101, 96, None), (129, 640, 128, 1), (64, 64, 48, 3),
+                                            (1500, 1030 * 384, 96, None)])   # the bench's K (C2: L*D)
 def test_knn_emb_distance_kernel_vs_f64(N, Kd, Bq, splits):
     from src import kernels as K
     g = torch.Generator(device="cuda").manual_seed(N + Kd)
