@@ -213,7 +213,7 @@ int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const int32_t* ex
  * E bf16 [N, K] panel embeddings, Q bf16 [Bq, K] queries, K % 64 == 0, Bq <= 128.
  * scan: ws (f32, knn_emb_ws_bytes) <- per-split partial dots Q E^T;
  * finish: dist [Bq, N] f32 = qn[q] + rn[r] - 2 sum_split ws (qn, rn: squared norms).
- * splits: 1..64 (snvrag_knn_emb_splits picks one that fills the chip). */
+ * splits: 1..256 (snvrag_knn_emb_splits picks one that fills the chip). */
 int snvrag_knn_emb_splits(int64_t N, int64_t K, int Bq);
 size_t snvrag_knn_emb_ws_bytes(int64_t N, int Bq, int splits);
 int snvrag_knn_emb_scan(const void* E, int64_t N, int64_t K, const void* Q, int Bq, int splits, float* ws,
