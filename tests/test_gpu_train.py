@@ -90,6 +90,47 @@ def test_attention_dropout_forward_backward_vs_torch(nseq, L, H, dh, p):
         assert err <= 2e-2 * b.abs().max().item() + 1e-3, (name, err, b.abs().max().item())
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_train_overflow_fallback_with_dropout(p):
+    """Scores far above the first key tile's max overflow the fixed shift of the training
+    forward too: the online-max fallback must apply the same (pair-hash) keep mask and return
+    the same lse, so forward and backward still match torch.  (The softmax is saturated here,
+    so dQ is tiny next to the bf16 rounding of its O(1) terms: gradients are held to 2 % of the
+    largest gradient of the three.)"""
+    from src import kernels as K
+    from attn_helpers import keep_mask
+    nseq, L, H, dh = 2, 300, 2, 32
+    g = torch.Generator(device="cpu").manual_seed(5)
+    D = H * dh
+    qkv = torch.randn(nseq * L, 3 * D, generator=g) * 0.1
+    qkv[:, :D] = 4.0
+    qkv[200, D:2 * D] = 8.0
+    qkv = qkv.to(DEV, torch.bfloat16)
+    dout = torch.randn(nseq * L, D, generator=g).to(DEV, torch.bfloat16)
+    seed = 0x0BADC0FFEE
+    keep = torch.from_numpy(keep_mask(seed, nseq, H, L, p)).to(DEV) if p > 0 else torch.ones(
+        nseq, H, L, L, dtype=torch.bool, device=DEV)
+    K.attention_fallbacks(True)
+    out, lse = K.attention_train_fwd(qkv, nseq, L, H, dh, p, seed)
+    assert K.attention_fallbacks(True) > 0
+    ref_in = qkv.float().clone().requires_grad_(True)
+    x = ref_in.view(nseq, L, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s_ = (x[0] @ x[1].transpose(-1, -2)) / math.sqrt(dh)
+    P = torch.softmax(s_, -1)
+    ref = ((P * keep / (1 - p)) @ x[2]).permute(0, 2, 1, 3).reshape(nseq * L, D)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(lse, (torch.logsumexp(s_, -1) / math.log(2.0)).detach(), rtol=1e-3, atol=2e-2)
+    ref.backward(dout.float())
+    got = K.attention_bwd(qkv, out, dout, lse, nseq, L, H, dh, p, seed).float()
+    scale = ref_in.grad.abs().max().item()
+    for i, name in enumerate("qkv"):
+        a = got[:, i * D:(i + 1) * D]
+        b = ref_in.grad[:, i * D:(i + 1) * D]
+        err = (a - b).abs().max().item()
+        assert err <= 2e-2 * scale + 1e-3, (name, err, scale)
+
+
 def test_attention_lse_matches_logsumexp():
     from src import kernels as K
     nseq, L, H, dh = 2, 300, 2, 32
