@@ -7,7 +7,8 @@ are these Functions, whose forward and backward run the HIP kernels:
                   forward  y = x W^T + b             (snvrag_linear)
                   backward dx = dy W                 (snvrag_linear on W^T)
                            dW = dy^T x               (hipBLASLt via torch.mm — a plain
-                                                      library GEMM, long-K reduction)
+                                                      library GEMM, long-K reduction, f32
+                                                      result stored by the GEMM)
   hip_attention   unmasked softmax attention: flash forward that keeps the row
                   log-sum-exp, FlashAttention-2 style dq / dkv backward kernels.
   focal_loss      FocalLoss(reduction='sum') over masked rows, forward and derivative
@@ -109,6 +110,26 @@ def tiny_embedding(tok: torch.Tensor, W: torch.Tensor, padding_idx: Optional[int
     return _TinyVocabEmbedding.apply(tok, W, padding_idx)
 
 
+_MM_F32_OUT = None
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b (bf16) with an f32 result written by the GEMM itself (aten::mm.dtype on ROCm:
+    f32 accumulate, f32 store) — the weight gradient keeps its f32 accumulation instead of being
+    rounded to bf16 and widened again by a separate conversion kernel.  Falls back to the
+    bf16-output GEMM + widening where the dtype overload is unavailable."""
+    global _MM_F32_OUT
+    if _MM_F32_OUT is None:
+        try:
+            torch.mm(a[:8, :8], b[:8, :8], out_dtype=torch.float32)
+            _MM_F32_OUT = True
+        except (RuntimeError, TypeError, NotImplementedError):
+            _MM_F32_OUT = False
+    if _MM_F32_OUT:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return torch.mm(a, b).float()
+
+
 class _HipLinear(torch.autograd.Function):
     """y = x [W_1; ..; W_n]^T + [b_1; ..; b_n]: one GEMM over weights concatenated along the
     output dim (the q/k/v Linear layers of multi_head_attention.py:44 as one N = 3D GEMM)."""
@@ -146,7 +167,7 @@ class _HipLinear(torch.autograd.Function):
                 torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
             gx = K.linear(g2, wt).reshape(ctx.in_shape).to(ctx.in_dtype)
         if any(ctx.needs_input_grad[2:2 + ctx.n]):
-            gw = torch.mm(g2.t(), x2).float()
+            gw = _mm_f32(g2.t(), x2)
             gws = list(torch.split(gw, sizes, 0))
         if ctx.has_bias:
             gb = K.colsum(g2) if g2.shape[-1] % 8 == 0 and g2.shape[-1] <= 2048 else g2.float().sum(0)
