@@ -137,6 +137,19 @@ def _sg_stream(ws, bs, n_out: int):
     return ent[2], ent[3]
 
 
+def _sg_stream_t(w: torch.Tensor, n_out: int):
+    """Packed stream of W^T (the dX = dY W GEMM of a single Linear with out_features = 384)."""
+    base, key = _base_key(w)
+    key = ("T",) + key
+    ver = (base._version, _EPOCH[0])
+    ent = _SG.get(key)
+    if ent is None or ent[0][0]() is not base or ent[1] != ver:
+        ent = [[weakref.ref(base)], ver, K.sgemm_pack(bf16_of(w, transposed=True)),
+               torch.zeros(n_out, device=w.device, dtype=torch.float32)]
+        _SG[key] = ent
+    return ent[2], ent[3]
+
+
 def _sg_ok(x2: torch.Tensor, n_out: int) -> bool:
     """The stream GEMM takes the K = 384, no-activation projections (QKV, FFN w_1, fusion /
     head Linear layers): 850-900 TFLOP/s vs the row panel's ~550 at the training shapes."""
@@ -202,9 +215,15 @@ class _HipLinear(torch.autograd.Function):
         gws = [None] * ctx.n
         gbs = [None] * ctx.n
         if ctx.needs_input_grad[0]:
-            wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else \
-                torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
-            gx = K.linear(g2, wt).reshape(ctx.in_shape).to(ctx.in_dtype)
+            n_in = ctx.in_shape[-1]
+            if ctx.n == 1 and _sg_ok(g2, n_in):
+                wsp, vec = _sg_stream_t(ws[0], n_in)
+                gx = K.sgemm(g2, wsp, n_in, vec)
+            else:
+                wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else \
+                    torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
+                gx = K.linear(g2, wt)
+            gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
         if any(ctx.needs_input_grad[2:2 + ctx.n]):
             gw = _mm_f32(g2.t(), x2)
             gws = list(torch.split(gw, sizes, 0))
