@@ -10,8 +10,12 @@ with kNN queries/s reported beside it.  Workload = configs[2] of BASELINE.json:
 window 1024 sites, k = 32, 1M-haplotype panel resident in HBM, d384/L12/H12.
 
 Launch: python bench.py --gpus 1 --steps K --warmup W   (N>1: torch.distributed.run,
-one rank per GPU; each rank imputes its own B samples against its own HBM copy of
-the panel -> weak scaling, no data-path collective).
+one rank per GPU; each rank imputes its own B samples -> weak scaling).  With N>1 the
+default ``--panel sharded`` gives every rank a contiguous 1/N of the panel: the search
+all-gathers the ranks' query tokens, scans the local shard, all-gathers and merges the
+partial top-k keys and all-reduces the neighbours' alt-allele counts over RCCL
+(src/retrieval/shards.py); ``--panel replicated`` keeps a full HBM copy per
+rank and runs no data-path collective.
 """
 
 from __future__ import annotations
@@ -60,7 +64,8 @@ def parse():
     p.add_argument("--c2-n", type=int, default=10_000,
                    help="SURVEY §8d C2 embedding-space cross-check: panel haplotypes embedded (bf16 [N, 1030*D]); 0 = skip")
     p.add_argument("--train-steps", type=int, default=3,
-                   help="timed DDP training steps at configs[1] (B=24/GPU, window 1020, k=8, 10k-haplotype panel); 0 = skip")
+                   help="timed DDP training steps at configs[1] (B=24/GPU, window 512, k=8, 10k-haplotype panel); 0 = skip")
+    p.add_argument("--train-window", type=int, default=512, help="configs[1] window (sites) of the training leg")
     return p.parse_args()
 
 
@@ -379,15 +384,16 @@ def precision_leg(args, wl, eng, k, out_bf16):
 
 
 def train_bench(args, world, rank, dev):
-    """Training throughput at configs[1] / configs[3] shape: per GPU B=24 samples, window 1020
-    sites, k=8 neighbours from a 10k-haplotype panel, d384/L12/H12, bf16 + f32 master weights.
+    """Training throughput at configs[1] / configs[3] shape: per GPU B=24 samples, window 512
+    sites (configs[1]; the encoder still runs L = 1030 tokens), k=8 neighbours from a
+    10k-haplotype panel, d384/L12/H12, bf16 + f32 master weights.
     One step = retrieval + forward + focal losses + backward + bucketed all-reduce (RCCL when
     world > 1) + clipped fused Adam.  Timed like the main metric (barrier + sync around)."""
     from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
     from src.dataset.synthetic import make_rag_dataset
     from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from src.model import build_model
-    Bt, S, nref = 24, 1020, 5000
+    Bt, S, nref = 24, args.train_window, 5000
     ds, vocab = make_rag_dataset(n_samples=Bt, n_sites=S, n_windows=1, n_ref_samples=nref, seed=7 + rank,
                                  name="train")
     batch = embedding_rag_collate_fn([ds[i] for i in range(Bt)])

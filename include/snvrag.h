@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 21
+#define SNVRAG_ABI_VERSION 22
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -281,21 +281,13 @@ typedef struct {
   /* factor already folded into the q rows of w_qkv / b_qkv (0 = none); the bf16 engine
    * folds log2(e)/sqrt(dh) so attention's exp2 needs no per-score scaling */
   float q_scale;
-  /* optional (bf16, D in {128,256,384}): fused FFN weight stream from snvrag_ffn_pack
-   * and its vector table (see snvrag_ffn_forward); NULL = unfused GEMM path */
-  const void* ffn_w; const float* ffn_v;
-  /* optional (bf16): snvrag_wsg_pack of w_qkv -> the QKV projection runs on the
-   * weight-streaming GEMM */
-  const void* qkv_ws;
-  /* optional (bf16, with ffn_w/ffn_v): snvrag_ffn_pre_pack of w_o -> the attention
-   * output projection + LN1 run inside the fused FFN launch (snvrag_block_tail_forward) */
-  const void* o_ws;
-  /* optional (bf16, with ffn_v, D in {128,256,384}): snvrag_tail_pack of (w_o, w1, w2g) ->
-   * the whole block tail runs on the 32x32-MFMA kernel (snvrag_tail_forward); takes
-   * precedence over o_ws / ffn_w */
+  /* optional (bf16, D in {128,256,384}): the block tail's vector table (ffn_vec of
+   * snvrag_tail_forward) and snvrag_tail_pack of (w_o, w1, w2g) -> the whole block tail runs
+   * on the 32x32-MFMA kernel (snvrag_tail_forward); NULL = the row-panel GEMM path */
+  const float* ffn_v;
   const void* tail_w;
   /* optional (bf16, D in {128,256,384}): snvrag_proj_pack of w_qkv (NC = 3) -> the QKV
-   * projection runs on snvrag_proj_forward; takes precedence over qkv_ws */
+   * projection runs on snvrag_proj_forward when it is too large for the stream GEMM */
   const void* qkv_pw;
   /* optional (bf16, D in {128,256,384}): snvrag_sgemm_pack of w_qkv -> the QKV projection runs on
    * the stream GEMM (snvrag_sgemm_forward, epi 0); takes precedence over qkv_pw while
@@ -303,43 +295,14 @@ typedef struct {
   const void* qkv_sg;
 } snvrag_layer_t;
 
-/* ------------------------------------------------------------------------
- * Fused FFN sublayer (model/utils/feed_forward.py:18-21 + the output
- * SublayerConnection, model/transformer.py:34, sublayer.py:15-16), bf16, eval:
- *   out = LN2(x1 + lrelu(LN_f(lrelu(x1 W1^T + b1)) W2^T + b2))
- * in ONE launch; the [M, 4D] hidden never reaches HBM.  The weights are first
- * packed (once per model) into a fragment-ordered bf16 stream of
- * snvrag_ffn_pack_bytes(D) bytes:
- *   snvrag_ffn_pack(D, w1 [4D,D], w2g [D,4D], out, stream)
- * with w2g = w2 diag(lnf_g) (the FFN LayerNorm's gamma folded in).  vec is an
- * f32 table of 8*D floats (16-byte aligned):
- *   [b1 4D | b2' D | c1 D | ln2_g D | ln2_b D]
- * with b2' = b2 + w2 lnf_b and c1[n] = sum_k w2g[n,k] (of the bf16 values).
- * x1 and out are [M, D] bf16 and must not alias.  D in {128, 256, 384}.
- * ---------------------------------------------------------------------- */
-size_t snvrag_ffn_pack_bytes(int D);
-int snvrag_ffn_pack(int D, const void* w1, const void* w2g, void* out, void* stream);
-int snvrag_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
-                       const float* vec, float eps, void* stream);
-
-/* Whole block tail in ONE launch (multi_head_attention.py:51 output projection,
- * sublayer.py:15-16 x2, feed_forward.py:18-21), bf16, eval, in place on x:
- *   x1 = LN1(x + att W_o^T + b_o);  x = LN2(x1 + FFN(x1))
- * x1 stays in LDS.  wo_stream from snvrag_ffn_pre_pack (snvrag_ffn_pre_pack_bytes(D)
- * bytes), ffn_stream / ffn_vec as for snvrag_ffn_forward.  att, x [M, D] bf16, must
- * not alias; all pointers 16-byte aligned; D in {128, 256, 384}. */
-size_t snvrag_ffn_pre_pack_bytes(int D);
-int snvrag_ffn_pre_pack(int D, const void* w_o, void* out, void* stream);
-int snvrag_block_tail_forward(int64_t M, int D, const void* att, void* x, const void* wo_stream,
-                              const float* b_o, const float* ln1_g, const float* ln1_b,
-                              const void* ffn_stream, const float* ffn_vec, float eps, void* stream);
-
 /* Block tail on 32x32x16 MFMAs (csrc/tail.hip), bf16, eval — same math as
- * snvrag_block_tail_forward: x1 = LN1(x + att W_o^T + b_o); x = LN2(x1 + FFN(x1)), in place
+ * x1 = LN1(x + att W_o^T + b_o); x = LN2(x1 + FFN(x1)), in place
  * on x.  128 token rows per workgroup (4 waves x 32 rows), activations in registers, the
  * LDS a 9-slot ring of 16 KiB weight slabs.  ONE weight stream of snvrag_tail_pack_bytes(D)
  * bytes packed by snvrag_tail_pack(D, w_o [D,D], w1 [4D,D], w2g [D,4D], out, stream)
- * (w2g as for snvrag_ffn_pack); ffn_vec as for snvrag_ffn_forward.  att and x must not
+ * with w2g = w2 diag(lnf_g) (the FFN LayerNorm's gamma folded in).  ffn_vec is an f32
+ * table of 8*D floats (16-byte aligned): [b1 4D | b2' D | c1 D | ln2_g D | ln2_b D] with
+ * b2' = b2 + w2 lnf_b and c1[n] = sum_k w2g[n,k] (of the bf16 values).  att and x must not
  * alias; pointers 16-byte aligned; D in {128, 256, 384}.
  * snvrag_tail_ffn_forward: the FFN sublayer alone (out = LN2(x1 + FFN(x1))), same stream. */
 size_t snvrag_tail_pack_bytes(int D);
@@ -356,28 +319,6 @@ size_t snvrag_proj_pack_bytes(int D, int NC);
 int snvrag_proj_pack(int D, int NC, const void* w, void* out, void* stream);
 int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, const void* wstream, const float* bias,
                         void* out, void* stream);
-
-/* Weight-streaming row GEMM (bf16; multi_head_attention.py:44 QKV and :51 out-projection
- * + sublayer.py:15-16 LayerNorm): out[M, N] = A[M, K] W^T + bias, then either
- * act(.) (ln_g == NULL) or LN(act(.) + resid) * ln_g + ln_b (N == K, resid [M, ld_resid]).
- * Optional rank-1 terms row1[m'] * col1[n] + row2[m'] * col2[n] join the bias before the
- * activation (m' = m % row_period when row_period > 0): the cat(x, af, af_p) Linear inputs of
- * fusion.py:355-360 and foundation_model.py:25-33 without widening K.
- * A [M, K] contiguous; W packed once by snvrag_wsg_pack (wsg_pack_bytes(N, K) bytes).
- * K in {128, 256, 384}, N % 64 == 0 (N / 64 in {2,4,6,8,12,16,18,24} without LN). */
-size_t snvrag_wsg_pack_bytes(int64_t N, int64_t K);
-int snvrag_wsg_pack(int64_t N, int64_t K, const void* w, void* out, void* stream);
-int snvrag_wsg_forward(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
-                       int act, float slope, const void* resid, int64_t ld_resid, const float* ln_g,
-                       const float* ln_b, float eps, const float* row1, const float* col1, const float* row2,
-                       const float* col2, int64_t row_period, void* out, int64_t ldo, void* stream);
-
-/* Hap-classifier tail in one pass (foundation_model.py:77-80): probs[M, 2] =
- * softmax(act(A W^T + bias) w_out^T + b_out), logits (nullable) before the softmax;
- * the [M, N] hidden stays in registers.  (K, N) in {(384,1536), (256,1024), (128,512)}. */
-int snvrag_wsg_head2(int64_t M, int64_t N, int64_t K, const void* A, const void* wstream, const float* bias,
-                     int act, float slope, const float* w_out, const float* b_out, float* logits, float* probs,
-                     void* stream);
 
 /* Stream GEMM on 32x32x16 MFMAs (csrc/sgemm.hip), bf16, eval: x [M, D] W^T with W [N, D]
  * packed once by snvrag_sgemm_pack (snvrag_sgemm_pack_bytes(D, N) bytes; D in {128, 256,

@@ -1,5 +1,8 @@
-// Encoder stack orchestration: all n_layers x 8 launches of the transformer
-// blocks issued from C++ (one C-ABI call per forward, capturable in a hipGraph).
+// Encoder stack orchestration: every launch of the n_layers transformer blocks issued
+// from C++ (one C-ABI call per forward, capturable in a hipGraph).  bf16 at D in {128,
+// 256, 384}: 3 launches per layer (QKV stream GEMM, attention, block tail); otherwise (f32
+// parity path, other D) the row-panel GEMM form below with LN fused into the epilogues
+// (SNVRAG_UNFUSED_LN=1: the 8-launch unfused form, test-only).
 //
 // Per block (model/transformer.py:27-30, sublayer.py:15-16, feed_forward.py:18-21,
 // multi_head_attention.py:44-51), eval:
@@ -80,14 +83,13 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       snvrag_epilogue_t e{};
       int rc;
       e.bias = ly.b_qkv;
+      // QKV: the 8-wave stream GEMM (csrc/sgemm.hip); its 32-bit output offsets cap one launch
+      // at 2 GiB, beyond that the 32x32 projection stream (csrc/tail.hip PROJ mode)
       if (dtype == SNVRAG_BF16 && ly.qkv_sg && M * 3 * D * 2 < (1L << 31))
         rc = snvrag_sgemm_forward(M, (int)D, (int)(3 * D), 0, SNVRAG_ACT_NONE, 0.f, xc, ly.qkv_sg, ly.b_qkv, nullptr,
                                   nullptr, 0, 0.f, qkv, nullptr, nullptr, stream);
-      else if (dtype == SNVRAG_BF16 && ly.qkv_pw && !getenv("SNVRAG_NO_PROJ"))
+      else if (dtype == SNVRAG_BF16 && ly.qkv_pw)
         rc = snvrag_proj_forward(M, D, 3, xc, ly.qkv_pw, ly.b_qkv, qkv, stream);
-      else if (dtype == SNVRAG_BF16 && ly.qkv_ws && !getenv("SNVRAG_NO_WSG"))
-        rc = snvrag_wsg_forward(M, 3 * D, D, xc, ly.qkv_ws, ly.b_qkv, SNVRAG_ACT_NONE, 0.f, nullptr, 0, nullptr,
-                                nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, 0, qkv, 3 * D, stream);
       else
         rc = snvrag_linear(dtype, dtype, M, 3 * D, D, xc, D, ly.w_qkv, D, qkv, 3 * D, &e, stream);
       if (rc) return rc;
@@ -95,18 +97,9 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       const float sc = ly.q_scale > 0.f ? scale / ly.q_scale : scale;
       rc = snvrag_attention(dtype, ns, L, heads, dh, qkv, 3 * D, att, D, sc, stream);
       if (rc) return rc;
-      if (fused && dtype == SNVRAG_BF16 && ly.tail_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN") &&
-          !getenv("SNVRAG_NO_TAIL") && !getenv("SNVRAG_TAIL16")) {
+      if (fused && dtype == SNVRAG_BF16 && ly.tail_w && ly.ffn_v) {
         // the whole block tail on 32x32 MFMAs (csrc/tail.hip): one launch
         rc = snvrag_tail_forward(M, D, att, xc, ly.tail_w, ly.b_o, ly.ln1_g, ly.ln1_b, ly.ffn_v, 1e-5f, stream);
-        if (rc) return rc;
-        continue;
-      }
-      if (fused && dtype == SNVRAG_BF16 && ly.o_ws && ly.ffn_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN") &&
-          !getenv("SNVRAG_NO_TAIL")) {
-        // x = LN2(x1 + FFN(x1)), x1 = LN1(x + attn Wo^T + bo): one launch, x1 in LDS
-        rc = snvrag_block_tail_forward(M, D, att, xc, ly.o_ws, ly.b_o, ly.ln1_g, ly.ln1_b, ly.ffn_w, ly.ffn_v,
-                                       1e-5f, stream);
         if (rc) return rc;
         continue;
       }
@@ -116,12 +109,6 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
         e.bias = ly.b_o; e.resid = xc; e.ld_resid = D; e.ln_g = ly.ln1_g; e.ln_b = ly.ln1_b; e.ln_eps = 1e-5f;
         rc = snvrag_linear(dtype, dtype, M, D, D, att, D, ly.w_o, D, x1, D, &e, stream);
         if (rc) return rc;
-        if (dtype == SNVRAG_BF16 && ly.ffn_w && ly.ffn_v && !getenv("SNVRAG_UNFUSED_FFN")) {
-          // x = LN2(x1 + FFN(x1)) with the 4D hidden kept in registers (one launch)
-          rc = snvrag_ffn_forward(M, D, x1, xc, ly.ffn_w, ly.ffn_v, 1e-5f, stream);
-          if (rc) return rc;
-          continue;
-        }
         // h = lrelu(x1 W1^T + b1), row stats of h for the FFN LayerNorm (one launch)
         e = snvrag_epilogue_t{};
         e.bias = ly.b1; e.act = SNVRAG_ACT_LRELU; e.slope = 0.1f; e.stats_out = (float*)stats;

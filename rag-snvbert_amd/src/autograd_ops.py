@@ -163,15 +163,19 @@ _MM_F32_OUT = None
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a @ b (bf16) with an f32 result written by the GEMM itself (aten::mm.dtype on ROCm:
     f32 accumulate, f32 store) — the weight gradient keeps its f32 accumulation instead of being
-    rounded to bf16 and widened again by a separate conversion kernel.  Falls back to the
-    bf16-output GEMM + widening where the dtype overload is unavailable."""
+    rounded to bf16 and widened again by a separate conversion kernel.  Where the dtype overload
+    is unavailable it falls back to the bf16-output GEMM + widening and says so (once): the
+    weight gradients are then bf16-rounded."""
     global _MM_F32_OUT
     if _MM_F32_OUT is None:
         try:
             torch.mm(a[:8, :8], b[:8, :8], out_dtype=torch.float32)
             _MM_F32_OUT = True
-        except (RuntimeError, TypeError, NotImplementedError):
+        except (RuntimeError, TypeError, NotImplementedError) as e:
             _MM_F32_OUT = False
+            import warnings
+            warnings.warn(f"torch.mm(..., out_dtype=float32) unavailable ({e!r}): weight gradients fall back "
+                          "to a bf16-output GEMM (bf16-rounded dW)", RuntimeWarning, stacklevel=2)
     if _MM_F32_OUT:
         return torch.mm(a, b, out_dtype=torch.float32)
     return torch.mm(a, b).float()

@@ -9,7 +9,13 @@ Drop-in surface:
     ``rag_mean`` kernel as [B, 1, L, D] — the model consumes it identically
     (bert.py:180-182) — and ``rag_idx_h1/h2`` [B, k] carry the neighbour indices.
     ``dense=True`` returns the reference's fp32 [B, k, L, D] neighbour embeddings
-    (eval; the model's mean over k then equals the K-mean path).
+    (the model's mean over k then equals the K-mean path).
+    Train mode (``embedding_layer.training``, :404-442): ``rag_emb_h1/h2`` are f32 and
+    autograd-connected to the embedding parameters — each window's unique neighbours
+    re-encoded once with the layer's dropout (``train_forward.neighbour_embeddings``) — so
+    the reference trainer's hand-off of just those two keys
+    (pretrain_with_val_optimized.py:192-195) trains through the retrieval; ``rag_groups``
+    (the neighbour indices per window) rides along for inspection.
   * ``regenerate_masks(seed)``, ``clear_jit_cache()``, ``add_level()``,
     ``window_masks``, ``ref_tokens_complete``, ``ref_af_windows``, ``jit_cache_win_idx``.
 
@@ -27,6 +33,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from ..train_forward import NeighbourGroup
 from .dataset import PanelData, TrainDataset, Window
 from .utils import mask_probs, sequence_padding
 from .vocab import WordVocab
@@ -111,7 +118,14 @@ class EmbeddingRAGDataset(TrainDataset):
 
     # ----------------------------------------------------------------- items --
     def __getitem__(self, item: int) -> dict:
-        """embedding_rag_dataset.py:486-555: seeded AF-guided mask per (epoch|2024, window)."""
+        """embedding_rag_dataset.py:486-555: seeded AF-guided mask per (epoch|2024, window).
+        ``item >= len(self)``: a DistributedWindowSampler padding duplicate of item - len(self)
+        — the same tokens (retrieval and forward run as usual) with an all-zero metric mask, so
+        its sites enter no loss, F1 or accuracy."""
+        if item >= len(self):
+            out = self[item - len(self)]
+            out["mask"] = torch.zeros_like(out["mask"])
+            return out
         w = item % self.window_count
         # panel-filtered windows: featurise only the matched sites (the reference indexes its
         # padded arrays with the unpadded site filter here, :498-507, and raises KeyError on 'label')
@@ -231,31 +245,44 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         # windows built from one freq table); otherwise pass both AF embeddings (exact LUT form).
         afw = af[rows_t]
         same = bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw)))
-        counts = None
+        counts = uniq = None
+        p_drop = embedding_layer.dropout.p if train else 0.0
         with torch.no_grad():
             Ar_emb = eng.af_embedding(ref_af.unsqueeze(0), True).float()[0].contiguous() \
                 if P.af is not None else None
+            Aq_drop = None
+            if p_drop > 0 and len(rows):
+                # train mode: the reference embeds the queries WITH dropout before the distance
+                # (:385-386).  u = W[tok] + Aq - Ar must equal drop(e_q) - pe - A_r, so Aq carries
+                # drop(e_q) - W[tok] - pe per query row (exact-LUT form, fresh torch RNG mask)
+                Afull = eng.af_embedding(torch.cat([afw, afw]), True).float() if P.af is not None else 0.0
+                e_q = P.W[tok] + P.pe[:L] + Afull
+                Aq_drop = (torch.nn.functional.dropout(e_q, p_drop, True) - P.W[tok] - P.pe[:L]).contiguous()
             if shard is not None:
                 from ..retrieval.shards import any_rank, kernel_ops, sharded_neighbours
-                exact = P.af is not None and any_rank(not same, dev, shard.group)
+                drop_any = any_rank(p_drop > 0, dev, shard.group)
+                exact = P.af is not None and not drop_any and any_rank(not same, dev, shard.group)
                 ops = kernel_ops(index, P.W, site_mask, k, limbs,
                                  aq_fn=lambda a: eng.af_embedding(a, True).float().contiguous(),
-                                 Ar=Ar_emb if exact else None)
-                idx, _, counts = sharded_neighbours(tok, k, ops, torch.cat([afw, afw]) if exact else None,
-                                                    shard.group)
+                                 Ar=Ar_emb if (exact or drop_any) else None)
+                if drop_any and Aq_drop is None:
+                    # a rank without queries of this window (or p = 0 while another rank drops):
+                    # its rows still enter the exact-LUT launch, as undropped offsets
+                    Afull = eng.af_embedding(torch.cat([afw, afw]), True).float() if P.af is not None else 0.0
+                    Aq_drop = (Afull + torch.zeros(tok.shape[0], L, D, device=dev)).contiguous()
+                idx, _, extra = sharded_neighbours(tok, k, ops, torch.cat([afw, afw]) if exact else None,
+                                                   shard.group, aq_rows=Aq_drop if drop_any else None,
+                                                   want_codes=train and (drop_any or dense))
+                if train and (drop_any or dense):
+                    uniq = extra
+                else:
+                    counts = extra
             else:
                 Aq = Ar = None
                 aq_period = len(rows)
-                p_drop = embedding_layer.dropout.p if train else 0.0
-                if train and p_drop > 0 and len(rows):
-                    # train mode: the reference embeds the queries WITH dropout before the distance
-                    # (:385-386).  u = W[tok] + Aq - Ar must equal drop(e_q) - pe - A_r, so Aq carries
-                    # drop(e_q) - W[tok] - pe per query row (exact-LUT form, fresh torch RNG mask)
-                    Afull = eng.af_embedding(torch.cat([afw, afw]), True).float() if P.af is not None else 0.0
-                    e_q = P.W[tok] + P.pe[:L] + Afull
-                    Aq = (torch.nn.functional.dropout(e_q, p_drop, True) - P.W[tok] - P.pe[:L]).contiguous()
+                if Aq_drop is not None:
+                    Aq, aq_period = Aq_drop, 2 * len(rows)
                     Ar = Ar_emb if Ar_emb is not None else torch.zeros(L, D, device=dev)
-                    aq_period = 2 * len(rows)
                 elif not same and P.af is not None:
                     Aq = eng.af_embedding(afw, True).float().contiguous()
                     Ar = Ar_emb
@@ -264,8 +291,8 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         if nb == 0:
             continue
         if train:
-            # the model re-encodes the neighbours WITH grad (train_forward.neighbour_means)
-            rag_groups.append((rows_t, idx[:nb], idx[nb:], index, counts))
+            rag_groups.append(NeighbourGroup(rows_t, idx[:nb], idx[nb:], index, counts,
+                                             *(uniq if uniq is not None else (None, None))))
         else:
             if nb == B and rows == list(range(B)):      # one window, batch order: no scatter
                 K.rag_mean(idx, index.codes, n, P.W, P.pe, Ar_emb, L, eng.dtype, out=rag_mean, counts=counts)
@@ -289,6 +316,15 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         rag_idx[rows_t + B] = idx[nb:]
     batch["rag_idx_h1"], batch["rag_idx_h2"] = rag_idx[:B], rag_idx[B:]
     if train:
+        # the reference's train-mode contract (:404-442): rag_emb_h1/h2 re-encoded WITH grad
+        # (embedding dropout included) — the K-mean [B, 1, L, D] (bert.py:180-182 takes it as is)
+        # or, dense, every neighbour [B, k, L, D]; f32, connected to the embedding parameters
+        from ..train_forward import neighbour_embeddings
+        e = neighbour_embeddings(embedding_layer, rag_groups, B, L, dense=dense)
+        if dense:
+            batch["rag_emb_h1"], batch["rag_emb_h2"] = e[:B], e[B:]
+        else:
+            batch["rag_emb_h1"], batch["rag_emb_h2"] = e[:B].unsqueeze(1), e[B:].unsqueeze(1)
         batch["rag_groups"] = rag_groups
         return batch
     if dense:

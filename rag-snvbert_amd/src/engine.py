@@ -41,6 +41,16 @@ def engine_for(module: nn.Module) -> "Engine":
     return eng
 
 
+def _rag_block_current(x: Dict[str, torch.Tensor]) -> bool:
+    """True when the retrieval's in-place neighbour means (``rag_block`` / ``rag_mean``) still
+    back ``rag_emb_h1/h2`` (the views retrieval returned), or no rag_emb_* is given at all."""
+    if "rag_emb_h1" not in x or "rag_mean" not in x:
+        return True
+    m, B = x["rag_mean"], x["rag_emb_h1"].shape[0]
+    return (x["rag_emb_h1"].data_ptr() == m.data_ptr() and x["rag_emb_h2"].data_ptr() == m[B:].data_ptr()
+            and x["rag_emb_h1"].dtype == m.dtype)
+
+
 def set_compute_dtype(module: nn.Module, dtype: torch.dtype) -> None:
     """torch.float32 (exact-f32 MFMA parity path, the default) or torch.bfloat16."""
     engine_for(module).set_dtype(dtype)
@@ -115,8 +125,6 @@ class Engine:
         f32 = lambda t: t.detach().to(dev, torch.float32).contiguous()
         cvt = lambda t: t.detach().to(dev, T).contiguous()
         P.keep = []
-        # weight-streaming GEMM (csrc/wsgemm.hip) for the K = D projections at bf16
-        use_ws = T == torch.bfloat16 and os.environ.get("SNVRAG_NO_WSG") is None
 
         def afmlp(a):
             return dict(freqs=f32(a.basis_freqs), w0=cvt(a.projection[0].weight), b0=f32(a.projection[0].bias),
@@ -140,14 +148,12 @@ class Engine:
         fw = f32(ef.fusion.weight)
         P.ef = dict(w=cvt(fw[:, :D]), c_pos=fw[:, D].contiguous(), c_af=fw[:, D + 1].contiguous(),
                     b=f32(ef.fusion.bias), g=f32(ef.norm.weight), bb=f32(ef.norm.bias))
-        ws_ok = use_ws and D in (128, 256, 384)
-        # stream GEMM (csrc/sgemm.hip, 32x32 MFMAs, tile epilogues under the next tiles' MFMAs)
-        sg_ok = ws_ok and os.environ.get("SNVRAG_NO_SG") is None
+        # stream GEMM (csrc/sgemm.hip, 32x32 MFMAs, tile epilogues under the next tiles' MFMAs) for
+        # the K = D projections at bf16; the row-panel GEMM (gemm_rows.hip) otherwise
+        sg_ok = T == torch.bfloat16 and D in (128, 256, 384)
         if sg_ok:
             P.ef["w_sg"] = K.sgemm_pack(P.ef["w"])
             P.ef["v_sg"] = K.sgemm_vec(P.ef["b"], P.ef["c_pos"], P.ef["c_af"], ln=(P.ef["g"], P.ef["bb"]))
-        # (emb_fusion stays on the row-panel GEMM: at N = K = D over 4B*L rows the
-        #  weight-streaming LN epilogue measured 4 % slower)
         pf = ef.pos_feat
         P.pf_t = [f32(t) for t in (pf.conv1.weight, pf.conv1.bias, pf.conv2.weight, pf.conv2.bias,
                                    pf.conv3.weight, pf.conv3.bias, pf.norm1.weight, pf.norm1.bias,
@@ -169,15 +175,13 @@ class Engine:
                     rs=float(rf.res_scale.detach().float().item()))
         if sg_ok and D == 384 and P.rf["f0"].shape == (4 * D, 2 * D):
             P.rf["f0_sg"], P.rf["f0_v"] = K.sgemm_pack(P.rf["f0"]), K.sgemm_vec(P.rf["f0b"])
-        mlp_ok = sg_ok and D == 384 and os.environ.get("SNVRAG_NO_MLP") is None
+        mlp_ok = sg_ok and D == 384
         if mlp_ok and P.rf["a0"].shape == (4 * D, D) and P.rf["a3"].shape == (D, 4 * D):
             # af_adapter: Linear -> GELU -> Linear -> Sigmoid in one launch, hidden on chip
             P.rf["a_mlp"] = K.mlp_pack(P.rf["a0"], P.rf["a3"])
             P.rf["a_mlp_v"] = K.sgemm_vec(torch.cat([P.rf["a0b"], P.rf["a3b"]]))
         elif sg_ok and P.rf["a0"].shape == (4 * D, D):
             P.rf["a0_sg"], P.rf["a0_v"] = K.sgemm_pack(P.rf["a0"]), K.sgemm_vec(P.rf["a0b"])
-        elif ws_ok and P.rf["a0"].shape == (4 * D, D):
-            P.rf["a0_ws"] = K.wsg_pack(P.rf["a0"])
         # encoder
         P.layers_t, P.layers = [], []
         for blk in bert.transformer_blocks:
@@ -200,18 +204,13 @@ class Engine:
                      ln2_g=f32(blk.output_sublayer.norm.weight), ln2_b=f32(blk.output_sublayer.norm.bias),
                      w2g=w2g, b2g=b2g, c2g=c2g)
             if T == torch.bfloat16 and D in (128, 256, 384):
-                # fused FFN: one fragment-ordered weight stream + vector table (csrc/ffn.hip)
-                t["ffn_w"] = K.ffn_pack(t["w1"], w2g)
+                # the whole block tail (W_o' + W1 + W2') on 32x32 MFMAs (csrc/tail.hip) + its vectors
                 t["ffn_v"] = K.ffn_vec(t["b1"], b2g, w2g, t["ln2_g"], t["ln2_b"])
-                t["qkv_ws"] = K.wsg_pack(t["w_qkv"])
-                t["o_ws"] = K.ffn_pre_pack(t["w_o"])
-                # the whole block tail (W_o' + W1 + W2') on 32x32 MFMAs (csrc/tail.hip)
                 t["tail_w"] = K.tail_pack(t["w_o"], t["w1"], w2g)
-                # QKV projection on the same 32x32 stream kernel (csrc/tail.hip PROJ mode)
+                # QKV on the stream GEMM (csrc/sgemm.hip, 8 waves); the 32x32 projection stream
+                # (csrc/tail.hip PROJ mode) for launches past the stream GEMM's 2 GiB output
+                t["qkv_sg"] = K.sgemm_pack(t["w_qkv"])
                 t["qkv_pw"] = K.proj_pack(t["w_qkv"])
-                if os.environ.get("SNVRAG_NO_SG") is None:
-                    # ... and on the stream GEMM (csrc/sgemm.hip, 8 waves), which the engine prefers
-                    t["qkv_sg"] = K.sgemm_pack(t["w_qkv"])
             P.layers_t.append(t)
             P.layers.append(N.LayerW(**{k: v.data_ptr() for k, v in t.items()}, q_scale=qs))
         if fm is None:
@@ -223,7 +222,7 @@ class Engine:
                     g=f32(hc.af_fusion[3].weight), bb=f32(hc.af_fusion[3].bias),
                     n0=cvt(hc.net[0].weight), n0b=f32(hc.net[0].bias),
                     n2=f32(hc.net[2].weight), n2b=f32(hc.net[2].bias))
-        if sg_ok and D == 384 and os.environ.get("SNVRAG_NO_MLP") is None and P.hh["w2"].shape == (D, 4 * D):
+        if sg_ok and D == 384 and P.hh["w2"].shape == (D, 4 * D):
             # af_fusion: Linear over cat(x, af, af_p) -> GELU -> Linear -> LayerNorm in one launch
             P.hh["f_mlp"] = K.mlp_pack(P.hh["w0"], P.hh["w2"])
             P.hh["f_mlp_v"] = torch.cat([P.hh["b0"], P.hh["c_af"], P.hh["c_afp"], P.hh["b2"], P.hh["g"],
@@ -231,15 +230,10 @@ class Engine:
         elif sg_ok and P.hh["w0"].shape == (4 * D, D):
             P.hh["w0_sg"] = K.sgemm_pack(P.hh["w0"])
             P.hh["w0_v"] = K.sgemm_vec(P.hh["b0"], P.hh["c_af"], P.hh["c_afp"])
-        elif ws_ok and P.hh["w0"].shape == (4 * D, D):
-            P.hh["w0_ws"] = K.wsg_pack(P.hh["w0"])
         if sg_ok and P.hh["n2"].shape[0] == 2 and P.hh["n0"].shape == (4 * D, D):
             # net[0] + GELU + net[2] + softmax on the stream GEMM's head epilogue
             P.hh["n0_sg"] = K.sgemm_pack(P.hh["n0"])
             P.hh["n0_v"] = K.sgemm_vec(P.hh["n0b"], head=(P.hh["n2"], P.hh["n2b"]))
-        elif ws_ok and P.hh["n2"].shape[0] == 2:
-            # fused net[0] + GELU + net[2] + softmax (csrc/wsgemm.hip, EPI 2)
-            P.hh["n0_ws"] = K.wsg_pack(P.hh["n0"])
         gc = fm.gt_classifier
         P.gt_t = [f32(t) for t in (gc.gf_fusion.weight, gc.gf_fusion.bias, gc.gf_norm.weight, gc.gf_norm.bias,
                                    gc.layer.w_1.weight, gc.layer.w_1.bias, gc.layer.norm.weight,
@@ -287,7 +281,12 @@ class Engine:
         return torch.empty(4 * B, L, self.packed(allow_train=True).D, device=device, dtype=self.dtype)
 
     def rag_means(self, x: Dict[str, torch.Tensor], B: int, L: int, D: int) -> Optional[torch.Tensor]:
-        """[2B, L, D] K-means of retrieved neighbours in compute dtype (bert.py:171-183)."""
+        """[2B, L, D] K-means of retrieved neighbours in compute dtype (bert.py:171-183).
+        The retrieval's ``rag_block`` / ``rag_mean`` are used only while ``rag_emb_h1`` is still
+        the view of them the retrieval returned: a caller that replaced rag_emb_h1/h2 gets its
+        own tensors."""
+        if not _rag_block_current(x):
+            x = {k: v for k, v in x.items() if k not in ("rag_block", "rag_mean")}
         if "rag_block" in x:
             return x["rag_block"][2 * B:].to(self.dtype)
         if "rag_mean" in x:
@@ -310,7 +309,8 @@ class Engine:
         afemb = self.af_embedding(af)                                 # [B, L, D]
         rag = self.rag_means(x, B, L, D)
         nblk = 4 if rag is not None else 2
-        blk = x.get("rag_block")
+        # the retrieval's block: its query rows [:2B] are written in place by the embedding below
+        blk = x.get("rag_block") if _rag_block_current(x) else None
         if blk is not None and (blk.dtype != T or tuple(blk.shape) != (4 * B, L, D) or not blk.is_contiguous()):
             blk = None                                # produced for another dtype: copy below
         if blk is not None:
@@ -325,9 +325,6 @@ class Engine:
         if "w_sg" in ef:
             fused = K.sgemm(hm, ef["w_sg"], D, ef["v_sg"], epi=K.SG_LN, act=N.ACT_LRELU, slope=0.1,
                             rank=(pf, af, BL))
-        elif "w_ws" in ef:
-            fused = K.wsg_linear(hm, ef["w_ws"], D, ef["b"], act=N.ACT_LRELU, slope=0.1, resid=hm,
-                                 ln=(ef["g"], ef["bb"]), row1=(pf, ef["c_pos"]), row2=(af, ef["c_af"]), row_period=BL)
         else:
             fused = K.linear(hm, ef["w"], ef["b"], row1=(pf, 1, ef["c_pos"]), row2=(af, 1, ef["c_af"]),
                              row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm, ln=(ef["g"], ef["bb"]))
@@ -339,8 +336,6 @@ class Engine:
             else:
                 if "a0_sg" in rf:
                     t = K.sgemm(fa, rf["a0_sg"], rf["a0"].shape[0], rf["a0_v"], act=N.ACT_GELU)
-                elif "a0_ws" in rf:
-                    t = K.wsg_linear(fa, rf["a0_ws"], rf["a0"].shape[0], rf["a0b"], act=N.ACT_GELU)
                 else:
                     t = K.linear(fa, rf["a0"], rf["a0b"], act=N.ACT_GELU)
                 aw = K.linear(t, rf["a3"], rf["a3b"], act=N.ACT_SIGMOID)
@@ -373,9 +368,6 @@ class Engine:
             if "w0_sg" in hh:
                 h = K.sgemm(o["x_all"], hh["w0_sg"], hh["w0"].shape[0], hh["w0_v"], act=N.ACT_GELU,
                             rank=(o["af"], o["af_p"], BL))
-            elif "w0_ws" in hh:
-                h = K.wsg_linear(o["x_all"], hh["w0_ws"], hh["w0"].shape[0], hh["b0"], act=N.ACT_GELU,
-                                 row1=(o["af"], hh["c_af"]), row2=(o["af_p"], hh["c_afp"]), row_period=BL)
             else:
                 h = K.linear(o["x_all"], hh["w0"], hh["b0"], row1=(o["af"], 1, hh["c_af"]),
                              row2=(o["af_p"], 1, hh["c_afp"]), row_period=BL, act=N.ACT_GELU)
@@ -383,9 +375,6 @@ class Engine:
         if "n0_sg" in hh:
             logits, probs = K.sgemm(h, hh["n0_sg"], hh["n0"].shape[0], hh["n0_v"], epi=K.SG_HEAD2, act=N.ACT_GELU,
                                     want_logits=want_logits)
-        elif "n0_ws" in hh:
-            logits, probs = K.wsg_head2(h, hh["n0_ws"], hh["n0"].shape[0], hh["n0b"], hh["n2"], hh["n2b"],
-                                        act=N.ACT_GELU, want_logits=want_logits)
         else:
             h = K.linear(h, hh["n0"], hh["n0b"], act=N.ACT_GELU)
             logits, probs = K.hap_head_out(h, hh["n2"], hh["n2b"], want_logits=want_logits)

@@ -84,64 +84,10 @@ def fold_layernorm(w: torch.Tensor, b: torch.Tensor, g: torch.Tensor, beta: torc
     return wg, (w64 @ beta.double() + b.double()).float().contiguous(), (w64 @ g.double()).float().contiguous()
 
 
-def ffn_pack(w1: torch.Tensor, w2g: torch.Tensor) -> torch.Tensor:
-    """Fragment-ordered bf16 weight stream of the fused FFN kernel (csrc/ffn.hip)."""
-    D = w1.shape[1]
-    nbytes = int(N.lib().snvrag_ffn_pack_bytes(D))
-    if nbytes == 0:
-        raise ValueError(f"fused FFN needs D in (128, 256, 384), got {D}")
-    out = torch.empty(nbytes, device=w1.device, dtype=torch.uint8)
-    ws = [_c(t.to(torch.bfloat16)) for t in (w1, w2g)]
-    assert tuple(ws[0].shape) == (4 * D, D) and tuple(ws[1].shape) == (D, 4 * D)
-    check(N.lib().snvrag_ffn_pack(D, ptr(ws[0]), ptr(ws[1]), ptr(out), stream_ptr()), "ffn_pack")
-    return out
-
-
 def ffn_vec(b1, b2g, w2g, ln2_g, ln2_b) -> torch.Tensor:
     """[b1 (4D) | b2' | c1 | ln2_g | ln2_b] f32; c1 = row sums of the bf16 w2g."""
     c1 = w2g.to(torch.bfloat16).double().sum(1).float()
     return torch.cat([t.detach().float().reshape(-1) for t in (b1, b2g, c1, ln2_g, ln2_b)]).contiguous()
-
-
-def ffn_forward(x1: torch.Tensor, wstream: torch.Tensor, vec: torch.Tensor, eps: float = 1e-5,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = LN2(x1 + FFN(x1)) in one launch (bf16; model/utils/feed_forward.py:18-21)."""
-    N.require_gpu(x1)
-    assert x1.dtype == torch.bfloat16
-    D = x1.shape[-1]
-    M = x1.numel() // D
-    if out is None:
-        out = torch.empty_like(x1)
-    check(N.lib().snvrag_ffn_forward(M, D, ptr(_c(x1)), ptr(out), ptr(wstream), ptr(vec), eps, stream_ptr()),
-          "ffn_forward")
-    return out
-
-
-def ffn_pre_pack(w_o: torch.Tensor) -> torch.Tensor:
-    """W_o stream of the fused block tail (csrc/ffn.hip, PRE variant)."""
-    D = w_o.shape[1]
-    nbytes = int(N.lib().snvrag_ffn_pre_pack_bytes(D))
-    if nbytes == 0:
-        raise ValueError(f"fused block tail needs D in (128, 256, 384), got {D}")
-    out = torch.empty(nbytes, device=w_o.device, dtype=torch.uint8)
-    w = _c(w_o.to(torch.bfloat16))
-    assert tuple(w.shape) == (D, D)
-    check(N.lib().snvrag_ffn_pre_pack(D, ptr(w), ptr(out), stream_ptr()), "ffn_pre_pack")
-    return out
-
-
-def block_tail_forward(att: torch.Tensor, x: torch.Tensor, wo_stream: torch.Tensor, b_o, ln1_g, ln1_b,
-                       ffn_stream: torch.Tensor, ffn_vec: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
-    """x <- LN2(x1 + FFN(x1)), x1 = LN1(x + att W_o^T + b_o), in place, one launch (bf16)."""
-    N.require_gpu(att, x)
-    assert att.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and x.is_contiguous()
-    D = x.shape[-1]
-    M = x.numel() // D
-    f = [_c(t.float()) for t in (b_o, ln1_g, ln1_b)]
-    check(N.lib().snvrag_block_tail_forward(M, D, ptr(_c(att)), ptr(x), ptr(wo_stream), ptr(f[0]), ptr(f[1]),
-                                            ptr(f[2]), ptr(ffn_stream), ptr(ffn_vec), eps, stream_ptr()),
-          "block_tail_forward")
-    return x
 
 
 def tail_pack(w_o: torch.Tensor, w1: torch.Tensor, w2g: torch.Tensor) -> torch.Tensor:
@@ -739,57 +685,3 @@ def sgemm_cat(q: torch.Tensor, x2: torch.Tensor, g2: torch.Tensor, period: int, 
                                            ptr(vec), ptr(out), stream_ptr()), "sgemm_cat")
     return out
 
-
-def wsg_pack(w: torch.Tensor) -> torch.Tensor:
-    """Fragment-ordered bf16 weight stream of the weight-streaming GEMM (csrc/wsgemm.hip)."""
-    Nn, Kk = w.shape
-    nbytes = int(N.lib().snvrag_wsg_pack_bytes(Nn, Kk))
-    if nbytes == 0:
-        raise ValueError(f"weight-streaming GEMM needs N % 64 == 0 and K in (128, 256, 384), got {tuple(w.shape)}")
-    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
-    check(N.lib().snvrag_wsg_pack(Nn, Kk, ptr(_c(w.to(torch.bfloat16).contiguous())), ptr(out), stream_ptr()),
-          "wsg_pack")
-    return out
-
-
-def wsg_linear(x: torch.Tensor, wstream: torch.Tensor, n_out: int, bias: torch.Tensor, *, act: int = N.ACT_NONE,
-               slope: float = 0.0, resid: Optional[torch.Tensor] = None,
-               ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, eps: float = 1e-5,
-               row1: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-               row2: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, row_period: int = 0,
-               out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = act(x W^T + bias + row1[m] col1 + row2[m] col2), or LN(act(.) + resid) with ``ln``;
-    ``row1 = (row_vector f32, col_vector f32 [n_out])``, row index modulo ``row_period``."""
-    N.require_gpu(x)
-    Kk = x.shape[-1]
-    M = x.numel() // Kk
-    if out is None:
-        out = torch.empty(*x.shape[:-1], n_out, device=x.device, dtype=torch.bfloat16)
-    rows = []
-    for rc in (row1, row2):
-        if rc is None:
-            rows += [None, None]
-        else:
-            assert rc[0].dtype == torch.float32 and rc[1].dtype == torch.float32 and rc[1].numel() == n_out
-            assert rc[0].numel() >= (row_period if row_period > 0 else M)
-            rows += [_c(rc[0]), _c(rc[1])]
-    check(N.lib().snvrag_wsg_forward(M, n_out, Kk, ptr(_c(x)), ptr(wstream), ptr(_c(bias)), act, slope,
-                                     ptr(resid), n_out if resid is not None else 0,
-                                     ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, eps,
-                                     *[ptr(t) for t in rows], row_period, ptr(out), n_out, stream_ptr()),
-          "wsg_linear")
-    return out
-
-
-def wsg_head2(x: torch.Tensor, wstream: torch.Tensor, n_hidden: int, bias: torch.Tensor, w_out: torch.Tensor,
-              b_out: torch.Tensor, act: int = N.ACT_GELU, want_logits: bool = False):
-    """(logits or None, probs) [..., 2] of softmax(act(x W^T + b) w_out^T + b_out) in one launch."""
-    N.require_gpu(x)
-    Kk = x.shape[-1]
-    M = x.numel() // Kk
-    probs = torch.empty(*x.shape[:-1], 2, device=x.device, dtype=torch.float32)
-    logits = torch.empty_like(probs) if want_logits else None
-    check(N.lib().snvrag_wsg_head2(M, n_hidden, Kk, ptr(_c(x)), ptr(wstream), ptr(_c(bias)), act, 0.0,
-                                   ptr(_c(w_out)), ptr(_c(b_out)), ptr(logits), ptr(probs), stream_ptr()),
-          "wsg_head2")
-    return logits, probs

@@ -121,10 +121,12 @@ class GradBucketer:
     """Bucketed asynchronous all-reduce (SUM) of FlatParams.grad; averaging is folded into
     FusedAdam's grad_scale (1 / world)."""
 
-    def __init__(self, flat: FlatParams, bucket_bytes: int = 32 << 20, group=None):
+    def __init__(self, flat: FlatParams, bucket_bytes: int = 32 << 20, group=None, always: bool = False):
+        """``always``: run the collectives even in a world of one (the RCCL smoke test)."""
         self.fp = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = self.world > 1 or (always and dist.is_initialized())
         self.buckets: List[List[int]] = []        # param indices (flat order)
         self.bounds: List[tuple] = []
         cur, start, size = [], 0, 0
@@ -144,7 +146,7 @@ class GradBucketer:
         self.handles: Dict[int, object] = {}
         self.enabled = True
         self._hooks = []
-        if self.world > 1:
+        if self.active:
             for i, p in enumerate(flat.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
 
@@ -170,7 +172,7 @@ class GradBucketer:
     def finish(self) -> float:
         """Wait for every bucket (launching those whose parameters got no gradient this step);
         returns the grad scale that averages over ranks."""
-        if self.world > 1:
+        if self.active:
             for b in range(len(self.buckets)):
                 if b not in self.handles:
                     self._launch(b)

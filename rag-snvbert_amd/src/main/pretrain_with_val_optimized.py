@@ -76,12 +76,15 @@ class BERTTrainerWithValidationOptimized:
         return out
 
     def loss(self, output, data) -> torch.Tensor:
+        """(3 FL(h1) + 3 FL(h2) + 4 FL(gt)) / grad_accum_steps over the masked sites
+        (pretrain_with_val_optimized.py:215-233) and the three unweighted focal losses the
+        reference's metrics accumulate (:312-313)."""
         masks = data["mask"].bool()
         w = 1.0 / self.grad_accum_steps
-        l1 = self.hap_criterion(output[0], data["hap_1_label"], masks, 3.0 * w)
-        l2 = self.hap_criterion(output[1], data["hap_2_label"], masks, 3.0 * w)
-        lg = self.gt_criterion(output[2], data["gt_label"], masks, 4.0 * w)
-        return l1 + l2 + lg, (l1, l2, lg)
+        l1 = self.hap_criterion(output[0], data["hap_1_label"], masks)
+        l2 = self.hap_criterion(output[1], data["hap_2_label"], masks)
+        lg = self.gt_criterion(output[2], data["gt_label"], masks)
+        return (3.0 * l1 + 3.0 * l2 + 4.0 * lg) * w, (l1, l2, lg)
 
     def train_step(self, data: Dict) -> torch.Tensor:
         """One micro-batch: retrieval, forward, loss, backward (+ optimizer step on the last
@@ -139,47 +142,106 @@ class BERTTrainerWithValidationOptimized:
                 loss_sum += torch.stack([p.detach().float() for p in parts])
                 m = data["mask"].bool()
                 maf = torch.minimum(data["af"], 1 - data["af"])
-                is_rare = (maf < self.rare_threshold) & m
+                is_rare = (maf < self.rare_threshold) & m          # :281-288
                 for k, lab in ((0, "hap_1_label"), (1, "hap_2_label")):
                     hap.update(output[k], data[lab], m)
                     rare.update(output[k], data[lab], m, is_rare)
                     common.update(output[k], data[lab], m, (~is_rare) & m)
                 gt.update(output[2], data["gt_label"], m)
             n_batches += 1
-            if train and self.log_freq and (i + 1) % self.log_freq == 0 and self.rank == 0:
+            if train and self.log_freq and i % self.log_freq == 0 and self.rank == 0:
+                # _print_log (:335-360): ALT-class (class 1) haplotype precision / recall / F1
+                c = hap.counts.float().cpu()
+                p_, r_, f_ = self.calculate_metrics(c[0], c[1], c[2])
                 ls = (loss_sum / n_batches).tolist()
-                print(f"EP_Train:{epoch} it {i + 1} loss h1 {ls[0]:.4f} h2 {ls[1]:.4f} gt {ls[2]:.4f} "
+                print(f"EP_Train:{epoch} it {i} Precision {p_[1].item():.4f} Recall {r_[1].item():.4f} "
+                      f"F1 {f_[1].item():.4f} avg_hap_loss {ls[0] + ls[1]:.4f} avg_gt_loss {ls[2]:.4f} "
                       f"{(time.perf_counter() - t0) / (i + 1) * 1e3:.1f} ms/it", flush=True)
         torch.cuda.synchronize(dev) if dev.type == "cuda" else None
         elapsed = time.perf_counter() - t0
-        ls = (loss_sum / max(n_batches, 1)).tolist()
-        res = {"epoch": epoch, "mode": "train" if train else "val", "hap_loss": ls[0] + ls[1], "gt_loss": ls[2],
-               "hap_f1": hap.f1(), "gt_f1": gt.f1(), "rare_f1": rare.f1(), "common_f1": common.f1(),
-               "batches": n_batches, "sec": elapsed}
-        self.epoch_metrics.append(res)
+        ls = loss_sum.tolist()
+        counts = {name: conf.counts.cpu() for name, conf in
+                  (("hap", hap), ("gt", gt), ("rare", rare), ("common", common))}
+        row = self.metric_row(epoch, train, counts, ls[0] + ls[1], max(n_batches, 1))
+        self.epoch_metrics.append(row)
+        res = dict(row)
+        for name, c in counts.items():                         # eval_dict's tp / fp / fn (:132-154)
+            res[f"{name}_tp"], res[f"{name}_fp"], res[f"{name}_fn"] = c[0], c[1], c[2]
+        gt_p, gt_r, gt_f1 = self.calculate_metrics(*counts["gt"].float())
+        res.update(hap_loss=ls[0] + ls[1], gt_loss=ls[2], gt_f1=float(gt_f1.mean()), batches=n_batches, sec=elapsed)
         if self.rank == 0:
-            print(f"{'Train' if train else 'Val'} epoch {epoch}: " +
-                  " ".join(f"{k}={v:.4f}" if isinstance(v, float) else f"{k}={v}" for k, v in res.items()),
-                  flush=True)
+            print(f"{'Train' if train else 'Val'} epoch {epoch + 1}: " +
+                  " ".join(f"{k}={v:.4f}" if isinstance(v, float) else f"{k}={v}" for k, v in row.items()) +
+                  f" gt_avg_f1={res['gt_f1']:.4f} {elapsed:.1f}s", flush=True)
             if self.output_csv:
-                new = not os.path.exists(self.output_csv)
-                with open(self.output_csv, "a", newline="") as f:
-                    w = csv.DictWriter(f, fieldnames=list(res))
-                    if new:
-                        w.writeheader()
-                    w.writerow(res)
+                self._save_epoch_metrics(row)
         return res
 
+    # ------------------------------------------------------------ metrics --
+    @staticmethod
+    def calculate_metrics(tp: torch.Tensor, fp: torch.Tensor, fn: torch.Tensor):
+        """Per-class precision, recall, F1 (pretrain_with_val_optimized.py:483-488), f32."""
+        tp, fp, fn = tp.float(), fp.float(), fn.float()
+        precision = tp / (tp + fp + 1e-10)
+        recall = tp / (tp + fn + 1e-10)
+        f1 = 2 * precision * recall / (precision + recall + 1e-10)
+        return precision, recall, f1
+
+    def metric_row(self, epoch: int, train: bool, counts: Dict[str, torch.Tensor], hap_loss_sum: float,
+                   num_batches: int, correct: Optional[int] = None, total: Optional[int] = None) -> Dict:
+        """The reference's per-epoch CSV row (:424-481): ALT-class (index 1) metrics overall and
+        split into rare (MAF < rare_threshold) / common sites; ``counts[name]`` = [tp; fp; fn] per
+        class; accuracy = correct / masked haplotype sites (cal_acc, optim_schedule.py:99-109) —
+        by default from the counts (an argmax call is right iff it is a TP of its label's class,
+        and every masked site is a TP or an FN of its label's class)."""
+        c = counts["hap"]
+        hp, hr, hf = self.calculate_metrics(c[0], c[1], c[2])
+        rp, rr, rf = self.calculate_metrics(*counts["rare"])
+        cp, cr, cf = self.calculate_metrics(*counts["common"])
+        if correct is None:
+            correct, total = int(c[0].sum()), int((c[0] + c[2]).sum())
+        return {"epoch": epoch + 1, "mode": "train" if train else "val",
+                "loss": hap_loss_sum / num_batches,
+                "accuracy": correct / total if total else float("nan"),
+                "overall_f1": hf[1].item(), "overall_precision": hp[1].item(), "overall_recall": hr[1].item(),
+                "rare_f1": rf[1].item(), "rare_precision": rp[1].item(), "rare_recall": rr[1].item(),
+                "common_f1": cf[1].item(), "common_precision": cp[1].item(), "common_recall": cr[1].item()}
+
+    def _save_epoch_metrics(self, row: Dict) -> None:
+        """Append ``row`` to output_csv, header on first write (:466-481)."""
+        os.makedirs(os.path.dirname(self.output_csv) or ".", exist_ok=True)
+        new = not os.path.exists(self.output_csv)
+        with open(self.output_csv, "a", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(row))
+            if new:
+                w.writeheader()
+            w.writerow(row)
+
     # ------------------------------------------------------------- checkpoint --
-    def save(self, epoch: int, file_path: str = "output/bert_trained.model") -> str:
-        """state_dict checkpoint (+ optimizer/schedule state) instead of the reference's pickled
-        module (pretrain_with_val_optimized.py:524-552): loadable with weights_only=True."""
+    def _checkpoint(self, epoch: int) -> Dict:
+        ck = {"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+              "optim": self.optim.state_dict(), "schedule_steps": self.optim_schedule.n_current_steps,
+              "epoch": epoch, "best_val_metric": float(self.best_val_metric),
+              "epochs_no_improve": int(self.epochs_no_improve)}
+        sampler = getattr(self.train_data, "sampler", None)
+        if sampler is not None and hasattr(sampler, "state_dict"):
+            ck["sampler"] = sampler.state_dict()
+        return ck
+
+    def save(self, epoch: int, file_path: str = "output/bert_trained.model", is_best: bool = False) -> str:
+        """``<file_path>.ep<epoch>`` and, ``is_best``, ``<file_path>.best.pth`` (:524-552) — as
+        state_dict checkpoints (+ optimizer, LR-schedule, early-stopping and sampler state)
+        instead of the reference's pickled module: loadable with weights_only=True."""
         path = f"{file_path}.ep{epoch}"
         if self.rank == 0:
             os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-            torch.save({"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
-                        "optim": self.optim.state_dict(),
-                        "schedule_steps": self.optim_schedule.n_current_steps, "epoch": epoch}, path)
+            ck = self._checkpoint(epoch)
+            torch.save(ck, path)
+            if is_best:
+                self.best_model_path = f"{file_path}.best.pth"
+                torch.save(ck, self.best_model_path)
+                print(f"Best model saved: {self.best_model_path}", flush=True)
+            print(f"EP:{epoch} Model Saved: {path}", flush=True)
         return path
 
     def load(self, path: str) -> int:
@@ -191,15 +253,29 @@ class BERTTrainerWithValidationOptimized:
         if "optim" in ck:
             self.optim.load_state_dict(ck["optim"])
             self.optim_schedule.n_current_steps = int(ck.get("schedule_steps", 0))
+        if "best_val_metric" in ck:
+            self.best_val_metric = float(ck["best_val_metric"])
+            self.epochs_no_improve = int(ck.get("epochs_no_improve", 0))
+        sampler = getattr(self.train_data, "sampler", None)
+        if "sampler" in ck and sampler is not None and hasattr(sampler, "load_state_dict"):
+            sampler.load_state_dict(ck["sampler"])
         return int(ck.get("epoch", 0))
 
-    def should_stop_early(self, val_res: Dict) -> bool:
-        key = {"f1": "hap_f1", "accuracy": "hap_f1", "loss": "hap_loss"}.get(self.val_metric, "hap_f1")
-        v = val_res[key]
-        better = v > self.best_val_metric + self.min_delta if self.val_metric != "loss" else \
-            v < self.best_val_metric - self.min_delta
-        if better:
-            self.best_val_metric, self.epochs_no_improve = v, 0
+    def should_stop_early(self, val_metrics: Dict, epoch: Optional[int] = None) -> bool:
+        """Early stopping on the validation ALT-class haplotype F1, hap_f1[1] (:490-522) — the
+        reference computes it from the epoch's TP/FP/FN whatever ``val_metric`` says."""
+        if "hap_tp" in val_metrics:
+            _, _, f1 = self.calculate_metrics(val_metrics["hap_tp"], val_metrics["hap_fp"], val_metrics["hap_fn"])
+            current = f1[1].item()
+        else:
+            current = float(val_metrics["overall_f1"])
+        if current > self.best_val_metric + self.min_delta:
+            self.best_val_metric, self.epochs_no_improve = current, 0
+            if self.rank == 0:
+                print(f"New best {self.val_metric}: {current:.4f}", flush=True)
             return False
         self.epochs_no_improve += 1
+        if self.rank == 0:
+            print(f"No improvement for {self.epochs_no_improve} epoch(s) (best: {self.best_val_metric:.4f}, "
+                  f"current: {current:.4f})", flush=True)
         return self.epochs_no_improve >= self.patience

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -70,7 +70,7 @@ class AdamS(C.Structure):
 class LayerW(C.Structure):
     _fields_ = [(n, vp) for n in ("w_qkv", "b_qkv", "w_o", "b_o", "ln1_g", "ln1_b", "w1", "b1",
                                   "lnf_g", "lnf_b", "w2", "b2", "ln2_g", "ln2_b", "w2g", "b2g", "c2g")] + [("q_scale", f32)] + \
-        [("ffn_w", vp), ("ffn_v", vp), ("qkv_ws", vp), ("o_ws", vp), ("tail_w", vp), ("qkv_pw", vp), ("qkv_sg", vp)]
+        [("ffn_v", vp), ("tail_w", vp), ("qkv_pw", vp), ("qkv_sg", vp)]
 
 
 _SIGS = {
@@ -116,12 +116,6 @@ _SIGS = {
     "snvrag_encoder_ws_bytes": ([C.c_int, i64, i64, C.c_int, C.c_int], sz),
     "snvrag_encoder_forward": ([C.c_int, i64, i64, C.c_int, C.c_int, C.c_int, C.POINTER(LayerW), vp, vp, sz, vp],
                                C.c_int),
-    "snvrag_ffn_pack_bytes": ([C.c_int], sz),
-    "snvrag_ffn_pack": ([C.c_int, vp, vp, vp, vp], C.c_int),
-    "snvrag_ffn_forward": ([i64, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
-    "snvrag_ffn_pre_pack_bytes": ([C.c_int], C.c_size_t),
-    "snvrag_ffn_pre_pack": ([C.c_int, vp, vp, vp], C.c_int),
-    "snvrag_block_tail_forward": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp], C.c_int),
     "snvrag_proj_pack_bytes": ([C.c_int, C.c_int], C.c_size_t),
     "snvrag_proj_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),
     "snvrag_proj_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, vp, vp], C.c_int),
@@ -146,11 +140,6 @@ _SIGS = {
     "snvrag_sgemm_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),
     "snvrag_sgemm_forward": ([i64, C.c_int, C.c_int, C.c_int, C.c_int, f32, vp, vp, vp, vp, vp, i64, f32, vp, vp, vp,
                               vp], C.c_int),
-    "snvrag_wsg_pack_bytes": ([i64, i64], sz),
-    "snvrag_wsg_pack": ([i64, i64, vp, vp, vp], C.c_int),
-    "snvrag_wsg_head2": ([i64, i64, i64, vp, vp, vp, C.c_int, f32, vp, vp, vp, vp, vp], C.c_int),
-    "snvrag_wsg_forward": ([i64, i64, i64, vp, vp, vp, C.c_int, f32, vp, i64, vp, vp, f32, vp, vp, vp, vp, i64, vp, i64,
-                            vp], C.c_int),
     "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, vp], C.c_int),
     "snvrag_ln_bwd_ws_bytes": ([i64, C.c_int], sz),
     "snvrag_ln_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),

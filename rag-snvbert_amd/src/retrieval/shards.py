@@ -13,8 +13,12 @@ and serves the queries of ALL ranks against it; one retrieval step is
      each rank counts the neighbours it owns for all queries, an all-reduce (SUM, u8,
      nq_all x n_sites_pad bytes) completes the counts, each rank keeps its own rows.
 
-No neighbour codes or embeddings cross the links (a [nq, k, sites] code exchange would
-be k times larger, a [nq, L, D] embedding reduction ~750x).  The compute steps are
+In eval no neighbour codes or embeddings cross the links (a [nq, k, sites] code exchange
+would be k times larger, a [nq, L, D] embedding reduction ~750x).  Train mode with dropout
+needs each neighbour's own dropout mask and drop(e_q) in the distance, so there step 1 also
+all-gathers the dropped-out query offsets and step 4 exchanges the codes of the unique
+retrieved haplotypes instead of counts (sharded_neighbours ``aq_rows`` / ``want_codes``:
+at C4, 48 queries x 1030 x 384 f32 = 76 MB per rank and <= 3 MB of codes).  The compute steps are
 pluggable (``ShardOps``): the product uses the HIP kernels, the world-2 gloo test the
 oracle's on the CPU, over the same collective plumbing.
 """
@@ -113,11 +117,14 @@ class ShardOps:
     keys(tok, af_rows) -> (keys [nq, k] uint64-as-int64 with global indices, exps, consts)
     merge(keys [n_lists, nq, k], k) -> [nq, k]
     decode(keys, exps, consts) -> (idx int64 [nq, k], dist f32 [nq, k])
-    counts(idx [nq, k]) -> u8 [nq, ld]: alt-allele counts over the neighbours this shard owns"""
+    counts(idx [nq, k]) -> u8 [nq, ld]: alt-allele counts over the neighbours this shard owns
+    codes(uniq [U]) -> u8 [U, ld]: the codes of the rows this shard owns, zero rows elsewhere
+    (keys also takes a third argument, per-query embedding offsets [nq, L, D], when given)"""
     keys: Callable
     merge: Callable
     decode: Callable
     counts: Callable
+    codes: Optional[Callable] = None
 
 
 def batch_windows(windows, group=None) -> List[int]:
@@ -135,20 +142,34 @@ def any_rank(flag: bool, device, group=None) -> bool:
 
 
 def sharded_neighbours(tok: torch.Tensor, k: int, ops: ShardOps, af_rows: Optional[torch.Tensor] = None,
-                       group=None):
+                       group=None, aq_rows: Optional[torch.Tensor] = None, want_codes: bool = False):
     """One sharded retrieval step for this rank's queries ``tok`` [nq, L] (token ids < 256).
 
-    Returns (idx [nq, k] global panel indices, dist [nq, k], counts u8 [nq, ld]) for the
-    rank's own queries — the inputs of ``rag_mean(..., counts=)``."""
+    Returns (idx [nq, k] global panel indices, dist [nq, k], counts) for the rank's own
+    queries.  ``counts`` is u8 [nq, ld] — the input of ``rag_mean(..., counts=)`` — or, with
+    ``want_codes`` (train mode with dropout: every neighbour is re-encoded with its own
+    dropout mask, embedding_rag_dataset.py:406-417), the pair (uniq, uniq_codes): the sorted
+    global indices of every neighbour retrieved for ANY rank's query and their allele codes
+    u8 [U, ld], assembled by one SUM all-reduce from the shards that own them (a code is 0/1
+    and each row has exactly one owner).  ``aq_rows`` [nq, L, D] f32: per-query embedding
+    offsets of the exact LUT form (train-mode queries embedded WITH dropout, :385-386) — they
+    travel with the tokens so every shard ranks the same dropped-out query embeddings."""
     tok_all, sizes = all_gather_rows(tok.to(torch.uint8), group)
     af_all = all_gather_rows(af_rows.float(), group)[0] if af_rows is not None else None
-    keys, exps, consts = ops.keys(tok_all.long(), af_all)
+    aq_all = all_gather_rows(aq_rows.float().contiguous(), group)[0] if aq_rows is not None else None
+    keys, exps, consts = ops.keys(tok_all.long(), af_all, aq_all) if aq_all is not None else \
+        ops.keys(tok_all.long(), af_all)
     merged = sharded_search(keys, k, group, ops.merge)
     idx, dst = ops.decode(merged, exps, consts)
-    counts = _all_reduce(ops.counts(idx), dist.ReduceOp.SUM, group)
     r = dist.get_rank(group)
     o = sum(sizes[:r])
-    return idx[o:o + sizes[r]], (dst[o:o + sizes[r]] if dst is not None else None), counts[o:o + sizes[r]]
+    if want_codes:
+        uniq = torch.unique(idx[idx >= 0])                   # identical on every rank
+        codes = _all_reduce(ops.codes(uniq), dist.ReduceOp.SUM, group)
+        extra = (uniq, codes)
+    else:
+        extra = _all_reduce(ops.counts(idx), dist.ReduceOp.SUM, group)[o:o + sizes[r]]
+    return idx[o:o + sizes[r]], (dst[o:o + sizes[r]] if dst is not None else None), extra
 
 
 def kernel_ops(index, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: int = 2,
@@ -158,8 +179,13 @@ def kernel_ops(index, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: i
     take the exact A_q != A_r form (``aq_fn`` maps AF rows to their AF embeddings)."""
     from .. import kernels as K
 
-    def keys(tok_all, af_all):
+    def keys(tok_all, af_all, aq_all=None):
         nq = tok_all.shape[0]
+        if aq_all is not None:
+            # per-query offsets (dropped-out train queries): Ar is the panel's AF embedding or 0
+            ar = Ar if Ar is not None else torch.zeros(aq_all.shape[1:], device=aq_all.device)
+            lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, aq_all.contiguous(), nq, ar)
+            return index.scan_keys(lut, nq, limbs, k), exps, consts
         if af_all is None:
             lut, exps, consts = index.lut(tok_all, W, site_mask, limbs)
             return index.scan_keys(lut, nq, limbs, k), exps, consts
@@ -167,5 +193,12 @@ def kernel_ops(index, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: i
         lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, Aq, nq, Ar)
         return index.scan_keys(lut, nq, limbs, k), exps, consts
 
+    def codes(uniq):
+        i = uniq - index.ref_offset
+        own = (i >= 0) & (i < index.codes.shape[0])
+        out = torch.zeros(uniq.numel(), index.codes.shape[1], device=uniq.device, dtype=torch.uint8)
+        out[own] = index.codes[i[own]]
+        return out
+
     return ShardOps(keys=keys, merge=K.topk_merge, decode=K.knn_decode,
-                    counts=lambda idx: K.neighbor_counts(idx, index.codes, index.ref_offset))
+                    counts=lambda idx: K.neighbor_counts(idx, index.codes, index.ref_offset), codes=codes)

@@ -118,33 +118,48 @@ def main(argv=None):
     trainer.rag_k = args.rag_k
     start = 0
     if args.resume_path:
+        # train_embedding_rag.py:155-191 (weights; here also optimizer / schedule / early-stopping /
+        # sampler state); start at --resume_epoch, or after the checkpoint's epoch
         start = trainer.load(args.resume_path) + 1 if not args.resume_epoch else args.resume_epoch
+    ds, val_ds = train_loader.dataset, val_loader.dataset
+    if start > 0 and hasattr(ds, "add_level"):
+        # :326-336 — the curriculum level of the resumed epoch, min(start // 2, 7)
+        for _ in range(min(start // 2, 7)):
+            ds.add_level()
     if args.max_steps:
         import itertools
 
         class _Cap:
             def __init__(self, dl, n):
-                self.dl, self.n, self.dataset = dl, n, dl.dataset
+                self.dl, self.n, self.dataset, self.sampler = dl, n, dl.dataset, dl.sampler
 
             def __iter__(self):
                 return itertools.islice(iter(self.dl), self.n)
 
         trainer.train_data = _Cap(train_loader, args.max_steps)
         trainer.val_data = _Cap(val_loader, args.max_steps)
-    for epoch in range(start, args.epochs):
-        ds = train_loader.dataset
-        if hasattr(train_loader.sampler, "set_epoch"):      # train_embedding_rag.py:349-351
+    for epoch in range(start, args.epochs):                    # train_embedding_rag.py:343-434
+        if hasattr(train_loader.sampler, "set_epoch"):      # :349-351
             train_loader.sampler.set_epoch(epoch)
-        if epoch > 0 and hasattr(ds, "regenerate_masks"):
-            ds.current_epoch = epoch
-            ds.regenerate_masks(seed=epoch)
+        for d in (ds, val_ds):                                 # :354-357
+            d.current_epoch = epoch
+        if epoch > 0:
+            # :360-389 — fresh training masks (the validation masks stay fixed), JIT caches reset
+            if hasattr(ds, "regenerate_masks"):
+                ds.regenerate_masks(seed=epoch)
+            ds.jit_cache_win_idx = -1
+            val_ds.jit_cache_win_idx = -1
         trainer.train(epoch)
         res = trainer.validate(epoch)
-        trainer.save(epoch, args.output_path)
-        if epoch % 2 == 1 and hasattr(ds, "add_level"):
-            ds.add_level()
-        if trainer.should_stop_early(res):
+        if hasattr(val_ds, "clear_jit_cache"):                # :398-402
+            val_ds.clear_jit_cache()
+        # :405-406 — "best" is decided BEFORE this epoch's early-stopping update, i.e. from the
+        # previous validation (the reference's order, kept for identical .best.pth semantics)
+        trainer.save(epoch, args.output_path, is_best=trainer.epochs_no_improve == 0)
+        if trainer.should_stop_early(res, epoch):
             break
+        if (epoch + 1) % 2 == 0 and hasattr(ds, "add_level"):  # :418-430, capped at the last level
+            ds.add_level()
     return trainer
 
 

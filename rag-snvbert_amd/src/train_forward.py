@@ -5,8 +5,9 @@ statistics with running-stat updates), call stack model/foundation_model.py:25-3
 model/bert.py:148-219:
 
   BERTEmbedding (embedding/bert.py:53-75)      W[tok] + pe + AFEmbedding(af) -> dropout
-  neighbour K-mean (bert.py:171-183)           rag_mean_train (autograd_ops) or a given
-                                               rag_emb_h1/h2 [B, K, L, D] averaged over K
+  neighbour K-mean (bert.py:171-183)           the rag_emb_h1/h2 [B, K, L, D] train-mode
+                                               retrieval adds (autograd-connected, averaged
+                                               over K here), built by neighbour_embeddings
   EmbeddingFusionModule x4 (fusion.py:336-369) one [4B, L, D] GEMM + rank-2 pos/af terms
   EnhancedRareVariantFusion x2 (fusion.py:131-162)
   12 TransformerBlocks (transformer.py:32-35) h1 and h2 batched into one 2B dimension
@@ -20,10 +21,10 @@ elementwise kernels.  Differences from the reference, all in the stochastic part
   * EnhancedRareVariantFusion's AF gate (af_adapter) is computed once per sample and
     shared by the h1 and h2 calls (the reference computes it twice with independent
     dropout masks; without dropout the two are identical);
-  * on a sharded panel (retrieval/shards.py) the neighbour mean comes from the all-reduced
-    alt-allele counts, so each neighbour's embedding is not dropped independently (the
-    replicated panel does apply the reference's per-neighbour dropout, ``neighbour_mean_dropout``),
-    and the retrieval query embeddings are not dropped.
+  * the neighbours' dropout masks (embedding_rag_dataset.py:412-417) come from torch's
+    generator on this rank, one per unique retrieved haplotype of a window, as in the
+    reference; on a sharded panel the ranks exchange those haplotypes' allele codes and the
+    dropped-out query embeddings (retrieval/shards.py) so the same semantics hold.
 With dropout p = 0 the graph computes the reference's train-mode function exactly
 (up to bf16 rounding) — the gradient parity tests run it that way.
 """
@@ -31,6 +32,7 @@ With dropout p = 0 the graph computes the reference's train-mode function exactl
 from __future__ import annotations
 
 import math
+from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import torch
@@ -147,8 +149,32 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     return _drop(x, p, training)
 
 
+@dataclass
+class NeighbourGroup:
+    """The neighbours of one window's queries, as train-mode retrieval hands them over.
+
+    rows          batch rows of this window (long [nb]); the group's queries are h1 of those
+                  rows then h2 (2 nb queries)
+    idx_h1/idx_h2 global panel indices [nb, k] (-1: no neighbour)
+    index         the window's PanelIndex (this rank's shard of it on a sharded panel)
+    counts        sharded panel, no dropout: the all-reduced per-site alt-allele counts of the
+                  2 nb queries' neighbours (u8 [2 nb, ld]) — the K-mean needs nothing else
+    uniq/uniq_codes  sharded panel with dropout: the sorted global indices of every neighbour
+                  any rank retrieved and their allele codes (u8 [U, ld], all-reduced from the
+                  owning shards), so each rank can re-encode its own neighbours"""
+    rows: torch.Tensor
+    idx_h1: torch.Tensor
+    idx_h2: torch.Tensor
+    index: object
+    counts: Optional[torch.Tensor] = None
+    uniq: Optional[torch.Tensor] = None
+    uniq_codes: Optional[torch.Tensor] = None
+
+
 def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
-    """[2B, L, D] bf16: given dense rag embeddings (mean over K) or retrieved indices + panels."""
+    """[2B, L, D] bf16 K-means of the retrieved neighbours (bert.py:171-183): from the
+    ``rag_emb_h1/h2`` the retrieval added (train or eval; [B, K, L, D] averaged over K), or —
+    a batch from an older hand-off carrying only ``rag_groups`` — re-encoded here."""
     if "rag_emb_h1" in x:
         out = []
         for key in ("rag_emb_h1", "rag_emb_h2"):
@@ -159,49 +185,91 @@ def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
     groups = x.get("rag_groups")
     if not groups:
         return None
-    emb = bert.embedding
+    return neighbour_embeddings(bert.embedding, groups, B, L).to(T)
+
+
+def neighbour_embeddings(emb, groups: List[NeighbourGroup], B: int, L: int, dense: bool = False) -> torch.Tensor:
+    """Train-mode re-encode of the retrieved neighbours (embedding_rag_dataset.py:404-442): the
+    complete-token sequences through ``emb`` (BERTEmbedding with its AF embedding, in its own
+    train/eval mode — dropout included), autograd-connected to the token table and the AF MLP.
+
+    Returns f32 [2B, L, D] — the mean over each query's k neighbours (bert.py:176-179), rows h1
+    then h2 — or, ``dense``, the reference's [2B, k, L, D] per-neighbour embeddings.
+
+    As in the reference, each window's UNIQUE neighbours (over h1 and h2 of its queries,
+    ``cat(I1, I2).unique()``, :406) are embedded once, so every query that retrieved the same
+    haplotype sees the same dropout mask; the K-mean is then one [nq, U] x [U, L*D] product.
+    Without dropout the mean comes from the ``rag_mean`` kernel (or the sharded counts) and an
+    analytic backward — the same function, no [U, L, D] transient."""
     D = emb.embed_size
     pe = emb.position.pe[0, :L].float().contiguous()
+    p = emb.dropout.p if emb.training else 0.0
     rows_out: List[torch.Tensor] = []
     vals: List[torch.Tensor] = []
-    p = emb.dropout.p if emb.training else 0.0
-    for rows, idx_h1, idx_h2, index, *cnt in groups:
-        Ar = af_embedding(emb.af_embedding, index.ref_af.view(1, -1))[0].float() if emb.use_af else \
+    for g in groups:
+        Ar = af_embedding(emb.af_embedding, g.index.ref_af.view(1, -1))[0].float() if emb.use_af else \
             torch.zeros(L, D, device=pe.device)
-        idx = torch.cat([idx_h1, idx_h2], 0)
-        # (sharded panel: the all-reduced alt-allele counts of the neighbours, retrieval/shards.py)
-        counts = cnt[0] if cnt else None
-        if p > 0 and counts is None:
-            m = neighbour_mean_dropout(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, p)
+        idx = torch.cat([g.idx_h1, g.idx_h2], 0)
+        if g.counts is not None and (p > 0 or dense):
+            raise NotImplementedError("a sharded panel hands over neighbour counts only; retrieval must "
+                                      "exchange codes (uniq/uniq_codes) for dropout or dense outputs")
+        if p > 0 or dense or g.uniq is not None:
+            m = _unique_neighbour_embed(emb.tokenizer.weight, Ar, idx, g, pe, L, p, dense)
         else:
-            m = rag_mean_train(emb.tokenizer.weight, Ar, idx, index.codes, index.n_sites, pe, L, counts=counts)
-        nb = rows.numel()
-        rows_out += [rows, rows + B]
+            m = rag_mean_train(emb.tokenizer.weight, Ar, idx, g.index.codes, g.index.n_sites, pe, L,
+                               counts=g.counts).float()
+        nb = g.rows.numel()
+        rows_out += [g.rows, g.rows + B]
         vals += [m[:nb], m[nb:]]
     order = torch.cat(rows_out)
     stacked = torch.cat(vals, 0)
-    out = torch.empty_like(stacked)
-    out[order] = stacked
+    out = stacked.new_zeros(stacked.shape)
+    out = out.index_put((order,), stacked)
     return out
 
 
-def neighbour_mean_dropout(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, codes: torch.Tensor, n_sites: int,
-                           pe: torch.Tensor, L: int, p: float, tok0: int = 5, sos: int = 2, eos: int = 3,
-                           pad: int = 0) -> torch.Tensor:
-    """Train-mode neighbour mean with the reference's per-neighbour dropout
-    (embedding_rag_dataset.py:404-417: each retrieved complete-token sequence re-encoded by
-    BERTEmbedding in train mode — its own dropout mask — then bert.py:171-183's mean over k):
-    [nq, L, D] bf16, differentiable in W and Ar."""
+def _unique_neighbour_embed(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, g: NeighbourGroup,
+                            pe: torch.Tensor, L: int, p: float, dense: bool, tok0: int = 5, sos: int = 2,
+                            eos: int = 3, pad: int = 0) -> torch.Tensor:
+    """Embed the group's unique neighbours once (dropout p, one mask per haplotype), then
+    gather (dense [nq, k, L, D]) or average ([nq, L, D]) them per query; f32."""
     nq, k = idx.shape
-    tok = torch.full((nq, k, L), pad, device=idx.device, dtype=torch.long)
-    tok[..., 0] = sos
-    if n_sites + 1 < L:
-        tok[..., n_sites + 1] = eos
+    n_sites = g.index.n_sites
     valid = idx >= 0
-    tok[..., 1:1 + n_sites] = tok0 + codes[idx.clamp(min=0)][..., :n_sites].long()
-    e = tiny_embedding(tok, W, 0) + pe[:L] + Ar
-    e = F.dropout(e, p, True) * valid[..., None, None]
-    return (e.sum(1) / valid.sum(1).clamp(min=1)[:, None, None]).to(T)
+    if g.uniq is not None:
+        uniq, rows_codes = g.uniq, g.uniq_codes
+        inv = torch.searchsorted(uniq, idx.clamp(min=0))
+    else:
+        uniq, inv = torch.unique(idx.clamp(min=0), return_inverse=True)
+        rows_codes = g.index.codes[uniq - g.index.ref_offset]
+    U = uniq.numel()
+    tok = torch.full((U, L), pad, device=idx.device, dtype=torch.long)
+    tok[:, 0] = sos
+    if n_sites + 1 < L:
+        tok[:, n_sites + 1] = eos
+    tok[:, 1:1 + n_sites] = tok0 + rows_codes[:, :n_sites].long()
+    e = tiny_embedding(tok, W, 0) + pe[:L] + Ar                       # [U, L, D]
+    if p > 0:
+        e = F.dropout(e, p, True)
+    if dense:
+        return e[inv] * valid[..., None, None]
+    # mean over each query's valid neighbours as a [nq, U] weight matrix (repeats counted)
+    nv = valid.sum(1).clamp(min=1).to(e.dtype)
+    S = torch.zeros(nq, U, device=e.device, dtype=e.dtype)
+    S.index_put_((torch.arange(nq, device=e.device)[:, None].expand(nq, k)[valid], inv[valid]),
+                 (1.0 / nv)[:, None].expand(nq, k)[valid], accumulate=True)
+    return (S @ e.reshape(U, -1)).view(nq, L, -1)
+
+
+def neighbour_mean_dropout(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, codes: torch.Tensor, n_sites: int,
+                           pe: torch.Tensor, L: int, p: float) -> torch.Tensor:
+    """[nq, L, D] bf16 train-mode neighbour mean of one window's queries with the reference's
+    dropout semantics (each unique neighbour re-encoded once, embedding_rag_dataset.py:404-417,
+    then bert.py:171-183's mean over k), differentiable in W and Ar."""
+    from types import SimpleNamespace
+    index = SimpleNamespace(codes=codes, n_sites=n_sites, ref_offset=0)
+    g = NeighbourGroup(rows=idx.new_zeros(0), idx_h1=idx, idx_h2=idx[:0], index=index)
+    return _unique_neighbour_embed(W, Ar, idx, g, pe, L, p, False).to(T)
 
 
 def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
@@ -223,9 +291,9 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     if emb.use_af:
         e = e + af_embedding(emb.af_embedding, af).float().repeat(2, 1, 1)
     h_raw = _drop(e.to(T), p, training)                                          # [2B, L, D]
+    # (no dropout on the mean itself: the re-encoded neighbours carry their own, bert.py:171-183)
     rag = neighbour_means(bert, x, B, L)
     if rag is not None:
-        rag = _drop(rag, p, training)
         fused = emb_fusion(bert.emb_fusion, torch.cat([h_raw, rag], 0), pos, af, 4)
         hx = rag_fusion(bert.rag_fusion, fused[:2 * B], fused[2 * B:], af, af_p, p, training)
     else:

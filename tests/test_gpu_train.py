@@ -479,3 +479,140 @@ def test_train_mode_retrieval_query_dropout():
     assert ((tr >= 0) & (tr < 80)).all()
     same = np.mean([len(set(a.tolist()) & set(b.tolist())) / 4 for a, b in zip(tr.cpu(), ev.cpu())])
     assert same >= 0.5
+
+
+def _ref_trainer_handoff(data, device):
+    """pretrain_with_val_optimized.py:180-195 — the reference trainer copies these keys to the
+    device and forwards ONLY rag_emb_h1/h2 of what retrieval added."""
+    gpu = {k: data[k].to(device, dtype=torch.long if k.startswith("hap") else torch.float)
+           for k in ("hap_1", "hap_2", "pos", "af", "af_p", "ref", "het", "hom")}
+    if "rag_emb_h1" in data:
+        gpu["rag_emb_h1"] = data["rag_emb_h1"]
+    if "rag_emb_h2" in data:
+        gpu["rag_emb_h2"] = data["rag_emb_h2"]
+    return gpu
+
+
+def test_train_retrieval_contract_through_reference_handoff():
+    """Train-mode process_batch_retrieval adds autograd-connected f32 rag_emb_h1/h2 [B, 1, L, D]
+    (embedding_rag_dataset.py:404-442), so a batch handed over the reference trainer's way
+    (:172-195) trains WITH the neighbours: the loss differs from the no-RAG forward and the
+    token table's gradient carries the neighbour path's contribution (= the total minus the
+    gradient with rag_emb detached, which must be non-zero on the allele rows)."""
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.dataset.synthetic import make_rag_dataset
+    from src.autograd_ops import focal_loss
+    from src.model import build_model
+    torch.manual_seed(0)
+    ds, vocab = make_rag_dataset(n_samples=4, n_sites=200, n_windows=1, n_ref_samples=24, seed=3, name="train")
+    m = build_model(len(vocab), 64, 2, 2, dropout=0.0).to(DEV).train()
+    emb = m.bert.embedding
+    W = emb.tokenizer.weight
+    batch = embedding_rag_collate_fn([ds[i] for i in range(4)])
+    with torch.enable_grad():                                          # :170-177
+        data = ds.process_batch_retrieval(batch, emb, DEV, k_retrieve=4)
+    r1 = data["rag_emb_h1"]
+    assert r1.shape == (4, 1, 1030, 64) and r1.dtype == torch.float32 and r1.requires_grad
+    gpu = _ref_trainer_handoff(data, DEV)
+    mk = data["mask"].to(DEV).bool()
+
+    def loss_of(x):
+        out = m(x)
+        return (3 * focal_loss(out[0], data["hap_1_label"].to(DEV), mk) + 3 * focal_loss(out[1], data["hap_2_label"].to(DEV), mk)
+                + 4 * focal_loss(out[2], data["gt_label"].to(DEV), mk))
+    loss = loss_of(gpu)
+    g_total, G1, G2 = torch.autograd.grad(loss, [W, gpu["rag_emb_h1"], gpu["rag_emb_h2"]])
+    det = dict(gpu, rag_emb_h1=gpu["rag_emb_h1"].detach(), rag_emb_h2=gpu["rag_emb_h2"].detach())
+    (g_query,) = torch.autograd.grad(loss_of(det), W)
+    norag = {k: v for k, v in gpu.items() if not k.startswith("rag")}
+    loss0 = loss_of(norag)
+    assert abs(loss.item() - loss0.item()) > 1e-4 * abs(loss0.item()), (loss.item(), loss0.item())
+    g_nb = g_total - g_query
+    assert g_nb[5].abs().sum() > 0 and g_nb[6].abs().sum() > 0        # allele rows via the neighbours
+    assert g_nb[0].abs().sum() == 0                                    # <pad>: padding_idx
+    # the neighbour gradient equals autograd through the reference's own K-mean formula
+    idx = torch.cat([data["rag_idx_h1"], data["rag_idx_h2"]])
+    codes = ds.panel_index(0, DEV).codes
+    tok = torch.zeros(*idx.shape, 1030, dtype=torch.long, device=DEV)
+    tok[..., 0], tok[..., 201] = 2, 3
+    tok[..., 1:201] = 5 + codes[idx][..., :200].long()
+    Wr = W.detach().clone().requires_grad_(True)
+    with torch.no_grad():
+        from src.train_forward import af_embedding
+        Ar = af_embedding(emb.af_embedding, torch.from_numpy(ds.ref_af_windows[0]).to(DEV).view(1, -1))[0].float()
+    ref = (torch.nn.functional.embedding(tok, Wr, padding_idx=0) + emb.position.pe[0, :1030] + Ar).mean(1)
+    torch.testing.assert_close(torch.cat([r1[:, 0], data["rag_emb_h2"][:, 0]]).detach(), ref.detach(),
+                               rtol=2e-2, atol=2e-2)
+    (g_ref,) = torch.autograd.grad((ref * torch.cat([G1, G2])[:, 0]).sum(), Wr)
+    torch.testing.assert_close(g_nb[[2, 3, 5, 6]], g_ref[[2, 3, 5, 6]], rtol=5e-2,
+                               atol=2e-2 * g_ref.abs().max().item())
+
+
+def test_train_retrieval_dense_and_shared_neighbour_dropout():
+    """dense=True in train mode returns the reference's [B, k, L, D] per-neighbour embeddings
+    whose mean over k is the K-mean; with dropout every retrieved haplotype of a window is
+    re-encoded ONCE (embedding_rag_dataset.py:406-417), so two queries that retrieved the same
+    haplotype see the identical dropped-out embedding, and the dropout is unbiased."""
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.dataset.synthetic import make_rag_dataset
+    from src.model import build_model
+    torch.manual_seed(1)
+    ds, vocab = make_rag_dataset(n_samples=6, n_sites=150, n_windows=1, n_ref_samples=6, seed=4, name="train")
+    m = build_model(len(vocab), 32, 1, 2, dropout=0.0).to(DEV).train()
+    emb = m.bert.embedding
+    batch = lambda: embedding_rag_collate_fn([ds[i] for i in range(6)])
+    d0 = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4, dense=True)
+    k0 = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4)
+    assert d0["rag_emb_h1"].shape == (6, 4, 1030, 32)
+    torch.testing.assert_close(d0["rag_emb_h1"].mean(1), k0["rag_emb_h1"][:, 0], rtol=2e-2, atol=2e-2)
+    emb.dropout.p = 0.3
+    d = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4, dense=True)
+    e = torch.cat([d["rag_emb_h1"], d["rag_emb_h2"]]).detach()
+    idx = torch.cat([d["rag_idx_h1"], d["rag_idx_h2"]])
+    flat_i, flat_e = idx.reshape(-1), e.reshape(-1, 1030, 32)
+    pairs = 0
+    for a in range(flat_i.numel()):
+        for b in range(a + 1, flat_i.numel()):
+            if flat_i[a] == flat_i[b] and a // 4 != b // 4:
+                assert torch.equal(flat_e[a], flat_e[b])
+                pairs += 1
+    assert pairs > 0                                      # 12 panel haplotypes, 48 picks: repeats
+    zero = (e == 0).float().mean().item()
+    assert 0.2 < zero < 0.4                               # ~p of the entries dropped
+
+
+def test_train_entry_point_save_best_and_resume(tmp_path, capsys):
+    """src/train_embedding_rag.main end to end (train_embedding_rag.py:343-434): two epochs of
+    retrieval + training + validation on synthetic data, per-epoch checkpoints, .best.pth, the
+    reference's CSV columns (train and val rows per epoch), then a resume from epoch 0's
+    checkpoint that restores the curriculum level, optimizer / schedule / sampler state and
+    continues at epoch 1."""
+    import csv
+    from src import train_embedding_rag as T
+    out = tmp_path / "rag_bert.model"
+    mcsv = tmp_path / "metrics.csv"
+    common = ["--synthetic", "4", "--synthetic_sites", "120", "--synthetic_windows", "2", "--synthetic_ref", "12",
+              "--dims", "64", "--layers", "1", "--attn_heads", "2", "--train_batch_size", "2",
+              "--val_batch_size", "2", "--max_steps", "2", "--log_freq", "1", "--warmup_steps", "3",
+              "--rag_k", "3", "--output_path", str(out), "--metrics_csv", str(mcsv)]
+    tr = T.main(common + ["--epochs", "2"])
+    for suffix in (".ep0", ".ep1", ".best.pth"):
+        assert (tmp_path / f"rag_bert.model{suffix}").exists(), suffix
+    with open(mcsv) as f:
+        rows = list(csv.DictReader(f))
+    assert list(rows[0]) == ["epoch", "mode", "loss", "accuracy", "overall_f1", "overall_precision",
+                             "overall_recall", "rare_f1", "rare_precision", "rare_recall", "common_f1",
+                             "common_precision", "common_recall"]
+    assert [(r["epoch"], r["mode"]) for r in rows] == [("1", "train"), ("1", "val"), ("2", "train"), ("2", "val")]
+    assert all(0.0 <= float(r["overall_f1"]) <= 1.0 for r in rows)
+    steps = tr.optim_schedule.n_current_steps
+    assert steps >= 2
+    assert tr.train_data.dataset._level == 1                  # add_level after epoch 1 ((1 + 1) % 2 == 0)
+    ck = torch.load(str(out) + ".ep0", map_location="cpu", weights_only=True)
+    assert {"model", "optim", "schedule_steps", "epoch", "sampler"} <= set(ck)
+    tr2 = T.main(common + ["--epochs", "2", "--resume_path", str(out) + ".ep0"])
+    assert tr2.optim_schedule.n_current_steps > ck["schedule_steps"]
+    assert tr2.train_data.dataset._level == 1                 # min(1 // 2, 7) restored, +1 after epoch 1
+    with open(mcsv) as f:
+        rows2 = list(csv.DictReader(f))
+    assert [(r["epoch"], r["mode"]) for r in rows2[4:]] == [("2", "train"), ("2", "val")]

@@ -37,8 +37,19 @@ def test_samplers_match_reference():
     np.testing.assert_array_equal(list(iter(s)), g["grouped_sampler_ep1"])
     np.testing.assert_array_equal(list(iter(WindowMajorSampler(DS()))), g["major_sampler"])
     shards = [list(iter(DistributedWindowSampler(DS(), r, 2, shuffle=False))) for r in range(2)]
-    assert sorted(set(shards[0] + shards[1])) == list(range(35))
+    # validation order: 5 samples per window over 2 ranks -> one wrapped duplicate per window,
+    # yielded as item + len(dataset) (served with an all-zero metric mask)
+    real = [i for s in shards for i in s if i < 35]
+    pads = [i - 35 for s in shards for i in s if i >= 35]
+    assert sorted(real) == list(range(35)) and len(pads) == 7
+    assert all(p in real for p in pads)
+    assert len(shards[0]) == len(shards[1]) == 21
     assert [i % 7 for i in shards[0][:3]] == [0, 0, 0]
+    s = DistributedWindowSampler(DS(), 0, 2, shuffle=True, seed=42)
+    s.set_epoch(3)
+    t = DistributedWindowSampler(DS(), 0, 2, shuffle=True, seed=0)
+    t.load_state_dict(s.state_dict())
+    assert list(iter(t)) == list(iter(s))                 # checkpointed sampler state resumes the order
 
 
 @pytest.mark.parametrize("n_samples,world", [(10, 4), (5, 4), (7, 3), (6, 2), (1, 3)])

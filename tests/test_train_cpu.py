@@ -109,3 +109,34 @@ def test_grad_bucketer_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_trainer_metric_rows_and_early_stopping_match_reference(tmp_path):
+    """The trainer's per-epoch CSV rows (ALT-class F1 / precision / recall overall, rare and
+    common; loss; accuracy — pretrain_with_val_optimized.py:424-488) and its early-stopping
+    decisions on hap_f1[1] (:490-522), with the `is_best` flag taken before the update
+    (train_embedding_rag.py:405-409), equal the reference's on the same counts
+    (tests/golden/metrics.npz, generated by running the reference's methods)."""
+    import csv
+    from types import SimpleNamespace
+    from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized as T
+    z = load_golden("metrics")
+    n = len(z["stops"])
+    st = SimpleNamespace(calculate_metrics=T.calculate_metrics, best_val_metric=-np.inf, min_delta=0.001,
+                         epochs_no_improve=0, patience=2, val_metric="f1", rank=1,
+                         output_csv=str(tmp_path / "m.csv"))
+    stops, bests = [], []
+    for e in range(n):
+        g = lambda k: torch.from_numpy(z[f"{e}:{k}"])
+        counts = {name: torch.stack([g(f"{name}_tp"), g(f"{name}_fp"), g(f"{name}_fn")])
+                  for name in ("hap", "rare", "common")}
+        row = T.metric_row(st, e, e % 2 == 0, counts, float(z[f"{e}:hap_loss"]), int(z["num_batches"][e]),
+                           int(z[f"{e}:hap_correct"]), int(z[f"{e}:hap_numbers"]))
+        T._save_epoch_metrics(st, row)
+        bests.append(st.epochs_no_improve == 0)
+        stops.append(T.should_stop_early(st, {f"hap_{k}": g(f"hap_{k}") for k in ("tp", "fp", "fn")}, e))
+    with open(st.output_csv) as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == list(z["header"])
+    np.testing.assert_array_equal(np.array(rows[1:]), z["rows"])
+    assert stops == list(z["stops"]) and bests == list(z["is_best_before"])

@@ -61,25 +61,6 @@ def main():
                                               M, D, 4 * D, 1),
         "ffn2 N384 K1536 plain": (lambda: K.linear(h, w[(D, 4 * D)], bias[D]), M, D, 4 * D, 0),
     }
-    w2g, b2g, _ = K.fold_layernorm(w[(D, 4 * D)].float(), bias[D], torch.ones(4 * D, device=dev),
-                                   torch.zeros(4 * D, device=dev), dt)
-    ffn_ws = K.ffn_pack(w[(4 * D, D)], w2g)
-    ffn_v = K.ffn_vec(bias[4 * D], b2g, w2g, lg, lb)
-    ffn_out = torch.empty_like(x)
-    cases["ffn fused (W1+W2, 2 GEMMs)"] = (lambda: K.ffn_forward(x, ffn_ws, ffn_v, out=ffn_out), M, 8 * D, D, -2)
-    wo_s = K.ffn_pre_pack(w[(D, D)])
-    xt = x.clone()
-    cases["block tail (Wo+LN1+FFN)"] = (lambda: K.block_tail_forward(x, xt, wo_s,
-                                                                      bias[D], lg, lb, ffn_ws, ffn_v),
-                                        M, 9 * D, D, -2)
-    qkv_ws = K.wsg_pack(w[(3 * D, D)])
-    o_ws = K.wsg_pack(w[(D, D)])
-    f1_ws = K.wsg_pack(w[(4 * D, D)])
-    cases["qkv N1152 K384 wsg"] = (lambda: K.wsg_linear(x, qkv_ws, 3 * D, bias[3 * D]), M, 3 * D, D, 0)
-    cases["oproj N384 K384 +resid+LN wsg"] = (lambda: K.wsg_linear(x, o_ws, D, bias[D], resid=x, ln=(lg, lb)),
-                                              M, D, D, 1)
-    cases["ffn1 N1536 K384 +gelu wsg"] = (lambda: K.wsg_linear(x, f1_ws, 4 * D, bias[4 * D], act=N.ACT_GELU),
-                                          M, 4 * D, D, 0)
     variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
     only = os.environ.get("GM_CASE")
     for name, (fn, m, n, k, extra) in cases.items():

@@ -1,6 +1,6 @@
 """Kernel resource usage (VGPRs, AGPRs, scratch, spills, occupancy) of one csrc/*.hip file,
 from hipcc's -Rpass-analysis=kernel-resource-usage remarks.
-usage: python tools/kres.py csrc/ffn.hip [name-filter]"""
+usage: python tools/kres.py csrc/tail.hip [name-filter]"""
 import os
 import re
 import subprocess

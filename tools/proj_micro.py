@@ -1,5 +1,4 @@
-"""QKV projection on the 32x32 stream kernel (csrc/tail.hip PROJ mode) vs the weight-streaming
-GEMM (csrc/wsgemm.hip) and the stream GEMM (csrc/sgemm.hip, 4 and 8 waves) at the bench shape
+"""QKV projection on the 32x32 stream kernel (csrc/tail.hip PROJ mode) vs the stream GEMM (csrc/sgemm.hip, 4 and 8 waves) at the bench shape
 (M = 512 x 1030, D = 384, N = 3D), plus the D -> 4D GELU projection on the stream GEMM: max |diff|
 vs an fp64 reference on a small M, then launch times (HIP events)."""
 import os
@@ -23,7 +22,6 @@ for M in (777, 128 * 5 + 3):
 M = 512 * 1030
 x = torch.randn(M, D, device=dev).to(bf)
 out = torch.empty(M, 3 * D, device=dev, dtype=bf)
-wsg = K.wsg_pack(w)
 
 
 def timeit(fn, reps=10):
@@ -40,8 +38,6 @@ def timeit(fn, reps=10):
 
 fl = 2.0 * M * D * 3 * D
 o1 = K.proj_forward(x, ws, b, 3, out=out).clone()
-o2 = K.wsg_linear(x, wsg, 3 * D, b)
-print(f"proj vs wsg max|diff| {(o1.float() - o2.float()).abs().max().item():.4f}", flush=True)
 sgw, sgv = K.sgemm_pack(w), K.sgemm_vec(b)
 o3 = K.sgemm(x, sgw, 3 * D, sgv)
 print(f"proj vs sgemm max|diff| {(o1.float() - o3.float()).abs().max().item():.4f}", flush=True)
@@ -59,7 +55,6 @@ def env(k, v):
 
 
 for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out), None, fl),
-                       ("wsg (wsgemm.hip)", lambda: K.wsg_linear(x, wsg, 3 * D, b), None, fl),
                        ("sgemm", lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out), None, fl),
                        ("gelu 4D", lambda: K.sgemm(x, sg4, 4 * D, sv4, act=1, out=out4), None, fl * 4 / 3)):
     env("SNVRAG_SG_WAVES4", e) if e else None

@@ -1,5 +1,5 @@
-"""32x32-MFMA block tail (csrc/tail.hip) vs the 16x16 one (csrc/ffn.hip): correctness against a
-float64 torch reference on a small M, then launch times at the bench shape (M = 512 x 1030)."""
+"""32x32-MFMA block tail (csrc/tail.hip): correctness against a float64 torch reference on a small M,
+then launch times of its variants at the bench shape (M = 512 x 1030)."""
 import os
 import sys
 
@@ -63,16 +63,10 @@ print(f"tail PRE   max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", fl
 o = K.tail_ffn_forward(c["x"], ts, c["vec"])
 e = (o.double() - ref(c, False)).abs()
 print(f"tail FFN   max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", flush=True)
-old = c["x"].clone()
-K.block_tail_forward(c["att"], old, K.ffn_pre_pack(c["w_o"]), c["b_o"], c["g1"], c["be1"],
-                     K.ffn_pack(c["w1"], c["w2g"]), c["vec"])
-e = (old.double() - ref(c, True)).abs()
-print(f"ffn.hip    max|err| {e.max().item():.4f} mean {e.mean().item():.5f}", flush=True)
 
 M = int(os.environ.get("GM_M", 512 * 1030))
 c = case(M, 1)
 ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
-ws, wo = K.ffn_pack(c["w1"], c["w2g"]), K.ffn_pre_pack(c["w_o"])
 xs = c["x"].clone()
 out = torch.empty_like(c["x"])
 fl9, fl8 = 18.0 * M * D * D, 16.0 * M * D * D
@@ -84,12 +78,10 @@ def tail_var(v):
 
 
 for name, fn, fl in (
-        ("ffn.hip block tail", lambda: K.block_tail_forward(c["att"], xs, wo, c["b_o"], c["g1"], c["be1"], ws, c["vec"]), fl9),
         ("tail.hip PRE", tail_var(0), fl9),
         ("tail.hip PRE PF=8", tail_var(1), fl9),
         ("tail.hip PRE no-DMA (diag)", tail_var(2), fl9),
         ("tail.hip PRE no sched groups", tail_var(3), fl9),
-        ("ffn.hip FFN only", lambda: K.ffn_forward(c["x"], ws, c["vec"], out=out), fl8),
         ("tail.hip FFN only", lambda: (os.environ.__setitem__("SNVRAG_TAIL_VARIANT", "0"),
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
     ms = timeit(fn)
