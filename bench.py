@@ -275,7 +275,7 @@ def main():
                     rate=float(work[sel].sum() / (ms[sel].sum() * 1e-3)))
 
     gemm, attn, ln, ffn = agg(1), agg(2), agg(3), agg(8)
-    # kNN: the full-panel scan launch (the threshold pre-pass over a 1/128 prefix is
+    # kNN: the full-panel scan launch (the threshold pre-pass over a 1/64 prefix is
     # reported with the rest of the search path)
     full = (kinds == 4) & (work >= 0.5 * work[kinds == 4].max())
     kinds = np.where((kinds == 4) & ~full, 9, kinds)

@@ -421,6 +421,17 @@ int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* 
 size_t snvrag_colsum_ws_bytes(int64_t M, int N);
 int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, size_t ws_bytes, void* stream);
 
+/* Weight (and bias) gradient of a Linear layer (the backward of pretrain_with_val_optimized.py:235
+ * through every nn.Linear of multi_head_attention.py:44-51, feed_forward.py:18-21, fusion.py,
+ * foundation_model.py), csrc/dw.hip: dw[N, K] += sum_m dy[m, n] x[m, k] and, db != NULL,
+ * db[N] += sum_m dy[m, n]; dy [M, N], x [M, K] bf16 row-major, f32 results ACCUMULATED (zero them
+ * first).  32x32x16 MFMAs on LDS-transposed tiles, M split into `splits` chunks (0: enough to fill
+ * the chip, snvrag_dw_splits) whose 128 x 128 tiles are added with float atomics (the summation
+ * order across chunks is not fixed).  N, K multiples of 128. */
+int snvrag_dw_splits(int64_t M, int64_t N, int64_t K);
+int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, const void* x, float* dw, float* db,
+                     int splits, void* stream);
+
 /* Inference post-processing (replaces infer_embedding_rag.py:145-152): probs_h1/h2 [M, 2]
  * f32 head probabilities -> p1, p2 [M] = softmax(probs)[..., 1] (the reference's second
  * softmax) and gt [M, 4] = (p00, p01, p10, p11).  gt 16-byte aligned. */

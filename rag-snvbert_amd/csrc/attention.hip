@@ -520,6 +520,160 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
   }
 }
 
+// ------------------------------------------- bf16, head dim 32, LDS-DMA ring --
+// attn32_dma: the attn32 math (same tile<> bodies, same LDS images) with K/V staged by
+// LDS-DMA (buffer_load ... lds) through a 4-slot ring instead of register staging.  In the
+// register-staged kernel every tile paid ~25 VALU instructions of staging (zeroing the
+// out-of-range rows, bounds compares, address arithmetic, the LDS stores and their
+// addressing) on a loop that is VALU-issue bound (v_exp + cvt + MFMA issue), plus a
+// vmcnt(0) stall when the one-tile-ahead load was not back; here a wave issues 2 LDS-DMA
+// instructions per tile whose per-lane offsets are loop-invariant (the tile advance rides in
+// soffset), the swizzles of k_off / v_off are applied to the SOURCE addresses, loads run 3
+// tiles ahead, and the full-tile loop is unrolled by the ring depth so every LDS address is an
+// instruction immediate.  Rows past L read the next sequence (finite data; their scores are
+// masked to -inf and their P is 0) or, past the tensor, the buffer's out-of-range zeros.
+namespace a32 {
+constexpr int NS = 4;                           // ring slots
+constexpr int SLOT = 2 * TB;                    // K tile + V tile
+}  // namespace a32
+
+template <bool PRESCALED, bool TRAIN = false>
+__global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
+                                                  bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
+                                                  int* __restrict__ n_fallback, long total_rows,
+                                                  float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{}) {
+  using namespace a32;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lg = lane >> 4;
+  const int D = H * 32;
+  const long base = (long)seq * L * ld;
+  const bf16* Qp = qkv + base + h * 32;
+  const bf16* Kp = qkv + base + D + h * 32;
+  const bf16* Vp = qkv + base + 2 * D + h * 32;
+  const int q0 = qb * QPB + wave * QPW;
+  const bool active = q0 < L;                      // wave-uniform
+
+  bf16x8 qf[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = q0 + 16 * qt + li;
+    bf16x8 v = q < L ? *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + 8 * lg) : bf16x8{};
+    if constexpr (!PRESCALED && !TRAIN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * scale_log2e);
+    }
+    qf[qt] = v;
+  }
+
+  // K / V pieces: wave w moves keys 16 w .. 16 w + 15 of a tile (1 KiB of K, 1 KiB of V); lane
+  // l lands at byte 16 l of the piece, i.e. key 16 w + l / 4, image chunk l % 4, so it loads the
+  // source chunk that k_off / v_off put there
+  const long rem = (total_rows - (long)seq * L) * ld * 2;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(qkv + base), (short)0, (int)(rem < 0x7fffffffL ? rem : 0x7fffffffL), 0x00020000);
+  const int kk = 16 * wave + (lane >> 2), c4 = lane & 3;
+  const int kc = c4 ^ ((-(kk >> 2)) & 3);
+  const int vc = 2 * ((c4 >> 1) ^ ((kk >> 2) & 1)) + (c4 & 1);
+  const int vk = (int)(kk * ld * 2) + (D + h * 32) * 2 + kc * 16;
+  const int vv = (int)(kk * ld * 2) + (2 * D + h * 32) * 2 + vc * 16;
+  const int tile_bytes = (int)(KT * ld * 2);
+  auto issue = [&](int t, int slot) {
+    char* s = smem + slot * SLOT + wave * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)s, 16, vk, t * tile_bytes,
+                                             0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)(s + TB), 16, vv,
+                                             t * tile_bytes, 0, 0);
+  };
+  // retire this wave's pieces of tile t: y = younger tiles still in flight (<= NS - 2)
+  auto wait = [&](int y) {
+    if (y >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (y == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  State st;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    st.o[0][qt] = st.o[1][qt] = st.ls[qt] = zero;
+    st.negm[qt] = zero;
+  }
+  Train tr{};
+  if constexpr (TRAIN) tr = Train{scale_log2e, drop, drop.thresh ? drop_base(drop.seed, (uint32_t)sh) : 0u, q0};
+  const int ntile = (L + KT - 1) / KT, nfull = L / KT;
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntile) issue(j, j);
+  // one tile of the ring: slot S is compile-time, so the LDS reads take immediate offsets
+  auto step = [&](auto s_tag, int t) {
+    constexpr int S = decltype(s_tag)::value;
+    wait(min(NS - 2, ntile - 1 - t));
+    __builtin_amdgcn_s_barrier();                  // tile t visible; every wave is done with t - 1
+    if (t + NS - 1 < ntile) issue(t + NS - 1, (S + NS - 1) % NS);
+    if (active) {
+      const char* Kt = smem + S * SLOT;
+      if (t == 0) tile<4, false, true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+      else tile<4, false, false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+    }
+  };
+  int t = 0;
+  for (; t + NS <= nfull; t += NS) {
+    step(std::integral_constant<int, 0>{}, t);
+    step(std::integral_constant<int, 1>{}, t + 1);
+    step(std::integral_constant<int, 2>{}, t + 2);
+    step(std::integral_constant<int, 3>{}, t + 3);
+  }
+  for (; t < ntile; ++t) {                         // the last < NS full tiles and the ragged tail
+    wait(min(NS - 2, ntile - 1 - t));
+    __builtin_amdgcn_s_barrier();
+    if (t + NS - 1 < ntile) issue(t + NS - 1, (t + NS - 1) % NS);
+    if (active) {
+      const char* Kt = smem + (t % NS) * SLOT;
+      if (t == 0) tile_any<true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+      else tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+    }
+  }
+  if (!active) return;
+
+  bool bad = false;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float l = st.ls[qt][0];
+    bad |= !(l > 0.f && l < INFINITY);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(st.o[e][qt][r]);
+  }
+  if (__ballot(bad)) {
+    if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
+    attn32_online<TRAIN>(Kp, Vp, ld, L, qf, st, li, lg, tr);
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = q0 + 16 * qt + li;
+    if (q >= L) continue;
+    const float inv = 1.0f / st.ls[qt][0];
+    if constexpr (TRAIN) {
+      if (lg == 0) lse[((long)seq * H + h) * L + q] = -scale_log2e * st.negm[qt][0] + log2f(st.ls[qt][0]);
+    }
+    bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * 32;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(st.o[e][qt][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * e + 4 * lg) = w;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- f32 path --
 template <int DH>
 __global__ __launch_bounds__(64) void attn_fwd_f32(int nseq, int L, int H, const float* __restrict__ qkv,
@@ -584,7 +738,16 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const float sl2 = scale * 1.4426950408889634f;
     const bool pre = fabsf(sl2 - 1.0f) < 1e-6f;      // Q already carries log2(e)/sqrt(dh)
     int* cnt = attn_fallback_counter();
-    if (pre)
+    const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
+    const bool dma = !(reg && reg[0] == '1');
+    if (dma) {
+      if (pre)
+        hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
+      else
+        hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
+    } else if (pre)
       hipLaunchKernelGGL(attn32_bf16<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
                          (bf16*)out, ldo, 1.0f, nqb, cnt);
     else
@@ -643,9 +806,15 @@ extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, in
     const int nqb3 = cdiv(L, a32::QPB);
     const long nb3 = (long)nqb3 * heads * nseq;
     SNV_CHECK_ARG(nb3 < (1L << 31), "grid too large");
-    hipLaunchKernelGGL((attn32_bf16<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
-                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
-                       lse, drop);
+    const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
+    if (reg && reg[0] == '1')
+      hipLaunchKernelGGL((attn32_bf16<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
+                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
+                         lse, drop);
+    else
+      hipLaunchKernelGGL((attn32_dma<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
+                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
+                         (long)nseq * L, lse, drop);
   } else if (dh == 32)
     hipLaunchKernelGGL(attn_fwd_bf16<32>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
                        (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);

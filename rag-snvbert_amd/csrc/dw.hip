@@ -1,0 +1,174 @@
+// Weight gradient of a Linear layer on 32x32x16 bf16 MFMAs (gfx950), f32 result:
+//
+//   dW[N, K] = sum_m dY[m, n] X[m, k]        (optionally db[N] = sum_m dY[m, n])
+//
+// the backward of every nn.Linear of the training graph (multi_head_attention.py:44-51,
+// feed_forward.py:18-21, fusion.py, foundation_model.py; pretrain_with_val_optimized.py:235
+// backward).  The reduction runs over the M = 2 B L token rows (~5e4 at B = 24), the output is
+// small (<= 1536 x 1536), so the launch splits M into S chunks (enough workgroups to fill 256
+// CUs) and every chunk's 128 x 128 tile is added into the f32 output with no-return float atomics
+// (one add per element per chunk: <= 17 M adds per layer, well inside the chip's atomic rate).
+//
+// Both operands are K-major for the MFMA (the reduction index m is the ROW of dY and X), so a
+// 32-row stage of each is staged row-major in LDS and read back TRANSPOSED with
+// ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i
+// receives column i of the 4 rows): two such reads are one 8-k MFMA fragment, A[n][m] = dY[m][n]
+// and B[m][k] = X[m][k].  Rows are 256 B; the 32-B column blocks are XOR-swizzled by (row & 7)
+// so the four rows of a transposed read fall in different banks.  Global -> LDS is register
+// staged, double buffered (the next stage's loads in flight under this stage's MFMAs).
+#include "common.h"
+
+namespace snvrag {
+
+constexpr int DW_T = 128;                 // output tile (n and k)
+constexpr int DW_R = 32;                  // m rows per stage
+constexpr int DW_STAGE = 2 * DW_R * DW_T * 2;   // dY tile + X tile, bf16
+
+__device__ __forceinline__ int dw_swz(int row, int colbyte) {   // byte offset in a [32][256 B] tile
+  return row * 256 + ((((colbyte >> 5) ^ (row & 7))) << 5) + (colbyte & 31);
+}
+
+__device__ __forceinline__ bf16x4 dw_tr(const char* p) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// grid: (N / 128, K / 128, S); 256 threads = 4 waves, wave (wn, wk) owns the 64 x 64 sub-tile
+// n0 + 64 wn, k0 + 64 wk (2 x 2 MFMA tiles of 32 x 32).
+__global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16* __restrict__ dy,
+                                                 const bf16* __restrict__ x, float* __restrict__ dw,
+                                                 float* __restrict__ db, int chunk) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * DW_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
+  const int m_begin = blockIdx.z * chunk;
+  const int m_end = min(M, m_begin + chunk);
+  if (m_begin >= m_end) return;                      // whole workgroup, before any barrier
+  const int nst = (m_end - m_begin + DW_R - 1) / DW_R;
+
+  // loader: stage = 32 rows x 256 B of dY and of X = 2 x 512 16-B chunks; thread t moves chunks
+  // t and t + 256 of each
+  u32x4 ry[2], rx[2];
+  auto load = [&](int st) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, c16 = c & 15;
+      const int m = m_begin + st * DW_R + row;
+      const bool ok = m < m_end;
+      ry[i] = ok ? *reinterpret_cast<const u32x4*>(dy + (long)m * N + n0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
+      rx[i] = ok ? *reinterpret_cast<const u32x4*>(x + (long)m * K + k0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+    char* s = smem + buf * DW_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, c16 = c & 15;
+      *reinterpret_cast<u32x4*>(s + dw_swz(row, 16 * c16)) = ry[i];
+      *reinterpret_cast<u32x4*>(s + DW_R * 256 + dw_swz(row, 16 * c16)) = rx[i];
+    }
+  };
+
+  // transposed-read addresses: 16-lane group g = lane / 16 takes columns 16 (g & 1) .. + 15 of
+  // its 32-column MFMA tile and rows 8 (g >> 1) + 4 h .. + 3 (h = first / second read)
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int rowb = 8 * (g >> 1) + q;                 // + 16 s (k-step) + 4 h
+  const int colb = 2 * (16 * (g & 1) + 4 * p);       // bytes, + 64 T within the wave's 64 columns
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  const bool do_db = db != nullptr && blockIdx.y == 0 && wk == 0;
+  float dbs[2] = {0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const bool more = st + 1 < nst;
+    if (more) load(st + 1);
+    const char* s = smem + (st & 1) * DW_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r0 = 16 * ks + rowb;
+        const int ca = 128 * wn + 64 * t + colb;     // bytes within the dY tile row
+        const int cb = 128 * wk + 64 * t + colb;
+        const bf16x4 a0 = dw_tr(s + dw_swz(r0, ca)), a1 = dw_tr(s + dw_swz(r0 + 4, ca));
+        const bf16x4 b0 = dw_tr(s + DW_R * 256 + dw_swz(r0, cb)), b1 = dw_tr(s + DW_R * 256 + dw_swz(r0 + 4, cb));
+        fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      if (do_db) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dbs[a] += (float)fa[a][j];
+      }
+    }
+    if (more) store((st + 1) & 1);
+    __syncthreads();
+  }
+
+  // C layout of 32x32x16: lane holds column k = lane % 32 and rows 8 (e / 4) + 4 (lane / 32) + e % 4
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int kk = k0 + 64 * wk + 32 * b + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int nn = n0 + 64 * wn + 32 * a + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+        unsafeAtomicAdd(dw + (long)nn * K + kk, acc[a][b][e]);
+      }
+    }
+  if (do_db) {
+    // A-fragment lanes l and l + 32 hold the same column n (rows 0..7 / 8..15 of each k-step)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const float v = dbs[a] + __shfl_xor(dbs[a], 32, 64);
+      if (lane < 32) unsafeAtomicAdd(db + n0 + 64 * wn + 32 * a + lane, v);
+    }
+  }
+}
+
+}  // namespace snvrag
+
+using namespace snvrag;
+
+extern "C" int snvrag_dw_splits(int64_t M, int64_t N, int64_t K) {
+  const long tiles = (N / DW_T) * (K / DW_T);
+  long s = (1024 + tiles - 1) / std::max<long>(tiles, 1);            // ~4 workgroups per CU
+  const long max_s = (M + 8 * DW_R - 1) / (8 * DW_R);                // >= 8 stages per chunk
+  s = std::min(std::max(s, 1L), std::max(max_s, 1L));
+  return (int)s;
+}
+
+extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, const void* x, float* dw,
+                                float* db, int splits, void* stream) {
+  SNV_CHECK_ARG(dy && x && dw, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && N % DW_T == 0 && K % DW_T == 0 && N > 0 && K > 0, "N and K must be multiples of 128");
+  SNV_CHECK_ARG(M * std::max(N, K) < (1L << 31), "operand too large for 32-bit row offsets");
+  SNV_CHECK_ARG(((uintptr_t)dy % 16) == 0 && ((uintptr_t)x % 16) == 0, "operands must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  // dw / db are accumulated: the caller zeroes them (or passes a running sum)
+  if (M == 0) return 0;
+  if (splits <= 0) splits = snvrag_dw_splits(M, N, K);
+  const int chunk = (int)((((M + splits - 1) / splits) + DW_R - 1) / DW_R * DW_R);
+  const int S = (int)((M + chunk - 1) / chunk);
+  evlog_begin(s);
+  hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
+                     (int)M, (int)N, (int)K, (const bf16*)dy, (const bf16*)x, dw, db, chunk);
+  SNV_LAUNCH_CHECK();
+  evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
+  return 0;
+}

@@ -3,12 +3,13 @@
 The training graph (``src/train_forward.py``) is ordinary autograd; its heavy nodes
 are these Functions, whose forward and backward run the HIP kernels:
 
-  hip_linear      Linear layers on the row-panel MFMA GEMM (bf16 in, f32 accumulate):
-                  forward  y = x W^T + b             (snvrag_linear)
-                  backward dx = dy W                 (snvrag_linear on W^T)
-                           dW = dy^T x               (hipBLASLt via torch.mm — a plain
-                                                      library GEMM, long-K reduction, f32
-                                                      result stored by the GEMM)
+  hip_linear      Linear layers on the MFMA GEMMs (bf16 in, f32 accumulate):
+                  forward  y = x W^T + b             (stream GEMM at K = 384, else snvrag_linear)
+                  backward dx = dy W                 (the same GEMMs on W^T)
+                           dW = dy^T x, db = sum dy  (snvrag_linear_dw: split-M MFMA kernel on
+                                                      LDS-transposed tiles, f32 result; shapes
+                                                      that are not multiples of 128 (the AF MLP's
+                                                      64 inputs) on torch.mm with an f32 result)
   hip_attention   unmasked softmax attention: flash forward that keeps the row
                   log-sum-exp, FlashAttention-2 style dq / dkv backward kernels.
   focal_loss      FocalLoss(reduction='sum') over masked rows, forward and derivative
@@ -32,6 +33,24 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import kernels as K
+
+_TRAIN_DT = [torch.bfloat16]              # compute dtype of the training graph
+
+
+def train_dtype() -> torch.dtype:
+    return _TRAIN_DT[0]
+
+
+def set_train_precision(dtype: torch.dtype) -> None:
+    """Compute dtype of the training graph: torch.bfloat16 (the product path: bf16 MFMA kernels,
+    f32 accumulation and master weights) or torch.float32 — the gradient-parity mode, whose
+    parameter gradients are held to 1e-3 of the reference's own autograd
+    (tests/test_gpu_train.py): every Linear on the exact-f32 row-panel MFMA GEMM (forward and
+    dX; f32 dW), LayerNorm and attention as f32 torch ops."""
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("training precision must be float32 or bfloat16")
+    _TRAIN_DT[0] = dtype
+
 
 _BF16: Dict[tuple, list] = {}
 _MIRROR: Dict[int, tuple] = {}              # id(param) -> (weakref(param), flat-buffer bf16 view)
@@ -189,6 +208,8 @@ class _HipLinear(torch.autograd.Function):
     def forward(ctx, x, n, *wb):
         ws, bs = wb[:n], wb[n:]
         Kd = x.shape[-1]
+        if train_dtype() == torch.float32:
+            return _HipLinear._forward_f32(ctx, x, n, ws, bs)
         x2 = x.reshape(-1, Kd)
         if x2.dtype != torch.bfloat16:
             x2 = x2.to(torch.bfloat16)
@@ -208,7 +229,22 @@ class _HipLinear(torch.autograd.Function):
         return y.reshape(*x.shape[:-1], n_out)
 
     @staticmethod
+    def _forward_f32(ctx, x, n, ws, bs):
+        """Parity mode: y = x W^T + b on the exact-f32 row-panel GEMM (v_mfma_f32_16x16x4f32)."""
+        x2 = x.reshape(-1, x.shape[-1]).float().contiguous()
+        w = torch.cat([t.detach().float() for t in ws], 0).contiguous()
+        has_b = bs[0] is not None
+        b = torch.cat([t.detach().float().reshape(-1) for t in bs]).contiguous() if has_b else None
+        y = K.linear(x2, w, b)
+        ctx.save_for_backward(x2, *ws)
+        ctx.n, ctx.has_bias, ctx.f32 = n, has_b, True
+        ctx.in_shape, ctx.in_dtype = x.shape, x.dtype
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
     def backward(ctx, gy):
+        if getattr(ctx, "f32", False):
+            return _HipLinear._backward_f32(ctx, gy)
         x2, *ws = ctx.saved_tensors
         sizes = [t.shape[0] for t in ws]
         g2 = gy.reshape(-1, sum(sizes))
@@ -228,6 +264,15 @@ class _HipLinear(torch.autograd.Function):
                     torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
                 gx = K.linear(g2, wt)
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
+        n_all, k_in = g2.shape[1], x2.shape[1]
+        if any(ctx.needs_input_grad[2:2 + ctx.n]) and n_all % 128 == 0 and k_in % 128 == 0 and \
+                not os.environ.get("SNVRAG_TRAIN_BLAS_DW"):
+            # dW (and db) on the split-M MFMA kernel (csrc/dw.hip), f32 accumulation and result
+            gw, gb = K.linear_dw(g2, x2, bias=ctx.has_bias)
+            gws = list(torch.split(gw, sizes, 0))
+            if ctx.has_bias:
+                gbs = list(torch.split(gb, sizes, 0))
+            return (gx, None, *gws, *gbs)
         if any(ctx.needs_input_grad[2:2 + ctx.n]):
             gw = _mm_f32(g2.t(), x2)
             gws = list(torch.split(gw, sizes, 0))
@@ -237,6 +282,22 @@ class _HipLinear(torch.autograd.Function):
         return (gx, None, *gws, *gbs)
 
 
+def _hip_linear_backward_f32(ctx, gy):
+    x2, *ws = ctx.saved_tensors
+    sizes = [t.shape[0] for t in ws]
+    g2 = gy.reshape(-1, sum(sizes)).float().contiguous()
+    gx = None
+    if ctx.needs_input_grad[0]:
+        wt = torch.cat([t.detach().float() for t in ws], 0).t().contiguous()
+        gx = K.linear(g2, wt).reshape(ctx.in_shape).to(ctx.in_dtype)
+    gws = list(torch.split(g2.t() @ x2, sizes, 0)) if any(ctx.needs_input_grad[2:2 + ctx.n]) else [None] * ctx.n
+    gbs = list(torch.split(g2.sum(0), sizes, 0)) if ctx.has_bias else [None] * ctx.n
+    return (gx, None, *gws, *gbs)
+
+
+_HipLinear._backward_f32 = staticmethod(_hip_linear_backward_f32)
+
+
 def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
     """nn.Linear on the MFMA kernels; bf16 activations in and out.  ``weight``/``bias`` may be
     lists (layers sharing the input, fused along the output dim)."""
@@ -244,6 +305,9 @@ def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
     bs = list(bias) if isinstance(bias, (list, tuple)) else [bias] * len(ws)
     Kd, Nn = ws[0].shape[1], sum(t.shape[0] for t in ws)
     if Kd % 8 or Nn % 8:
+        if train_dtype() == torch.float32:
+            b = torch.cat(bs, 0) if bs[0] is not None else None
+            return torch.nn.functional.linear(x.float(), torch.cat(ws, 0), b)
         w = torch.cat(ws, 0).to(torch.bfloat16)
         b = torch.cat(bs, 0).to(torch.bfloat16) if bs[0] is not None else None
         return torch.nn.functional.linear(x.to(torch.bfloat16), w, b)
@@ -272,7 +336,11 @@ class _HipAddLayerNorm(torch.autograd.Function):
 
 
 def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln) -> torch.Tensor:
-    """bf16 LayerNorm(x + r) with the parameters of nn.LayerNorm ``ln`` (N % 8 == 0, N <= 2048)."""
+    """bf16 LayerNorm(x + r) with the parameters of nn.LayerNorm ``ln`` (N % 8 == 0, N <= 2048)
+    (f32 parity mode: torch's f32 LayerNorm)."""
+    if train_dtype() == torch.float32:
+        s = x.float() + r.float() if r is not None else x.float()
+        return torch.nn.functional.layer_norm(s, (s.shape[-1],), ln.weight, ln.bias, ln.eps)
     return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps)
 
 
@@ -298,6 +366,14 @@ def hip_attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int, dro
     """softmax(q k^T / sqrt(dh)) v per (sequence, head); qkv [nseq*L, 3D] bf16 -> [nseq*L, D].
     ``dropout_p`` > 0: attention-probability dropout (attention.py:28-29); the keep mask is a
     counter-based hash of ``seed`` (drawn from torch's RNG when None), shared by the backward."""
+    if train_dtype() == torch.float32:
+        # parity mode: the unfused f32 softmax attention (attention.py:21-31) under torch autograd
+        D = heads * dh
+        q, k, v = qkv.float().view(nseq, L, 3, heads, dh).permute(2, 0, 3, 1, 4)
+        p = torch.softmax((q @ k.transpose(-1, -2)) / dh ** 0.5, -1)
+        if dropout_p > 0:
+            p = torch.nn.functional.dropout(p, dropout_p, True)
+        return (p @ v).permute(0, 2, 1, 3).reshape(nseq * L, D)
     if dropout_p > 0 and seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     return _HipAttention.apply(qkv, nseq, L, heads, dh, float(dropout_p), int(seed or 0))
@@ -327,7 +403,7 @@ class _RagMean(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W, Ar, idx, codes, n_sites, pe, L, tok0, tok1, sos, eos, counts):
         out = K.rag_mean(idx, codes, n_sites, W.detach().float().contiguous(), pe, Ar.detach().float().contiguous(),
-                         L, torch.bfloat16, tok0=tok0, tok1=tok1, sos=sos, eos=eos, counts=counts)
+                         L, train_dtype(), tok0=tok0, tok1=tok1, sos=sos, eos=eos, counts=counts)
         valid = idx >= 0
         nv = valid.sum(1)
         if counts is not None:

@@ -162,7 +162,8 @@ def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_le
     h1, h2, gt, mask = geometry(host["h1"], host["h2"], host["gt"], host["mask"], ds.window_count,
                                 len(ds.ori_pos), window_len)
     return dict(h1=h1, h2=h2, gt=gt, mask=mask, idx1=host["idx1"], idx2=host["idx2"], seconds=elapsed,
-                masked_snvs=int(host["mask"].sum()) * 2, batch_mask=host["mask"])
+                masked_snvs=int(host["mask"].sum()) * 2, batch_mask=host["mask"], batch_h1=host["h1"],
+                batch_h2=host["h2"])
 
 
 def infer(argv=None):

@@ -570,6 +570,20 @@ def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tens
     return ds, dg, db
 
 
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, bias: bool = False, splits: int = 0):
+    """(dW f32 [N, K] = dy^T x, db f32 [N] = column sums of dy or None) for bf16 dy [M, N],
+    x [M, K] (csrc/dw.hip; N, K multiples of 128)."""
+    N.require_gpu(dy, x)
+    assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[0] == x.shape[0]
+    M, Nn = dy.shape
+    Kk = x.shape[1]
+    dw = torch.zeros(Nn, Kk, device=dy.device, dtype=torch.float32)
+    db = torch.zeros(Nn, device=dy.device, dtype=torch.float32) if bias else None
+    check(N.lib().snvrag_linear_dw(M, Nn, Kk, ptr(_c(dy)), ptr(_c(x)), ptr(dw), ptr(db), int(splits), stream_ptr()),
+          "linear_dw")
+    return dw, db
+
+
 def colsum(x: torch.Tensor) -> torch.Tensor:
     """f32 column sums of a bf16 matrix [..., N] (bias gradients)."""
     Nn = x.shape[-1]

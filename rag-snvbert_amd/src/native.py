@@ -145,6 +145,8 @@ _SIGS = {
     "snvrag_ln_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_colsum_ws_bytes": ([i64, C.c_int], sz),
     "snvrag_colsum_bf16": ([i64, C.c_int, vp, vp, vp, sz, vp], C.c_int),
+    "snvrag_dw_splits": ([i64, i64, i64], C.c_int),
+    "snvrag_linear_dw": ([i64, i64, i64, vp, vp, vp, vp, C.c_int, vp], C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

@@ -76,16 +76,18 @@ class PanelIndex:
     def scan_keys(self, lut: torch.Tensor, nq: int, limbs: int, k: int, presample: Optional[bool] = None) -> torch.Tensor:
         """Exact local top-k keys [nq, k] (uint64 in int64 storage) with global indices.
 
-        Large panels first scan a 1/128 prefix of the panel: its k-th best distance is an
+        Large panels first scan a 1/64 prefix of the panel: its k-th best distance is an
         upper bound on the panel's, so the full scan can start from it (strictly above it
         nothing can enter the top-k) and keeps far fewer candidates; the result is the
-        same exact top-k."""
+        same exact top-k.  (1/64 measured best for the whole search on the bench panel:
+        1M x 1024, 96 queries: 0.319 ms vs 0.3315 ms at 1/128 and 0.337 ms at 1/32 — the
+        full scan's candidate compaction is its compute-side cost, profiles/r3_knn_probe.txt.)"""
         n_ref = self.codes.shape[0]
         if presample is None:
             presample = n_ref >= self.SAMPLE_MIN
         th = None
         if presample:
-            div = int(os.environ.get("SNVRAG_SAMPLE_DIV", "128"))
+            div = int(os.environ.get("SNVRAG_SAMPLE_DIV", "64"))
             rpp = int(os.environ.get("SNVRAG_SAMPLE_RPP", "64"))
             m = max(16 * k, ((n_ref // div) + 15) // 16 * 16)
             sample = K.knn_scan(self.codes[:m], self.n_sites_pad, lut, nq, limbs, k, self.ref_offset,

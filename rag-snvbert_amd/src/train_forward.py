@@ -38,9 +38,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train, tiny_embedding
-
-T = torch.bfloat16
+from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train, tiny_embedding, train_dtype
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -102,7 +100,7 @@ def emb_fusion(ef, embs: torch.Tensor, pos: torch.Tensor, af: torch.Tensor, n_ca
             for _ in range(n_calls - 1):
                 pos_feat(ef.pos_feat, pos)
     rep = lambda t: t.repeat(n_calls, 1)
-    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1).to(T)
+    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1).to(train_dtype())
     return hip_add_layernorm(embs, y, ef.norm)
 
 
@@ -120,14 +118,14 @@ def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p
     w = _drop(F.gelu(hip_linear(fused_af, ad[0].weight, ad[0].bias)), p, training)
     w = torch.sigmoid(hip_linear(w, ad[3].weight, ad[3].bias).float())            # [B, L, D]
     w2 = w.repeat(2, 1, 1)
-    pooled = (rag.float() * w2).to(T)
+    pooled = (rag.float() * w2).to(train_dtype())
     fu = rf.fusion
     h = _drop(F.gelu(hip_linear(torch.cat([orig, pooled], -1), fu[0].weight, fu[0].bias)), p, training)
     h = hip_add_layernorm(hip_linear(h, fu[3].weight, fu[3].bias), None, fu[4]).float()
     af2 = af.repeat(2, 1)
     maf = torch.minimum(af2, 1 - af2).unsqueeze(-1)
     mw = torch.log1p(1.0 / (maf + 1e-6)).clamp(max=3.0)
-    return (orig.float() + rf.res_scale * (h * mw)).to(T)
+    return (orig.float() + rf.res_scale * (h * mw)).to(train_dtype())
 
 
 def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, training: bool) -> torch.Tensor:
@@ -180,12 +178,12 @@ def neighbour_means(bert, x: Dict, B: int, L: int) -> Optional[torch.Tensor]:
         for key in ("rag_emb_h1", "rag_emb_h2"):
             r = x[key]
             r = r.mean(1) if r.dim() == 4 else r
-            out.append(r.to(T))
+            out.append(r.to(train_dtype()))
         return torch.cat(out, 0)
     groups = x.get("rag_groups")
     if not groups:
         return None
-    return neighbour_embeddings(bert.embedding, groups, B, L).to(T)
+    return neighbour_embeddings(bert.embedding, groups, B, L).to(train_dtype())
 
 
 def neighbour_embeddings(emb, groups: List[NeighbourGroup], B: int, L: int, dense: bool = False) -> torch.Tensor:
@@ -269,7 +267,7 @@ def neighbour_mean_dropout(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor,
     from types import SimpleNamespace
     index = SimpleNamespace(codes=codes, n_sites=n_sites, ref_offset=0)
     g = NeighbourGroup(rows=idx.new_zeros(0), idx_h1=idx, idx_h2=idx[:0], index=index)
-    return _unique_neighbour_embed(W, Ar, idx, g, pe, L, p, False).to(T)
+    return _unique_neighbour_embed(W, Ar, idx, g, pe, L, p, False).to(train_dtype())
 
 
 def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
@@ -290,7 +288,7 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     e = tiny_embedding(tok, emb.tokenizer.weight, 0) + emb.position.pe[:, :L]
     if emb.use_af:
         e = e + af_embedding(emb.af_embedding, af).float().repeat(2, 1, 1)
-    h_raw = _drop(e.to(T), p, training)                                          # [2B, L, D]
+    h_raw = _drop(e.to(train_dtype()), p, training)                                          # [2B, L, D]
     # (no dropout on the mean itself: the re-encoded neighbours carry their own, bert.py:171-183)
     rag = neighbour_means(bert, x, B, L)
     if rag is not None:
@@ -304,7 +302,7 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     # 3. heads (foundation_model.py:25-33)
     hc = fm.hap_classifier
     af2, afp2 = af.repeat(2, 1), af_p.repeat(2, 1)
-    hh = F.gelu(_linear_cat2(hx, hc.af_fusion[0], af2, afp2).to(T))
+    hh = F.gelu(_linear_cat2(hx, hc.af_fusion[0], af2, afp2).to(train_dtype()))
     hh = hip_add_layernorm(hip_linear(hh, hc.af_fusion[2].weight, hc.af_fusion[2].bias), None, hc.af_fusion[3])
     hh = F.gelu(hip_linear(hh, hc.net[0].weight, hc.net[0].bias))
     logits = F.linear(hh.float(), hc.net[2].weight, hc.net[2].bias)

@@ -319,7 +319,7 @@ def _faiss_standin():
 
 
 def run_infer_case(name, d, layers, heads, n_sites, n_samples, n_ref_samples, k, batch_size, seed=0,
-                   ref_missing=2, compact=False):
+                   ref_missing=2, compact=False, missing_rate=0.3):
     """The reference imputation path end to end on synthetic arrays: InferDataset
     (dataset.py:629-900), EmbeddingRAGInferDataset (embedding_rag_infer_dataset.py:20-324:
     510-site index windows, infer masks, panel embeddings, process_batch_retrieval) with the
@@ -333,8 +333,8 @@ def run_infer_case(name, d, layers, heads, n_sites, n_samples, n_ref_samples, k,
     torch.set_num_threads(8)
     vocab = ref_vocab()
     model, digest = build_model(d, layers, heads, len(vocab), seed)
-    a = synthetic.make_infer_arrays(n_sites, n_samples, n_ref_samples, missing_rate=0.3, ref_missing=ref_missing,
-                                    seed=seed + 5)
+    a = synthetic.make_infer_arrays(n_sites, n_samples, n_ref_samples, missing_rate=missing_rate,
+                                    ref_missing=ref_missing, seed=seed + 5)
     vpm = SimpleNamespace(sequence_padding=seq_pad, position_normalize=pos_norm)
     glb = dict(NP_GLB, Dataset=Dataset, math=math, INFER_WINDOW_LEN=1020, REF=0, HET=1, HOM=2, AF=3, GLOBAL=5,
                VCFProcessingModule=vpm, WordVocab=WordVocabRef)
@@ -406,6 +406,7 @@ def run_infer_case(name, d, layers, heads, n_sites, n_samples, n_ref_samples, k,
     probs2 = np.concatenate([o[1].detach().numpy() for o in rec.outs])
     res = dict(cfg=np.array(json.dumps(dict(d=d, layers=layers, heads=heads, vocab=len(vocab), k=k, seed=seed,
                                               batch_size=batch_size, n_samples=n_samples, index_window_len=510,
+                                              missing_rate=missing_rate, n_ref_samples=n_ref_samples,
                                               window_len=1020, sd_digest=digest, pops=a["pops"]))),
                ori_pos=a["ori_pos"], pos=a["pos"], vcf=a["vcf"], freq=a["freq"], ref_gt=a["ref_gt"],
                ref_pos=a["ref_pos"], order=np.array(order),
@@ -470,7 +471,7 @@ def masks_fixture():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag", "infer", "infer256"]
+    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag", "infer", "infer256", "infer384", "sweep"]
     if "data" in which:
         masks_fixture()
     if "tiny" in which:
@@ -489,3 +490,12 @@ if __name__ == "__main__":
         # C5 geometry: one batch of 256 sample-windows spanning both windows
         run_infer_case("infer_c5_b256", d=64, layers=2, heads=4, n_sites=1300, n_samples=128, n_ref_samples=24,
                        k=2, batch_size=256, seed=7, compact=True)
+    if "infer384" in which:
+        # the v18 model shape (d384 / 12 layers / 12 heads) through the whole imputation path
+        run_infer_case("infer_c5_d384", d=384, layers=12, heads=12, n_sites=1300, n_samples=4, n_ref_samples=24,
+                       k=2, batch_size=8, seed=8)
+    if "sweep" in which:
+        # C5 mask sweep end points (10 % and 90 % of the panel sites missing from the target)
+        for rate, tag in ((0.1, "m10"), (0.9, "m90")):
+            run_infer_case(f"infer_c5_{tag}", d=64, layers=2, heads=4, n_sites=1300, n_samples=6, n_ref_samples=24,
+                           k=2, batch_size=12, seed=9, missing_rate=rate, compact=True)

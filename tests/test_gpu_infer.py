@@ -63,15 +63,21 @@ def _fixture_run(case, dtype):
 
 
 @pytest.mark.parametrize("case,dtype", [("infer_c5", torch.float32), ("infer_c5", torch.bfloat16),
-                                        ("infer_c5_b256", torch.float32)])
+                                        ("infer_c5_b256", torch.float32), ("infer_c5_b256", torch.bfloat16),
+                                        ("infer_c5_d384", torch.float32), ("infer_c5_d384", torch.bfloat16),
+                                        ("infer_c5_m10", torch.float32), ("infer_c5_m90", torch.float32),
+                                        ("infer_c5_m90", torch.bfloat16)])
 def test_infer_matches_reference_fixture(case, dtype):
     """The whole imputation path (EmbeddingRAGInferDataset items, 510-site index windows,
     process_batch_retrieval on the HBM index, forward, device post-processing, geometry) vs
-    the reference run on the same arrays (tests/golden/make_golden.py run_infer_case).
+    the reference run on the same arrays (tests/golden/make_golden.py run_infer_case): the
+    d64/L2 cases at batch 4 and 256, the v18 shape d384/L12/H12, and the C5 sweep end points
+    (10 % / 90 % of the panel sites missing from the target), in f32 and bf16.
     Neighbours: equal top-k sets wherever the reference's k-th/(k+1)-th distance margin is
     not a tie (> 1e-3); imputed probabilities of the sample-windows whose neighbours are
-    unambiguous: f32 1e-4 (1e-3 against the float16-stored batch-256 fixture), bf16 2e-2;
-    masks bit-exact."""
+    unambiguous: f32 1e-4 (1e-3 against the float16-stored fixtures), bf16 2e-2 (3e-2 at
+    d384/L12); masks bit-exact.  The tied sample-windows are covered by
+    test_infer_tied_rows_vs_oracle."""
     g, cfg, ds, res = _fixture_run(case, dtype)
     k, S = cfg["k"], cfg["n_samples"]
     clear = (g["kth_margin_h1"] > 1e-3) & (g["kth_margin_h2"] > 1e-3)
@@ -85,10 +91,54 @@ def test_infer_matches_reference_fixture(case, dtype):
     for r in np.nonzero(clear)[0]:
         w, s = divmod(int(r), S)
         ok[1020 * w:1020 * (w + 1), s] = True
-    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    tol = 1e-4 if dtype == torch.float32 else (3e-2 if cfg["layers"] > 2 else 2e-2)
     if g["hap1"].dtype == np.float16:
         tol = max(tol, 1e-3)
     for h in ("1", "2"):
         np.testing.assert_allclose(res[f"h{h}"][ok], g[f"hap{h}"].astype(np.float32)[ok], atol=tol, rtol=0)
     if "gt" in g:
         np.testing.assert_allclose(res["gt"][ok], g["gt"][ok], atol=2 * tol, rtol=0)
+
+
+@pytest.mark.parametrize("case", ["infer_c5_b256", "infer_c5_m90"])
+def test_infer_tied_rows_vs_oracle(case):
+    """The sample-windows the fixture test above leaves out (the reference's k-th neighbour
+    distance ties the (k+1)-th: its FAISS order picks one of the tied haplotypes arbitrarily).
+    For EVERY row: our neighbours are tie-equivalent to the reference's — the multisets of exact
+    (float64) squared distances in the reference's own index embedding space are equal
+    (embedding_rag_infer_dataset.py:164-181, :274-285) — and our imputed p(alt) equals the
+    oracle (oracle/model_np.forward + data_np.infer_probs, infer_embedding_rag.py:141-152) run
+    on OUR neighbours within 1e-4 (f32).  Together with the fixture test this covers 100 % of
+    the sample-windows."""
+    from conftest import golden_state_dict, load_golden
+    from oracle import data_np, model_np
+    from src.dataset.sampler import WindowMajorSampler
+    g, cfg, ds, res = _fixture_run(case, torch.float32)
+    k = cfg["k"]
+    sd = golden_state_dict(cfg)
+    sd = {kk: np.asarray(v, np.float32) for kk, v in sd.items()}
+    order = list(iter(WindowMajorSampler(ds)))
+    tied = np.nonzero(~((g["kth_margin_h1"] > 1e-3) & (g["kth_margin_h2"] > 1e-3)))[0]
+    assert len(tied) > 0
+    check_rows = sorted(set(tied.tolist()) | {0, len(order) - 1})
+    for r in check_rows:
+        it = ds[order[r]]
+        w = int(it["window_idx"])
+        ref_tok = np.asarray(ds.ref_tokens_complete[w]).astype(np.int64)
+        ref_af = np.asarray(ds.ref_af_windows[w], np.float32)
+        masked = ref_tok.copy()
+        masked[:, np.asarray(ds.infer_masks[w]) == 1] = 4
+        e_ref = model_np.embed(masked, np.broadcast_to(ref_af, masked.shape), sd).astype(np.float64)
+        af = it["af"].numpy()[None]
+        for h, ours, theirs in (("1", res["idx1"][r], g["I_h1"][r]), ("2", res["idx2"][r], g["I_h2"][r])):
+            e_q = model_np.embed(it[f"hap_{h}"].numpy()[None], af, sd).astype(np.float64)[0]
+            d = ((e_ref - e_q[None]) ** 2).sum((1, 2))
+            np.testing.assert_allclose(np.sort(d[ours]), np.sort(d[theirs]), rtol=1e-6,
+                                       err_msg=f"row {r} h{h}: not tie-equivalent")
+        xo = {key: it[key].numpy()[None] for key in ("hap_1", "hap_2", "af", "af_p", "pos", "ref", "het", "hom")}
+        xo["rag_mean_h1"] = model_np.rag_mean(ref_tok, res["idx1"][r][None], ref_af, sd)
+        xo["rag_mean_h2"] = model_np.rag_mean(ref_tok, res["idx2"][r][None], ref_af, sd)
+        o = model_np.forward(xo, sd, cfg["layers"], cfg["heads"])
+        p1, p2, _ = data_np.infer_probs(o["probs_h1"], o["probs_h2"])
+        np.testing.assert_allclose(res["batch_h1"][r], p1[0], atol=1e-4, rtol=0, err_msg=f"row {r}")
+        np.testing.assert_allclose(res["batch_h2"][r], p2[0], atol=1e-4, rtol=0, err_msg=f"row {r}")

@@ -3,7 +3,7 @@
 The bench (configs[2]) searches 512 query haplotypes against a 1,000,000-haplotype,
 1024-site panel: 32 query tiles -> G = 4 co-scheduled query groups sharing each panel
 range (csrc/knn.hip scan2_kernel slot/group/part mapping), the n_parts >= 256 branch of
-``scan_parts`` and the threshold pre-pass over a 1/128 panel prefix.  Every case here
+``scan_parts`` and the threshold pre-pass over a 1/64 panel prefix.  Every case here
 compares the device top-k keys with the ORACLE (``oracle/knn_np.knn``, float64-exact
 (distance, index) order) run on the host copy of the same panel and the same integer LUT
 the device quantised; sampled queries cover every query group.

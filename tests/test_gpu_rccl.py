@@ -32,7 +32,9 @@ def _free_port():
 
 
 def _worker(port, q):
+    import faulthandler
     import sys
+    faulthandler.dump_traceback_later(80, exit=True)   # a hung collective names itself, then exits
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
     sys.path[:0] = [root, os.path.join(root, "rag-snvbert_amd")]
     import torch.distributed as dist
@@ -47,6 +49,7 @@ def _worker(port, q):
         from src import kernels as K
         from src.main.optimizer import FlatParams, GradBucketer
         done = []
+        print("nccl up", flush=True)
         x8 = torch.arange(4 * 70, device=dev, dtype=torch.int64).remainder(251).to(torch.uint8).view(4, 70)
         g8 = shards._all_gather(x8)
         assert g8.shape == (1, 4, 70) and g8.dtype == torch.uint8 and torch.equal(g8[0], x8)
@@ -54,13 +57,16 @@ def _worker(port, q):
         g64 = shards._all_gather(x64)
         assert torch.equal(g64[0], x64)
         done.append("all_gather_into_tensor u8/int64")
+        print(done[-1], flush=True)
         rows, sizes = shards.all_gather_rows(torch.randn(3, 7, device=dev))
         assert sizes == [3] and rows.shape == (3, 7)
         done.append("all_gather_rows")
+        print(done[-1], flush=True)
         c = shards._all_reduce(x8.clone(), dist.ReduceOp.SUM)
         assert torch.equal(c, x8)
         assert shards.any_rank(True, dev) and not shards.any_rank(False, dev)
         done.append("all_reduce u8 SUM / int32 MAX")
+        print(done[-1], flush=True)
         # the sharded search on the HIP kernels, a world of one == the plain index search
         rng = np.random.default_rng(1)
         N, S, L, D, k = 3000, 300, 1030, 64, 8
@@ -71,8 +77,8 @@ def _worker(port, q):
         site_mask = torch.from_numpy((rng.random(S) < 0.4).astype(np.uint8)).to(dev)
         tok = torch.zeros(9, L, dtype=torch.long, device=dev)
         tok[:, 0], tok[:, S + 1] = 2, 3
-        q = codes[torch.from_numpy(rng.integers(0, N, 9)).to(dev), :S].long()
-        tok[:, 1:S + 1] = torch.where(site_mask.bool()[None], torch.full_like(q, 4), 5 + q)
+        qr = codes[torch.from_numpy(rng.integers(0, N, 9)).to(dev), :S].long()
+        tok[:, 1:S + 1] = torch.where(site_mask.bool()[None], torch.full_like(qr, 4), 5 + qr)
         ops = shards.kernel_ops(index, W, site_mask, k)
         idx, _, counts = shards.sharded_neighbours(tok, k, ops)
         want, _ = index.search(tok, W, site_mask, k)
@@ -87,6 +93,7 @@ def _worker(port, q):
         assert torch.equal(idx2, want2)
         assert torch.equal(uniq, torch.unique(want2[want2 >= 0])) and torch.equal(ucodes, codes[uniq])
         done.append("sharded_neighbours (counts, codes + query offsets)")
+        print(done[-1], flush=True)
         # one bucketed gradient all-reduce step over RCCL
         net = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.Tanh(), torch.nn.Linear(64, 16)).to(dev)
         fp = FlatParams(net.parameters(), mirror=False)
@@ -106,14 +113,21 @@ def _worker(port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
+@pytest.mark.timeout(140)
 def test_rccl_world1_collectives():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_free_port(), q))
     p.start()
-    status, info = q.get(timeout=220)
-    p.join(60)
+    try:
+        status, info = q.get(timeout=100)
+    except Exception:                                  # queue.Empty: the child hung (e.g. in init)
+        status, info = "hung", "no result from the nccl child within 100 s"
+    finally:
+        p.join(20)
+        if p.is_alive():
+            p.kill()
+            p.join(10)
     assert status == "ok", info
     assert p.exitcode == 0
     print("\n".join(info))

@@ -170,6 +170,25 @@ def test_hip_linear_backward(M, K_, N, multi):
         assert rel(b.grad, r.grad) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K_,splits", [(1, 128, 128, 0), (1000, 1152, 384, 0), (4097, 384, 1536, 0),
+                                            (4097, 384, 1536, 3), (24 * 2 * 1025, 384, 384, 0), (33, 256, 128, 64)])
+def test_linear_dw_kernel_vs_fp32(M, N, K_, splits):
+    """dW = dy^T x and db = sum dy (csrc/dw.hip) against fp32 torch on the same bf16 values: ragged
+    M (not a multiple of the 32-row stage), more chunks than stages, the bench's 2BL rows."""
+    from src import kernels as K
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(M, K_, generator=g).to(DEV, torch.bfloat16)
+    dw, db = K.linear_dw(dy, x, bias=True, splits=splits)
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    tol = 1e-5 * math.sqrt(M) * 4
+    assert (dw.double() - ref_w).abs().max().item() < tol
+    assert (db.double() - ref_b).abs().max().item() < tol
+    dw2, none = K.linear_dw(dy, x)
+    assert none is None and (dw2.double() - ref_w).abs().max().item() < tol
+
+
 @pytest.mark.parametrize("M,N,resid", [(1000, 384, True), (517, 1536, False), (64, 64, True)])
 def test_hip_add_layernorm_fwd_bwd(M, N, resid):
     from src.autograd_ops import hip_add_layernorm
@@ -329,6 +348,51 @@ def test_train_gradients_vs_reference_autograd():
     for key in (k for k in g if k.startswith("b:")):
         buf = dict(m.named_buffers())[key[2:]]
         np.testing.assert_allclose(buf.cpu().numpy(), g[key], rtol=1e-4, atol=1e-5)
+
+
+def test_train_gradients_f32_mode_vs_reference_autograd():
+    """The same train-mode graph in the f32 parity mode (autograd_ops.set_train_precision:
+    exact-f32 MFMA Linear layers, f32 LayerNorm / attention): EVERY parameter gradient within
+    1e-3 relative (Frobenius) of the reference's own autograd (train_tiny.npz), the losses within
+    1e-5 and the outputs within 1e-5 — so a gradient bug of any size in any layer, BatchNorm
+    path included, fails here rather than hiding in bf16 noise (the bf16 bar above stays)."""
+    from src.autograd_ops import focal_loss, set_train_precision
+    g, cfg, m = _train_model("train_tiny")
+    x = _train_inputs(g)
+    set_train_precision(torch.float32)
+    try:
+        out = m(x)
+        mk = x["mask"].bool()
+        l1 = focal_loss(out[0], x["hap_1_label"], mk, 2.0, 1.0)
+        l2 = focal_loss(out[1], x["hap_2_label"], mk, 2.0, 1.0)
+        lg = focal_loss(out[2], x["gt_label"], mk, 2.0, 1.0)
+        total = 3 * l1 + 3 * l2 + 4 * lg
+        total.backward()
+    finally:
+        set_train_precision(torch.bfloat16)
+    np.testing.assert_allclose([l1.item(), l2.item(), lg.item(), total.item()], g["losses"], rtol=1e-5)
+    np.testing.assert_allclose(out[0].detach().cpu().numpy(), g["probs_h1"], atol=1e-5)
+    np.testing.assert_allclose(out[2].detach().cpu().numpy(), g["gt"], atol=1e-5)
+    named = dict(m.named_parameters())
+    gnorm_all = math.sqrt(sum(float((g[k] ** 2).sum()) for k in g if k.startswith("g:")))
+    worst, checked = (0.0, None), 0
+    for key in (k for k in g if k.startswith("g:")):
+        name = key[2:]
+        ref = torch.from_numpy(g[key]).to(DEV).double()
+        p = named[name]
+        got = p.grad.double() if p.grad is not None else torch.zeros_like(ref)
+        rn = ref.norm().item()
+        if rn < 1e-6 * gnorm_all:
+            assert got.norm().item() <= 1e-5 * gnorm_all + 1e-9, name
+            continue
+        rel = ((got - ref).norm() / rn).item()
+        worst = max(worst, (rel, name))
+        checked += 1
+    assert worst[0] <= 1e-3, worst
+    assert checked > 50
+    for key in (k for k in g if k.startswith("b:")):
+        buf = dict(m.named_buffers())[key[2:]]
+        np.testing.assert_allclose(buf.cpu().numpy(), g[key], rtol=1e-5, atol=1e-6)
 
 
 def test_train_forward_matches_eval_engine_without_dropout():

@@ -25,7 +25,7 @@ def _dataset(g, index_window_len=510):
     return make_infer_dataset(a, index_window_len=index_window_len)[0]
 
 
-@pytest.mark.parametrize("case", ["infer_c5", "infer_c5_b256"])
+@pytest.mark.parametrize("case", ["infer_c5", "infer_c5_b256", "infer_c5_d384", "infer_c5_m10", "infer_c5_m90"])
 def test_infer_index_windows_match_reference(case):
     g = load_golden(case)
     ds = _dataset(g)

@@ -21,7 +21,7 @@ for s in $STEPS; do
   case $s in
     kernels) step pytest_kernels 900 python -m pytest tests/test_gpu_kernels.py -q -rf --timeout 300 ;;
     model)   step pytest_model 900 python -m pytest tests/test_gpu_model.py -q -rf --timeout 300 ;;
-    gpu)     step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf --timeout 300 ;;
+    gpu)     step pytest_gpu 1200 python -u -m pytest tests -m gpu -v -rf --timeout 150 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 900 python bench.py --steps ${BSTEPS:-5} --warmup 2 ${BENCH_ARGS:-} ;;
     benchab) step bench_old 900 env SNVRAG_GEMM_TILE128=1 SNVRAG_UNFUSED_LN=1 python bench.py --steps ${BSTEPS:-5} --warmup 2 --cpu-baseline 0
