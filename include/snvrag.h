@@ -311,6 +311,9 @@ int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, const void* 
                         const float* ln1_g, const float* ln1_b, const float* ffn_vec, float eps, void* stream);
 int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* out, const void* wstream,
                             const float* ffn_vec, float eps, void* stream);
+/* Diagnostics: buffer of [workgroups][4 waves][10] uint64 phase stamps filled by the block tail at
+ * D = 384 when SNVRAG_TAIL_VARIANT=4 (a separate stamped instantiation; NULL turns it off). */
+int snvrag_tail_stamps(void* buf);
 /* Projection on the same 32x32-MFMA stream machinery (the QKV projection of
  * multi_head_attention.py:44-46, bf16): out[M, NC*D] = x[M, D] W^T + bias with W [NC*D, D]
  * packed once by snvrag_proj_pack (snvrag_proj_pack_bytes(D, NC) bytes); D in {128, 256,

@@ -113,10 +113,16 @@ struct TailArgs {
   const float* vec;     // [b1 4D | b2' | c1 | g2 | be2]
   const float* b_o; const float* g1; const float* be1;
   float eps;
+  unsigned long long* stamps;   // VAR 2 (diagnostics): [workgroup][wave][TL_NSTAMP] s_memtime stamps
 };
 
+// diagnostic stamp points of VAR 2 (slot 0: s_memrealtime at entry, 1..: s_memtime)
+constexpr int TL_NSTAMP = 10;
+enum { TS_REAL0 = 0, TS_START, TS_PROLOGUE, TS_PROJ, TS_LN1, TS_FFN, TS_EPI, TS_END, TS_REAL1 };
+
 // VAR (diagnostics): 0 default; 1 = no weight DMA after the prologue (compute-side ceiling;
-// results are garbage).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
+// results are garbage); 2 = the default kernel plus per-wave s_memtime stamps at the phase
+// boundaries into p.stamps (a separate instantiation: no stamp executes in the real kernel).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
 // SNVRAG_TAIL_VARIANT (launch_tail): 1 = PF 8, 2 = VAR 1, 3 = no schedule groups.
 // NC > 0: projection mode (snvrag_proj_forward): out[M, NC*D] = act W^T + b over NC output
 // chunks of D features (the QKV projection: NC = 3), the same stream / ring / read machinery.
@@ -138,6 +144,17 @@ void tail_kernel(TailArgs p) {
   const int ln = lane & 31, hh = lane >> 5;
   const long row = (long)blockIdx.x * TL_ROWS + wave * 32 + ln;
   const long rc = row < p.M ? row : (long)p.M - 1;
+  // (VAR 2) stamp: every lane writes the same value to the same slot through a vector store
+  // (branch-free: an exec-masked store splits the unrolled stream into blocks and changes the
+  // register allocation being measured)
+  auto stamp = [&](int slot, bool real = false) {
+    if constexpr (VAR == 2) {
+      const unsigned long long t = real ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+      __builtin_nontemporal_store(t, p.stamps + ((long)blockIdx.x * 4 + wave) * TL_NSTAMP + slot);
+    }
+  };
+  stamp(TS_REAL0, true);
+  stamp(TS_START);
 
   // ---- vector tables to LDS first (their loads are waited on at once), then the activations
   // as B fragments (k-step s: features tail_in_feat(s, hh, 0..7)); the residual rows of PRE are
@@ -217,6 +234,7 @@ void tail_kernel(TailArgs p) {
   static_assert(4 * (TL_NSLOT - 2) + NRR <= 63, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (TL_NSLOT - 2) + NRR) : "memory");
   __syncthreads();                                   // slab 0, the activations + the vector tables visible
+  stamp(TS_PROLOGUE);
 
   // read side: rd_slot = ring slot of the current part's first slab
   int rd_slot = 0;
@@ -354,13 +372,24 @@ void tail_kernel(TailArgs p) {
     // xa[0..3], shifted down after each group (a straight-line 288-MFMA body makes hipcc
     // shuffle the accumulators between AGPRs)
     static_assert(KS % 4 == 0 && (4 * NT) % 16 == 0, "groups of 4 k-steps are whole slabs");
+    // the residual x is added into ao at the start of group RR_G (its loads, queued behind the
+    // first NSLOT - 1 weight slabs, have landed by then), so its 96 registers (D = 384) are free
+    // again before LN1, where they would otherwise sit beside x1's B fragments and spill
+    constexpr int RR_G = KS / 4 > 3 ? 3 : -1;
     tl_unroll([&](auto gc) {
       constexpr int g = decltype(gc)::value;
+      if constexpr (g == RR_G) {
+#pragma unroll
+        for (int T = 0; T < NT; ++T)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ao[T][i] += tl_bf(rr[2 * T + (i >> 3)], i & 7);
+      }
       run(std::integral_constant<int, 4 * NT>{}, std::integral_constant<int, g * (NT / 4)>{}, [&](auto fc, const u32x4& A) {
         constexpr int f = decltype(fc)::value;
         ao[f % NT] = mfma32(A, xa[4 * g + f / NT], ao[f % NT]);
       });
     }, std::make_integer_sequence<int, KS / 4>{});
+    stamp(TS_PROJ);
     // ---- x1 = LN1(ao) -> xr (B fragments): pass 1 sums v and v^2, pass 2 normalises
     // (v re-read from the AGPR accumulators, never all held in VGPRs)
     float sum = 0.f, sq = 0.f;
@@ -368,8 +397,11 @@ void tail_kernel(TailArgs p) {
     for (int T = 0; T < NT; ++T)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float v = ao[T][i] + tl_bf(rr[2 * T + (i >> 3)], i & 7);
-        ao[T][i] = v;
+        float v = ao[T][i];
+        if constexpr (RR_G < 0) {
+          v += tl_bf(rr[2 * T + (i >> 3)], i & 7);
+          ao[T][i] = v;
+        }
         sum += v;
         sq = fmaf(v, v, sq);
       }
@@ -394,6 +426,7 @@ void tail_kernel(TailArgs p) {
                                tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
     }
   }
+  stamp(TS_LN1);
   // x1 opaque from here on: otherwise hipcc folds the epilogue's bf16 -> f32 unpacking of x1
   // into LN1 (it knows pack(y)) and carries 192 unpacked floats through the FFN loop
 #pragma unroll
@@ -476,6 +509,7 @@ void tail_kernel(TailArgs p) {
   for (int m = 0; m < 16; ++m) epi_pair(h1, m);
   phase2(std::false_type{});
 
+  stamp(TS_FFN);
   // ---- epilogue: out = LN2(x1 + lrelu(rstd_f acc - rstd_f mean_f c1 + b2'))
   st1 += __shfl_xor(st1, 32, 64);
   st2 += __shfl_xor(st2, 32, 64);
@@ -486,6 +520,7 @@ void tail_kernel(TailArgs p) {
   float* ev = reinterpret_cast<float*>(ring);        // [b2' | c1 | g2 | be2]
   for (int i = tid; i < 4 * D; i += 256) ev[i] = p.vec[4 * D + i];
   __syncthreads();
+  stamp(TS_EPI);
   const float* b2 = ev;
   const float* c1 = ev + D;
   const float* g2 = ev + 2 * D;
@@ -529,6 +564,11 @@ void tail_kernel(TailArgs p) {
             u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
                   tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
     }
+  }
+  if constexpr (VAR == 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the row stores have left
+    stamp(TS_END);
+    stamp(TS_REAL1, true);
   }
 }
 
@@ -588,12 +628,18 @@ static int launch_proj(const TailArgs& a, hipStream_t s) {
   return 0;
 }
 
+static unsigned long long* g_tail_stamps = nullptr;   // snvrag_tail_stamps (diagnostics)
+
 template <int D, bool PRE>
-static int launch_tail(const TailArgs& a, hipStream_t s) {
+static int launch_tail(TailArgs a, hipStream_t s) {
   const char* ev = getenv("SNVRAG_TAIL_VARIANT");
   const int var = ev ? atoi(ev) : 0;
   auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
               : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false> : tail_kernel<D, PRE>;
+  if (var == 4 && D == 384 && g_tail_stamps) {           // phase stamps (tools/tail_micro.py)
+    kern = tail_kernel<D, PRE, TL_PF_DEFAULT, 2>;
+    a.stamps = g_tail_stamps;
+  }
   constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + 7 * D * 4;     // ring + b1, g1, be1, b_o
   static_assert(7 * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -618,6 +664,11 @@ static size_t tail_bytes(int D) {
 using namespace snvrag;
 
 extern "C" size_t snvrag_tail_pack_bytes(int D) { return tail_bytes(D); }
+
+extern "C" int snvrag_tail_stamps(void* buf) {
+  g_tail_stamps = (unsigned long long*)buf;
+  return 0;
+}
 
 extern "C" int snvrag_tail_pack(int D, const void* w_o, const void* w1, const void* w2g, void* out, void* stream) {
   SNV_CHECK_ARG(tail_d_ok(D), "block tail needs D in {128, 256, 384}");
@@ -663,7 +714,7 @@ extern "C" int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, c
                 "pointers must be 16-byte aligned");
   if (M == 0) return 0;
   const TailArgs a{(int)M, (const bf16*)att, (const bf16*)x, (bf16*)x, (const char*)wstream, ffn_vec, b_o, ln1_g,
-                   ln1_b, eps};
+                   ln1_b, eps, nullptr};
   return tail_common(M, D, true, a, stream);
 }
 
@@ -678,7 +729,7 @@ extern "C" int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* o
                 "pointers must be 16-byte aligned");
   if (M == 0) return 0;
   const TailArgs a{(int)M, (const bf16*)x1, nullptr, (bf16*)out, (const char*)wstream, ffn_vec, nullptr, nullptr,
-                   nullptr, eps};
+                   nullptr, eps, nullptr};
   return tail_common(M, D, false, a, stream);
 }
 
@@ -714,7 +765,7 @@ extern "C" int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, cons
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const TailArgs a{(int)M, (const bf16*)x, nullptr, (bf16*)out, (const char*)wstream, bias, nullptr, nullptr,
-                   nullptr, 0.f};
+                   nullptr, 0.f, nullptr};
   evlog_begin(s);
   int rc;
   switch (D * 8 + NC) {

@@ -190,13 +190,16 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, *, resid: Optio
 
 
 def attention(qkv: torch.Tensor, nseq: int, L: int, heads: int, dh: int,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, scale: Optional[float] = None) -> torch.Tensor:
+    """softmax(q k^T * scale) v per (sequence, head); scale defaults to 1/sqrt(dh).  scale =
+    1/log2(e) declares Q pre-scaled by log2(e)/sqrt(dh) (the engine's q_scale)."""
     N.require_gpu(qkv)
     D = heads * dh
     if out is None:
         out = torch.empty(nseq * L, D, device=qkv.device, dtype=qkv.dtype)
     check(N.lib().snvrag_attention(_dt(qkv.dtype), nseq, L, heads, dh, ptr(_c(qkv)), qkv.shape[-1],
-                                   ptr(out), D, 1.0 / float(dh) ** 0.5, stream_ptr()), "attention")
+                                   ptr(out), D, 1.0 / float(dh) ** 0.5 if scale is None else float(scale),
+                                   stream_ptr()), "attention")
     return out
 
 

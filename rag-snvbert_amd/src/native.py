@@ -123,6 +123,7 @@ _SIGS = {
     "snvrag_tail_pack": ([C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_tail_forward": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, f32, vp], C.c_int),
     "snvrag_tail_ffn_forward": ([i64, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
+    "snvrag_tail_stamps": ([vp], C.c_int),
     "snvrag_attention_train_fwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, f32, f32, C.c_uint64, vp],
                                    C.c_int),
     "snvrag_attention_bwd": ([i64, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, i64, vp, vp, vp, i64, f32, f32,

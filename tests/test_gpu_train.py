@@ -385,6 +385,11 @@ def test_train_gradients_f32_mode_vs_reference_autograd():
         if rn < 1e-6 * gnorm_all:
             assert got.norm().item() <= 1e-5 * gnorm_all + 1e-9, name
             continue
+        if name.endswith(("pos_feat.conv1.bias", "pos_feat.conv2.bias")):
+            # a bias feeding a train-mode BatchNorm: the batch-mean subtraction cancels it, the
+            # true gradient is 0 and both sides hold only rounding noise of the same size
+            assert got.norm().item() <= 2 * rn + 1e-6 * gnorm_all, name
+            continue
         rel = ((got - ref).norm() / rn).item()
         worst = max(worst, (rel, name))
         checked += 1
@@ -622,18 +627,18 @@ def test_train_retrieval_dense_and_shared_neighbour_dropout():
     from src.model import build_model
     torch.manual_seed(1)
     ds, vocab = make_rag_dataset(n_samples=6, n_sites=150, n_windows=1, n_ref_samples=6, seed=4, name="train")
-    m = build_model(len(vocab), 32, 1, 2, dropout=0.0).to(DEV).train()
+    m = build_model(len(vocab), 64, 1, 2, dropout=0.0).to(DEV).train()
     emb = m.bert.embedding
     batch = lambda: embedding_rag_collate_fn([ds[i] for i in range(6)])
     d0 = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4, dense=True)
     k0 = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4)
-    assert d0["rag_emb_h1"].shape == (6, 4, 1030, 32)
+    assert d0["rag_emb_h1"].shape == (6, 4, 1030, 64)
     torch.testing.assert_close(d0["rag_emb_h1"].mean(1), k0["rag_emb_h1"][:, 0], rtol=2e-2, atol=2e-2)
     emb.dropout.p = 0.3
     d = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=4, dense=True)
     e = torch.cat([d["rag_emb_h1"], d["rag_emb_h2"]]).detach()
     idx = torch.cat([d["rag_idx_h1"], d["rag_idx_h2"]])
-    flat_i, flat_e = idx.reshape(-1), e.reshape(-1, 1030, 32)
+    flat_i, flat_e = idx.reshape(-1), e.reshape(-1, 1030, 64)
     pairs = 0
     for a in range(flat_i.numel()):
         for b in range(a + 1, flat_i.numel()):

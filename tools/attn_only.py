@@ -1,5 +1,6 @@
 """Run only the bf16 dh=32 attention kernel at the bench shape (512 sequences x 1030 tokens,
 12 heads) — for rocprofv3 PMC passes and timing."""
+import math
 import os
 import sys
 
@@ -10,12 +11,18 @@ from src import kernels as K  # noqa: E402
 
 nseq, L, H, dh = int(os.environ.get("NSEQ", 512)), 1030, 12, 32
 qkv = (torch.randn(nseq * L, 3 * H * dh, device="cuda") * float(os.environ.get("QKV_STD", 0.4))).to(torch.bfloat16)
+# PRESCALED=1 (default): Q carries log2(e)/sqrt(dh) as in the engine (the QKV epilogue's q_scale),
+# so the bench's attn32_dma<true> runs; PRESCALED=0: the unscaled-Q kernel
+pre = os.environ.get("PRESCALED", "1") == "1"
+scale = 1.0 / math.log2(math.e) if pre else 1.0 / math.sqrt(dh)
+if pre:
+    qkv[:, :H * dh] = (qkv[:, :H * dh].float() * (math.log2(math.e) / math.sqrt(dh))).to(torch.bfloat16)
 out = None
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for i in range(int(os.environ.get("REPS", 3))):
     if i == 1:
         a.record()
-    out = K.attention(qkv, nseq, L, H, dh)
+    out = K.attention(qkv, nseq, L, H, dh, scale=scale)
 b.record()
 torch.cuda.synchronize()
 n = int(os.environ.get("REPS", 3)) - 1

@@ -1,5 +1,6 @@
 """32x32-MFMA block tail (csrc/tail.hip): correctness against a float64 torch reference on a small M,
-then launch times of its variants at the bench shape (M = 512 x 1030)."""
+then launch times of its variants at the bench shape (M = 512 x 1030), and the per-wave phase
+breakdown from the stamped diagnostic instantiation (s_memtime / s_memrealtime)."""
 import os
 import sys
 
@@ -86,3 +87,37 @@ for name, fn, fl in (
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
     ms = timeit(fn)
     print(f"{name:22s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
+
+# ---- phase stamps (SNVRAG_TAIL_VARIANT=4: the PRE kernel with s_memtime stamps per wave)
+import numpy as np  # noqa: E402
+from src import native as N  # noqa: E402
+
+nwg = (M + 127) // 128
+st = torch.zeros(nwg * 4 * 10, dtype=torch.int64, device=dev)
+N.lib().snvrag_tail_stamps(st.data_ptr())
+for _ in range(20):                                  # warm the clock up on the default kernel
+    tail_var(0)()
+tail_var(4)()
+torch.cuda.synchronize()
+N.lib().snvrag_tail_stamps(None)
+os.environ["SNVRAG_TAIL_VARIANT"] = "0"
+s = st.view(nwg * 4, 10).cpu().numpy().astype(np.float64)
+names = ["prologue (act loads + 8 slabs)", "out-projection (864 MFMA)", "LN1", "FFN (1728 MFMA)",
+         "FFN end -> ring free (vmcnt 0 + barrier + vec tables)", "LN2 + stores (+ vmcnt 0)"]
+clk = (s[:, 7] - s[:, 1]) / np.maximum(s[:, 8] - s[:, 0], 1) * 0.1     # GHz (realtime = 100 MHz)
+print(f"stamped launch: {nwg} workgroups; in-kernel clock median {np.median(clk):.3f} GHz", flush=True)
+tot = s[:, 7] - s[:, 1]
+for i, nm in enumerate(names):
+    d = s[:, i + 2] - s[:, i + 1]
+    print(f"  {nm:55s} median {np.median(d):9.0f} cyc  p10 {np.percentile(d, 10):9.0f}  p90 {np.percentile(d, 90):9.0f}"
+          f"  ({np.median(d) / np.median(tot):.3f} of the wave)", flush=True)
+print(f"  {'wave total':55s} median {np.median(tot):9.0f} cyc  (MFMA floor 2592 x 32 = 82944)", flush=True)
+r0 = s[:, 0].reshape(nwg, 4).min(1)
+r1 = s[:, 8].reshape(nwg, 4).max(1)
+span = (r1.max() - r0.min())
+busy = (r1 - r0).sum() / (256 * span)
+print(f"  workgroup residency: span {span / 100:.1f} us, sum of workgroup lifetimes / (256 CUs x span) = {busy:.3f}",
+      flush=True)
+order = np.sort(r0 - r0.min()) / 100
+print("  workgroup start times (us) at ranks 0/256/512/.../end: " +
+      " ".join(f"{order[i]:.1f}" for i in range(0, nwg, 256)) + f" | last {order[-1]:.1f}", flush=True)
