@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 22
+#define SNVRAG_ABI_VERSION 23
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -412,14 +412,21 @@ int snvrag_confusion(int64_t M, int C, const float* probs, const int64_t* labels
                      const uint8_t* mask2, uint64_t* counts, void* stream);
 
 /* Training LayerNorm (sublayer.py:15-16, feed_forward.py:20, nn.LayerNorm under autograd):
- * y = LN(x + r) g + b, bf16 [M, N] in/out (r nullable), f32 statistics; writes s = bf16(x + r)
- * (when r is given) and stats [M] = (mean, rstd) for the backward, which returns
- * ds (= dx = dr, bf16), dg, db (f32 [N]).  N % 8 == 0, N <= 2048. */
+ * y = drop_o(LN(x + drop_r(r)) g + b), bf16 [M, N] in/out (r nullable), f32 statistics; writes
+ * s = bf16(x + drop_r(r)) (when r is given) and stats [M] = (mean, rstd) for the backward.  The
+ * dropouts around the norms (sublayer.py / transformer.py: nn.Dropout) are fused: p_r on the
+ * residual operand, p_out on the output, counter-based keep masks of (seed, row, column)
+ * (attn_common.h's hash; streams 0 / 1), regenerated by the backward.  The backward returns
+ * ds (= dx; = dr when p_r == 0), dres = the masked ds (the gradient of r when p_r > 0), and
+ * dg, db (f32 [N]) written, or added to their contents when accumulate != 0 (the parameters'
+ * .grad buffers).  N % 8 == 0, N <= 2048. */
 int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
-                        float eps, void* y, void* s_out, float* stats, void* stream);
+                        float eps, void* y, void* s_out, float* stats, float p_r, float p_out, uint64_t seed,
+                        void* stream);
 size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N);
 int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
-                  void* ds, float* dg, float* db, void* ws, size_t ws_bytes, void* stream);
+                  void* ds, void* dres, float* dg, float* db, int accumulate, float p_r, float p_out,
+                  uint64_t seed, void* ws, size_t ws_bytes, void* stream);
 /* out[n] = sum_m x[m, n] for a bf16 [M, N] matrix (Linear bias gradients), f32 out. */
 size_t snvrag_colsum_ws_bytes(int64_t M, int N);
 int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, size_t ws_bytes, void* stream);
@@ -428,12 +435,13 @@ int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, si
  * through every nn.Linear of multi_head_attention.py:44-51, feed_forward.py:18-21, fusion.py,
  * foundation_model.py), csrc/dw.hip: dw[N, K] += sum_m dy[m, n] x[m, k] and, db != NULL,
  * db[N] += sum_m dy[m, n]; dy [M, N], x [M, K] bf16 row-major, f32 results ACCUMULATED (zero them
- * first).  32x32x16 MFMAs on LDS-transposed tiles, M split into `splits` chunks (0: enough to fill
+ * first; a parameter's f32 .grad can be passed directly), rows of dy / x ldy / ldx elements apart
+ * (a column slice of a fused N: the q/k/v parts).  32x32x16 MFMAs on LDS-transposed tiles, M split into `splits` chunks (0: enough to fill
  * the chip, snvrag_dw_splits) whose 128 x 128 tiles are added with float atomics (the summation
  * order across chunks is not fixed).  N, K multiples of 128. */
 int snvrag_dw_splits(int64_t M, int64_t N, int64_t K);
-int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, const void* x, float* dw, float* db,
-                     int splits, void* stream);
+int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x, int64_t ldx,
+                     float* dw, float* db, int splits, void* stream);
 
 /* Inference post-processing (replaces infer_embedding_rag.py:145-152): probs_h1/h2 [M, 2]
  * f32 head probabilities -> p1, p2 [M] = softmax(probs)[..., 1] (the reference's second

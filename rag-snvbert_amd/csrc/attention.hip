@@ -284,6 +284,14 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
   bf16x8 pb[NCB][2];
   bf16x8 pd[TRAIN ? NCB : 1][2];                 // TRAIN: the dropped-out PV operand
   float dmp[2] = {1.f, 1.f};                     // TRAIN: dropout multipliers of a key pair
+  // TRAIN: hash input of (query 16 qt + li, this lane's first key pair (kbase + 4 lg) / 2); the
+  // pair of (kt, j) adds the compile-time 8 kt + (j & 3) / 2
+  uint32_t drow[TRAIN ? 2 : 1];
+  if constexpr (TRAIN) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      drow[qt] = drop_row(tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li), (uint32_t)((kbase >> 1) + 2 * lg));
+  }
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
@@ -297,8 +305,7 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
           // keys 2i, 2i + 1 share one hash: computed at the even j, used at both
           if ((j & 1) == 0) {
             if (tr.drop.thresh)
-              drop_mul2(tr.drop, tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li),
-                        (uint32_t)(kbase + 16 * kt + 4 * lg + (j & 3)), dmp[0], dmp[1]);
+              drop_split(tr.drop, drop_mix24(drow[qt] + (uint32_t)(8 * kt + ((j & 3) >> 1)) * DROP_C2), dmp[0], dmp[1]);
             else
               dmp[0] = dmp[1] = 1.f;
           }

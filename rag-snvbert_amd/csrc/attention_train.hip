@@ -173,12 +173,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
       }
     }
     bf16x8 dsb[2];
+    // hash input of (q, key pair (64 t + 4 lg) / 2); (kt, r) adds 8 kt + r / 2
+    const uint32_t drow = drop_row(dbase, (uint32_t)q, (uint32_t)(32 * t + 2 * lg));
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; r += 2) {
         float dm[2] = {1.f, 1.f};
-        if (drop.thresh) drop_mul2(drop, dbase, (uint32_t)q, (uint32_t)(t * 64 + 16 * kt + 4 * lg + r), dm[0], dm[1]);
+        if (drop.thresh) drop_split(drop, drop_mix24(drow + (uint32_t)(8 * kt + (r >> 1)) * DROP_C2), dm[0], dm[1]);
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int key = t * 64 + 16 * kt + 4 * lg + r + e;
@@ -288,12 +290,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
     float mkv[4][4];
     if (drop.thresh) {
       const bool odd = li & 1;
+      // hash input of (query 64 t + 4 lg (+ 2 on odd lanes), this key's pair); (qt, rr) adds
+      // (16 qt + rr) * C1
+      const uint32_t drow = drop_row(dbase, (uint32_t)(t * 64 + 4 * lg + (odd ? 2 : 0)), (uint32_t)key >> 1);
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) {
-          const int r_mine = odd ? 2 + rr : rr;
-          const uint32_t hm = drop_hash(dbase, (uint32_t)(t * 64 + 16 * qt + 4 * lg + r_mine), (uint32_t)key >> 1);
+          const uint32_t hm = drop_mix24(drow + (uint32_t)(16 * qt + rr) * DROP_C1);
           const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
           const uint32_t h_lo = odd ? ho : hm, h_hi = odd ? hm : ho;       // hashes of r = rr, 2 + rr
           mkv[qt][rr] = (odd ? h_lo >> 16 : h_lo & 0xFFFFu) >= drop.thresh ? drop.scale : 0.f;

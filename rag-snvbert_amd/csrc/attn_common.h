@@ -30,18 +30,26 @@ __device__ __forceinline__ int k_off(int key, int chunk) {
 
 // Attention-probability dropout (model/attention/attention.py:28-29) with a counter-based
 // RNG, so the forward and both backward kernels regenerate the same keep mask.  One hash
-// serves a key PAIR (2j, 2j + 1), 16 bits each — the mask costs half the integer multiplies
-// of a hash per probability in the kernels whose lanes hold consecutive keys:
-//   h(q, j) = fmix32(base + q * 0x9E3779B1 + j * 0x85EBCA77),
+// serves a key PAIR (2j, 2j + 1), 16 bits each:
+//   h(q, j) = mix24(base + q * 0x9E3779B1 + j * 0x85EBCA77),
 //   base    = fmix32(lo(seed) ^ fmix32(hi(seed) + sh * 0xC2B2AE3D)),   sh = seq * heads + head
+//   mix24(h): h ^= h >> 16; h = lo32((h & 0xFFFFFF) * 0xEB352D); h ^= h >> 15;
+//             h = lo32((h & 0xFFFFFF) * 0x6CA68B); h ^= h >> 16
 // keep (q, k) iff half (k & 1) of h(q, k >> 1) >= thresh (thresh = round(p * 2^16), so the
 // drop probability is p to within 2^-17); kept probabilities are scaled by 1 / (1 - p).
-// thresh == 0: no dropout.  (tests/attn_helpers.py restates it for the parity tests.)
+// mix24 is the lowbias32 mixer with 24-bit multiplies (v_mul_u32_u24, full VALU rate) instead
+// of the quarter-rate 32-bit ones of fmix32: the mask is hashed per probability pair inside the
+// VALU-issue-bound attention loops (head dim 32), where fmix32's two v_mul_lo_u32 dominated the
+// dropout cost.  Callers keep the hash input additive (drop_row + pair offset * C2) so the
+// per-element work is one add plus the mixer.  thresh == 0: no dropout.
+// (tests/attn_helpers.py restates it; tests/test_host_cpu.py checks the mask statistics.)
 struct AttnDrop {
   uint32_t thresh;
   float scale;
   uint64_t seed;
 };
+constexpr uint32_t DROP_C1 = 0x9E3779B1u;     // query multiplier
+constexpr uint32_t DROP_C2 = 0x85EBCA77u;     // key-pair multiplier
 __host__ __device__ inline uint32_t drop_fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -50,11 +58,28 @@ __host__ __device__ inline uint32_t drop_fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
+__device__ __forceinline__ uint32_t drop_mix24(uint32_t h) {
+  h ^= h >> 16;
+  h = __umul24(h, 0xEB352Du);
+  h ^= h >> 15;
+  h = __umul24(h, 0x6CA68Bu);
+  h ^= h >> 16;
+  return h;
+}
 __host__ __device__ inline uint32_t drop_base(uint64_t seed, uint32_t sh) {
   return drop_fmix32((uint32_t)seed ^ drop_fmix32((uint32_t)(seed >> 32) + sh * 0xC2B2AE3Du));
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t base, uint32_t q, uint32_t pair) {
-  return drop_fmix32(base + q * 0x9E3779B1u + pair * 0x85EBCA77u);
+  return drop_mix24(base + q * DROP_C1 + pair * DROP_C2);
+}
+// hash input of (q, pair0): add dpair * DROP_C2 for pair0 + dpair
+__device__ __forceinline__ uint32_t drop_row(uint32_t base, uint32_t q, uint32_t pair0) {
+  return base + q * DROP_C1 + pair0 * DROP_C2;
+}
+// multipliers of the two keys of a pair from its hash
+__device__ __forceinline__ void drop_split(const AttnDrop& d, uint32_t h, float& m0, float& m1) {
+  m0 = (h & 0xFFFFu) >= d.thresh ? d.scale : 0.f;
+  m1 = (h >> 16) >= d.thresh ? d.scale : 0.f;
 }
 // dropout multiplier of probability (q, k): 0 or 1 / (1 - p)
 __device__ __forceinline__ float drop_mul(const AttnDrop& d, uint32_t base, uint32_t q, uint32_t k) {
@@ -64,9 +89,7 @@ __device__ __forceinline__ float drop_mul(const AttnDrop& d, uint32_t base, uint
 // multipliers of (q, k) and (q, k + 1) for even k: one hash
 __device__ __forceinline__ void drop_mul2(const AttnDrop& d, uint32_t base, uint32_t q, uint32_t k, float& m0,
                                           float& m1) {
-  const uint32_t h = drop_hash(base, q, k >> 1);
-  m0 = (h & 0xFFFFu) >= d.thresh ? d.scale : 0.f;
-  m1 = (h >> 16) >= d.thresh ? d.scale : 0.f;
+  drop_split(d, drop_hash(base, q, k >> 1), m0, m1);
 }
 static inline AttnDrop make_attn_drop(float p, uint64_t seed) {
   AttnDrop d;

@@ -36,8 +36,8 @@ __device__ __forceinline__ bf16x4 dw_tr(const char* p) {
 
 // grid: (N / 128, K / 128, S); 256 threads = 4 waves, wave (wn, wk) owns the 64 x 64 sub-tile
 // n0 + 64 wn, k0 + 64 wk (2 x 2 MFMA tiles of 32 x 32).
-__global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16* __restrict__ dy,
-                                                 const bf16* __restrict__ x, float* __restrict__ dw,
+__global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16* __restrict__ dy, long ldy,
+                                                 const bf16* __restrict__ x, long ldx, float* __restrict__ dw,
                                                  float* __restrict__ db, int chunk) {
   __shared__ __attribute__((aligned(16))) char smem[2 * DW_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -57,8 +57,8 @@ __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16
       const int c = tid + 256 * i, row = c >> 4, c16 = c & 15;
       const int m = m_begin + st * DW_R + row;
       const bool ok = m < m_end;
-      ry[i] = ok ? *reinterpret_cast<const u32x4*>(dy + (long)m * N + n0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
-      rx[i] = ok ? *reinterpret_cast<const u32x4*>(x + (long)m * K + k0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
+      ry[i] = ok ? *reinterpret_cast<const u32x4*>(dy + (long)m * ldy + n0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
+      rx[i] = ok ? *reinterpret_cast<const u32x4*>(x + (long)m * ldx + k0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto store = [&](int buf) {
@@ -153,11 +153,11 @@ extern "C" int snvrag_dw_splits(int64_t M, int64_t N, int64_t K) {
   return (int)s;
 }
 
-extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, const void* x, float* dw,
-                                float* db, int splits, void* stream) {
+extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x,
+                                int64_t ldx, float* dw, float* db, int splits, void* stream) {
   SNV_CHECK_ARG(dy && x && dw, "null pointer");
   SNV_CHECK_ARG(M >= 0 && N % DW_T == 0 && K % DW_T == 0 && N > 0 && K > 0, "N and K must be multiples of 128");
-  SNV_CHECK_ARG(M * std::max(N, K) < (1L << 31), "operand too large for 32-bit row offsets");
+  SNV_CHECK_ARG(ldy >= N && ldx >= K && ldy % 8 == 0 && ldx % 8 == 0, "leading dims: >= N / K, multiples of 8");
   SNV_CHECK_ARG(((uintptr_t)dy % 16) == 0 && ((uintptr_t)x % 16) == 0, "operands must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
   // dw / db are accumulated: the caller zeroes them (or passes a running sum)
@@ -167,7 +167,7 @@ extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy,
   const int S = (int)((M + chunk - 1) / chunk);
   evlog_begin(s);
   hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
-                     (int)M, (int)N, (int)K, (const bf16*)dy, (const bf16*)x, dw, db, chunk);
+                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, dw, db, chunk);
   SNV_LAUNCH_CHECK();
   evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
   return 0;

@@ -87,6 +87,7 @@ struct SgArgs {
   // CAT: x = [q | bf16(x2 * g2[m % period2])], q = `x` and x2 [M, D/2], g2 [period2, D/2] (fusion.py:157:
   // cat(h, aw * h_rag) built in registers)
   const bf16* x2; const bf16* g2; int period2;
+  int desync;               // > 0: first-round phase step in cycles (tail.hip's de-synchronised rounds)
 };
 
 template <int EPI, bool RANK> __host__ __device__ constexpr int sg_nvec(int N) {
@@ -112,6 +113,13 @@ void sg_kernel(SgArgs p) {
   const int N = p.N, NP = N / 64;                                  // tile pairs
   const long row = (long)blockIdx.x * ROWS + wave * 32 + ln;
   const long rc = row < p.M ? row : (long)p.M - 1;
+  // first-round workgroups start at 8 phase offsets (see tail.hip): later rounds' activation
+  // loads and output stores then stop hitting HBM as one chip-wide burst
+  if (p.desync > 0 && blockIdx.x < 256) {
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
 
   // ---- vector table -> LDS, x -> B fragments, rank scalars: all plain loads retire before the
   // DMA ring starts (its waits are counted)
@@ -641,8 +649,10 @@ __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w,
 }
 
 template <int D, int EPI, int ACT, bool RANK, int WAVES = 4, bool CAT = false>
-static int sg_launch(const SgArgs& a, hipStream_t s) {
+static int sg_launch(SgArgs a, hipStream_t s) {
   auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES, CAT>;
+  const char* dz = getenv("SNVRAG_SG_DESYNC");
+  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 && dz ? atoi(dz) : 0;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -114,6 +114,7 @@ struct TailArgs {
   const float* b_o; const float* g1; const float* be1;
   float eps;
   unsigned long long* stamps;   // VAR 2 (diagnostics): [workgroup][wave][TL_NSTAMP] s_memtime stamps
+  int desync;                   // > 0: first-round phase step in cycles (see tail_kernel)
 };
 
 // diagnostic stamp points of VAR 2 (slot 0: s_memrealtime at entry, 1..: s_memtime)
@@ -122,8 +123,10 @@ enum { TS_REAL0 = 0, TS_START, TS_PROLOGUE, TS_PROJ, TS_LN1, TS_FFN, TS_EPI, TS_
 
 // VAR (diagnostics): 0 default; 1 = no weight DMA after the prologue (compute-side ceiling;
 // results are garbage); 2 = the default kernel plus per-wave s_memtime stamps at the phase
-// boundaries into p.stamps (a separate instantiation: no stamp executes in the real kernel).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
-// SNVRAG_TAIL_VARIANT (launch_tail): 1 = PF 8, 2 = VAR 1, 3 = no schedule groups.
+// boundaries into p.stamps (a separate instantiation: no stamp executes in the real kernel);
+// 3 = residual added early (see RR_G).  TL_SGB: shape each slab's schedule as MFMA f / read f + PF pairs.
+// SNVRAG_TAIL_VARIANT (launch_tail): 1 = PF 8, 2 = VAR 1, 3 = no schedule groups, 4 = VAR 2
+// (stamps), 5 = VAR 3.
 // NC > 0: projection mode (snvrag_proj_forward): out[M, NC*D] = act W^T + b over NC output
 // chunks of D features (the QKV projection: NC = 3), the same stream / ring / read machinery.
 template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0, bool TL_SGB = true, int NC = 0>
@@ -154,6 +157,19 @@ void tail_kernel(TailArgs p) {
     }
   };
   stamp(TS_REAL0, true);
+  // De-synchronised rounds: every workgroup runs the same weight stream for the same time, so
+  // without this all 256 CUs start each round together and the prologue's activation + residual
+  // loads (192 KB per CU) and the epilogue's stores hit HBM as one chip-wide burst (measured:
+  // prologue 12 % of the wave, HBM-bound at ~4 TB/s, then idle HBM for the rest of the round).
+  // The first round's workgroups start at 8 phase offsets of `desync` cycles (per XCD: dispatch
+  // order blockIdx / 8), so later rounds stay spread and each CU's bursts overlap other CUs'
+  // MFMA phases.  The delay is paid once per CU; with >= 17 blocks per CU it ends inside the
+  // last partial round's slack.
+  if (p.desync > 0 && blockIdx.x < 256) {
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
   stamp(TS_START);
 
   // ---- vector tables to LDS first (their loads are waited on at once), then the activations
@@ -372,10 +388,10 @@ void tail_kernel(TailArgs p) {
     // xa[0..3], shifted down after each group (a straight-line 288-MFMA body makes hipcc
     // shuffle the accumulators between AGPRs)
     static_assert(KS % 4 == 0 && (4 * NT) % 16 == 0, "groups of 4 k-steps are whole slabs");
-    // the residual x is added into ao at the start of group RR_G (its loads, queued behind the
-    // first NSLOT - 1 weight slabs, have landed by then), so its 96 registers (D = 384) are free
-    // again before LN1, where they would otherwise sit beside x1's B fragments and spill
-    constexpr int RR_G = KS / 4 > 3 ? 3 : -1;
+    // VAR 3 (diagnostics): the residual x added into ao at the start of group 3 instead of in
+    // LN1's first pass (frees its registers before LN1, but waits for the residual burst earlier:
+    // measured slower, tools/tail_micro.py)
+    constexpr int RR_G = (VAR == 3 && KS / 4 > 3) ? 3 : -1;
     tl_unroll([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       if constexpr (g == RR_G) {
@@ -635,11 +651,18 @@ static int launch_tail(TailArgs a, hipStream_t s) {
   const char* ev = getenv("SNVRAG_TAIL_VARIANT");
   const int var = ev ? atoi(ev) : 0;
   auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
-              : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false> : tail_kernel<D, PRE>;
+              : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false>
+              : var == 5 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 3> : tail_kernel<D, PRE>;
   if (var == 4 && D == 384 && g_tail_stamps) {           // phase stamps (tools/tail_micro.py)
     kern = tail_kernel<D, PRE, TL_PF_DEFAULT, 2>;
     a.stamps = g_tail_stamps;
   }
+  // first-round phase step: only when every CU runs several rounds (the delay is paid once).
+  // Default 1/8 of a block's ~200 k cycles at D = 384 (tools/tail_micro.py, M = 527 360:
+  // 1.668 ms without, 1.611 / 1.593 / 1.602 ms at 12 k / 25 k / 40 k), scaled with the D^2 work
+  const char* dz = getenv("SNVRAG_TAIL_DESYNC");
+  const long nwg = cdiv(a.M, TL_ROWS);
+  a.desync = nwg >= 8 * 256 ? (dz ? atoi(dz) : 25000 * D / 384 * D / 384) : 0;
   constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + 7 * D * 4;     // ring + b1, g1, be1, b_o
   static_assert(7 * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -714,7 +737,7 @@ extern "C" int snvrag_tail_forward(int64_t M, int D, const void* att, void* x, c
                 "pointers must be 16-byte aligned");
   if (M == 0) return 0;
   const TailArgs a{(int)M, (const bf16*)att, (const bf16*)x, (bf16*)x, (const char*)wstream, ffn_vec, b_o, ln1_g,
-                   ln1_b, eps, nullptr};
+                   ln1_b, eps, nullptr, 0};
   return tail_common(M, D, true, a, stream);
 }
 
@@ -729,7 +752,7 @@ extern "C" int snvrag_tail_ffn_forward(int64_t M, int D, const void* x1, void* o
                 "pointers must be 16-byte aligned");
   if (M == 0) return 0;
   const TailArgs a{(int)M, (const bf16*)x1, nullptr, (bf16*)out, (const char*)wstream, ffn_vec, nullptr, nullptr,
-                   nullptr, eps, nullptr};
+                   nullptr, eps, nullptr, 0};
   return tail_common(M, D, false, a, stream);
 }
 
@@ -765,7 +788,7 @@ extern "C" int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, cons
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   const TailArgs a{(int)M, (const bf16*)x, nullptr, (bf16*)out, (const char*)wstream, bias, nullptr, nullptr,
-                   nullptr, 0.f, nullptr};
+                   nullptr, 0.f, nullptr, 0};
   evlog_begin(s);
   int rc;
   switch (D * 8 + NC) {

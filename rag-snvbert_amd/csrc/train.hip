@@ -14,6 +14,7 @@
 //             written for the next step's MFMA GEMMs.
 //   confusion: cal_pr (optim_schedule.py:167-203) as device counters (no per-batch D2H).
 #include "common.h"
+#include "attn_common.h"
 
 #include <cmath>
 
@@ -201,11 +202,35 @@ __device__ __forceinline__ void st8bf(bf16* p, const float* v) {
   *reinterpret_cast<bf16x8*>(p) = a;
 }
 
+// Element dropout fused into the LayerNorm kernels (the SublayerConnection / TransformerBlock
+// dropouts around the norms, transformer.py / sublayer.py): keep (m, n) iff half (n & 1) of
+// mix24(base + m * C1 + (n >> 1) * C2) >= thresh, base = drop_base(seed, stream) with stream 0
+// for the residual operand r and 1 for the output (attn_common.h's hash over (row, column)).
+struct LnDrop {
+  uint32_t th_r, th_o;          // round(p * 2^16); 0: off
+  float sc_r, sc_o;             // 1 / (1 - p)
+  uint32_t base_r, base_o;
+};
+static LnDrop make_ln_drop(float p_r, float p_o, uint64_t seed) {
+  const AttnDrop a = make_attn_drop(p_r, seed), b = make_attn_drop(p_o, seed);
+  return LnDrop{a.thresh, b.thresh, a.scale, b.scale, drop_base(seed, 0u), drop_base(seed, 1u)};
+}
+// multipliers of the 8 columns 8 cc .. 8 cc + 7 of row m: 4 hashes
+__device__ __forceinline__ void ln_drop8(uint32_t base, uint32_t th, float sc, long m, int cc, float (&mk)[8]) {
+  const uint32_t row = base + (uint32_t)m * DROP_C1 + (uint32_t)(4 * cc) * DROP_C2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t h = drop_mix24(row + (uint32_t)i * DROP_C2);
+    mk[2 * i] = (h & 0xFFFFu) >= th ? sc : 0.f;
+    mk[2 * i + 1] = (h >> 16) >= th ? sc : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ r, const float* __restrict__ g,
                                                            const float* __restrict__ b, float eps,
                                                            bf16* __restrict__ y, bf16* __restrict__ s_out,
-                                                           float2* __restrict__ stats) {
+                                                           float2* __restrict__ stats, LnDrop dr) {
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (m >= M) return;
@@ -220,6 +245,12 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
       if (r) {
         float t[8];
         ld8bf(r + m * N + 8 * cc, t);
+        if (dr.th_r) {
+          float mk[8];
+          ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] *= mk[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)(v[c][j] + t[j]);   // s is kept in bf16
       }
@@ -242,6 +273,12 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * g[8 * cc + j] + b[8 * cc + j];
+      if (dr.th_o) {
+        float mk[8];
+        ln_drop8(dr.base_o, dr.th_o, dr.sc_o, m, cc, mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+      }
       st8bf(y + m * N + 8 * cc, o);
       if (s_out) st8bf(s_out + m * N + 8 * cc, v[c]);
     }
@@ -250,11 +287,12 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
 }
 
 // RPB rows per block (one wave each, looping): the block's dg/db partials go to
-// part[blockIdx.x][2][N]
+// part[blockIdx.x][2][N].  Output dropout: dy is masked on load; residual dropout: dr = ds
+// masked (the gradient of r), written next to ds.
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per_wave, const bf16* __restrict__ dy,
                                                      const bf16* __restrict__ s, const float2* __restrict__ stats,
                                                      const float* __restrict__ g, bf16* __restrict__ ds,
-                                                     float* __restrict__ part) {
+                                                     bf16* __restrict__ dres, float* __restrict__ part, LnDrop dr) {
   extern __shared__ float red[];                      // [4 waves][2][N]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nc = N / 8;
@@ -277,6 +315,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
         float dv[8];
         ld8bf(s + m * N + 8 * cc, xh[c]);
         ld8bf(dy + m * N + 8 * cc, dv);
+        if (dr.th_o) {
+          float mk[8];
+          ln_drop8(dr.base_o, dr.th_o, dr.sc_o, m, cc, mk);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dv[j] *= mk[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] = (xh[c][j] - st.x) * st.y;
@@ -298,6 +342,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = st.y * (gy[c][j] - a1 - xh[c][j] * a2);
         st8bf(ds + m * N + 8 * cc, o);
+        if (dres) {
+          float mk[8];
+          ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+          st8bf(dres + m * N + 8 * cc, o);
+        }
       }
     }
   }
@@ -318,6 +369,36 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc += red[(w * 2 + which) * N + col];
     part[(long)blockIdx.x * 2 * N + n] = acc;
+  }
+}
+
+// column sums of the ln_bwd partials [R][2N] into dg (columns < N) and db: written, or added
+// to what they hold (accumulate: the parameters' .grad buffers); fixed-order (deterministic)
+__global__ __launch_bounds__(256) void ln_part_sum_kernel(long R, int N, const float* __restrict__ x,
+                                                          float* __restrict__ dg, float* __restrict__ db,
+                                                          int accumulate) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl, W = 2 * N;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < W) {
+    long r = gi;
+    for (; r + 48 < R; r += 64) {
+      a0 += x[r * W + c];
+      a1 += x[(r + 16) * W + c];
+      a2 += x[(r + 32) * W + c];
+      a3 += x[(r + 48) * W + c];
+    }
+    for (; r < R; r += 16) a0 += x[r * W + c];
+  }
+  red[gi][cl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (gi == 0 && c < W) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum += red[i][cl];
+    float* o = c < N ? dg + c : db + (c - N);
+    *o = accumulate ? *o + sum : sum;
   }
 }
 
@@ -381,13 +462,17 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, int row
 }  // namespace snvrag
 
 extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
-                                   float eps, void* y, void* s_out, float* stats, void* stream) {
+                                   float eps, void* y, void* s_out, float* stats, float p_r, float p_out,
+                                   uint64_t seed, void* stream) {
   SNV_CHECK_ARG(x && g && b && y && stats, "null pointer");
   SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
   SNV_CHECK_ARG(!r || s_out, "a residual needs s_out");
+  SNV_CHECK_ARG(p_r >= 0.f && p_r < 1.f && p_out >= 0.f && p_out < 1.f, "dropout probabilities must be in [0, 1)");
+  SNV_CHECK_ARG(r || p_r == 0.f, "residual dropout without a residual");
   if (M == 0) return 0;
   hipLaunchKernelGGL(ln_fwd_train_kernel, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N,
-                     (const bf16*)x, (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats);
+                     (const bf16*)x, (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats,
+                     make_ln_drop(p_r, p_out, seed));
   SNV_LAUNCH_CHECK();
   return 0;
 }
@@ -398,24 +483,26 @@ extern "C" size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N) {
 }
 
 extern "C" int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
-                             void* ds, float* dg, float* db, void* ws, size_t ws_bytes, void* stream) {
+                             void* ds, void* dres, float* dg, float* db, int accumulate, float p_r, float p_out,
+                             uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
   SNV_CHECK_ARG(dy && s && stats && g && ds && dg && db && ws, "null pointer");
   SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
   SNV_CHECK_ARG(ws_bytes >= snvrag_ln_bwd_ws_bytes(M, N), "workspace too small");
+  SNV_CHECK_ARG(p_r >= 0.f && p_r < 1.f && p_out >= 0.f && p_out < 1.f, "dropout probabilities must be in [0, 1)");
+  SNV_CHECK_ARG(!dres || p_r > 0.f, "dres is the residual-dropout gradient (p_r > 0)");
   if (M == 0) return 0;
   hipStream_t st = as_stream(stream);
   const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
   const int rpw = (int)((M + nblk * 4 - 1) / (nblk * 4));
   float* part = (float*)ws;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nblk), dim3(256), 4 * 2 * N * sizeof(float), st, (long)M, N, rpw,
-                     (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, part);
+                     (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, (bf16*)dres, part,
+                     make_ln_drop(p_r, p_out, seed));
   SNV_LAUNCH_CHECK();
-  // reduce the [nblk][2][N] partials: dg = part[:, 0, :], db = part[:, 1, :]
-  hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, 2 * N,
-                     (const float*)part, part, 0);   // rows of 2N: in place into row 0
+  // dg = sum over blocks of part[:, 0, :], db of part[:, 1, :] (written or accumulated)
+  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)part,
+                     dg, db, accumulate);
   SNV_LAUNCH_CHECK();
-  SNV_HIP(hipMemcpyAsync(dg, part, N * sizeof(float), hipMemcpyDeviceToDevice, st));
-  SNV_HIP(hipMemcpyAsync(db, part + N, N * sizeof(float), hipMemcpyDeviceToDevice, st));
   return 0;
 }
 

@@ -26,6 +26,7 @@ parameter version (the fused Adam kernel bumps the version in place).
 
 from __future__ import annotations
 
+import contextlib
 import os
 import weakref
 from typing import Dict, Optional, Tuple
@@ -200,6 +201,38 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b).float()
 
 
+_DIRECT_GRADS = False
+
+
+@contextlib.contextmanager
+def direct_weight_grads(enabled: bool = True):
+    """Inside this context (the trainer's ``loss.backward()``), Linear backward accumulates dW
+    and db straight into the parameters' f32 ``.grad`` (the flat gradient buffer of
+    ``FlatParams``) with the dW kernel, instead of returning fresh tensors that autograd then
+    adds in with one kernel per parameter (and zero-fills before: ~300 small launches per
+    step).  Those parameters get no autograd accumulation, so the post-accumulate hooks are
+    replaced by ``p._snv_grad_ready(p)`` (set by ``GradBucketer``).  Outside the context (e.g.
+    ``torch.autograd.grad``), gradients are returned as usual."""
+    global _DIRECT_GRADS
+    prev = _DIRECT_GRADS
+    _DIRECT_GRADS = enabled
+    try:
+        yield
+    finally:
+        _DIRECT_GRADS = prev
+
+
+def _grad_buffer(p) -> Optional[torch.Tensor]:
+    g = p.grad if (p is not None and p.requires_grad) else None
+    return g if (g is not None and g.dtype == torch.float32 and g.is_contiguous()) else None
+
+
+def _grad_ready(p) -> None:
+    cb = getattr(p, "_snv_grad_ready", None)
+    if cb is not None:
+        cb(p)
+
+
 class _HipLinear(torch.autograd.Function):
     """y = x [W_1; ..; W_n]^T + [b_1; ..; b_n]: one GEMM over weights concatenated along the
     output dim (the q/k/v Linear layers of multi_head_attention.py:44 as one N = 3D GEMM)."""
@@ -226,6 +259,7 @@ class _HipLinear(torch.autograd.Function):
         ctx.save_for_backward(x2, *ws)
         ctx.n, ctx.has_bias = n, has_b
         ctx.in_shape, ctx.in_dtype = x.shape, x.dtype
+        ctx.params = (ws, bs)                       # leaves: for the direct .grad accumulation
         return y.reshape(*x.shape[:-1], n_out)
 
     @staticmethod
@@ -265,8 +299,21 @@ class _HipLinear(torch.autograd.Function):
                 gx = K.linear(g2, wt)
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
         n_all, k_in = g2.shape[1], x2.shape[1]
-        if any(ctx.needs_input_grad[2:2 + ctx.n]) and n_all % 128 == 0 and k_in % 128 == 0 and \
-                not os.environ.get("SNVRAG_TRAIN_BLAS_DW"):
+        dw_ok = n_all % 128 == 0 and k_in % 128 == 0 and all(sz % 128 == 0 for sz in sizes) and \
+            not os.environ.get("SNVRAG_TRAIN_BLAS_DW")
+        pws, pbs = ctx.params
+        if _DIRECT_GRADS and dw_ok and all(_grad_buffer(w) is not None for w in pws) and \
+                (not ctx.has_bias or all(_grad_buffer(b) is not None for b in pbs)):
+            # accumulate into the flat gradient buffer: one dW launch per weight (its column
+            # slice of dy), bias sums fused
+            off = 0
+            for w, b, sz in zip(pws, pbs, sizes):
+                K.linear_dw(g2[:, off:off + sz], x2, dw=w.grad, db=b.grad if ctx.has_bias else None)
+                off += sz
+            for t in list(pws) + (list(pbs) if ctx.has_bias else []):
+                _grad_ready(t)
+            return (gx, None, *([None] * ctx.n), *([None] * ctx.n))
+        if any(ctx.needs_input_grad[2:2 + ctx.n]) and dw_ok:
             # dW (and db) on the split-M MFMA kernel (csrc/dw.hip), f32 accumulation and result
             gw, gb = K.linear_dw(g2, x2, bias=ctx.has_bias)
             gws = list(torch.split(gw, sizes, 0))
@@ -315,33 +362,58 @@ def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
 
 
 class _HipAddLayerNorm(torch.autograd.Function):
-    """y = LayerNorm(x + r) (r optional) in bf16 with f32 statistics (snvrag_ln_fwd_train /
-    snvrag_ln_bwd): one pass each way instead of torch's f32 conversion + LN + grad kernels."""
+    """y = drop_o(LayerNorm(x + drop_r(r))) (r optional) in bf16 with f32 statistics
+    (snvrag_ln_fwd_train / snvrag_ln_bwd): one pass each way instead of torch's f32 conversion +
+    LN + grad kernels, the dropouts around the norm fused (counter-based masks, regenerated by
+    the backward)."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps):
+    def forward(ctx, x, r, weight, bias, eps, p_r, p_out, seed):
         x = x.to(torch.bfloat16).contiguous()
         r = r.to(torch.bfloat16).contiguous() if r is not None else None
         y, s, stats = K.ln_fwd_train(x, r, weight.detach().float().contiguous(),
-                                     bias.detach().float().contiguous(), eps)
+                                     bias.detach().float().contiguous(), eps, p_r, p_out, seed)
         ctx.save_for_backward(s, stats, weight)
         ctx.has_r = r is not None
+        ctx.drop = (p_r, p_out, seed)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         s, stats, weight = ctx.saved_tensors
-        ds, dg, db = K.ln_bwd(gy.to(torch.bfloat16).contiguous(), s, stats, weight.detach().float().contiguous())
-        return ds, (ds if ctx.has_r else None), dg, db, None
+        p_r, p_out, seed = ctx.drop
+        w, b = ctx.params
+        direct = _DIRECT_GRADS and _grad_buffer(w) is not None and _grad_buffer(b) is not None
+        ds, dres, dg, db = K.ln_bwd(gy.to(torch.bfloat16).contiguous(), s, stats, weight.detach().float().contiguous(),
+                                    p_r, p_out, seed, dg=w.grad if direct else None, db=b.grad if direct else None)
+        dr = (dres if dres is not None else ds) if ctx.has_r else None
+        if direct:
+            _grad_ready(w)
+            _grad_ready(b)
+            return ds, dr, None, None, None, None, None, None
+        return ds, dr, dg, db, None, None, None, None
 
 
-def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln) -> torch.Tensor:
-    """bf16 LayerNorm(x + r) with the parameters of nn.LayerNorm ``ln`` (N % 8 == 0, N <= 2048)
-    (f32 parity mode: torch's f32 LayerNorm)."""
+def _drop_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln, p_r: float = 0.0,
+                      p_out: float = 0.0) -> torch.Tensor:
+    """bf16 drop_o(LayerNorm(x + drop_r(r))) with the parameters of nn.LayerNorm ``ln``
+    (N % 8 == 0, N <= 2048); p_r / p_out: dropout on the residual operand / the output
+    (training; the masks are a counter-based hash of a seed from torch's RNG).  f32 parity
+    mode: torch's f32 LayerNorm and F.dropout."""
     if train_dtype() == torch.float32:
-        s = x.float() + r.float() if r is not None else x.float()
-        return torch.nn.functional.layer_norm(s, (s.shape[-1],), ln.weight, ln.bias, ln.eps)
-    return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps)
+        rr = r.float() if r is not None else None
+        if rr is not None and p_r > 0:
+            rr = torch.nn.functional.dropout(rr, p_r, True)
+        s = x.float() + rr if rr is not None else x.float()
+        y = torch.nn.functional.layer_norm(s, (s.shape[-1],), ln.weight, ln.bias, ln.eps)
+        return torch.nn.functional.dropout(y, p_out, True) if p_out > 0 else y
+    seed = _drop_seed() if (p_r > 0 or p_out > 0) else 0
+    return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, float(p_r), float(p_out), seed)
 
 
 class _HipAttention(torch.autograd.Function):

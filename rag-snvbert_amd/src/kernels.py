@@ -545,8 +545,10 @@ def infer_post(probs_h1: torch.Tensor, probs_h2: torch.Tensor):
     return p1, p2, gt
 
 
-def ln_fwd_train(x: torch.Tensor, r: Optional[torch.Tensor], g: torch.Tensor, b: torch.Tensor, eps: float):
-    """(y bf16, s bf16 = x + r (x itself when r is None), stats f32 [M, 2])."""
+def ln_fwd_train(x: torch.Tensor, r: Optional[torch.Tensor], g: torch.Tensor, b: torch.Tensor, eps: float,
+                 p_r: float = 0.0, p_out: float = 0.0, seed: int = 0):
+    """(y bf16, s bf16 = x + drop(r) (x itself when r is None), stats f32 [M, 2]); y carries the
+    output dropout p_out (masks: counter-based hash of seed, row, column)."""
     N.require_gpu(x)
     Nn = x.shape[-1]
     M = x.numel() // Nn
@@ -555,35 +557,54 @@ def ln_fwd_train(x: torch.Tensor, r: Optional[torch.Tensor], g: torch.Tensor, b:
     stats = torch.empty(M, 2, device=x.device, dtype=torch.float32)
     check(N.lib().snvrag_ln_fwd_train(M, Nn, ptr(_c(x)), ptr(_c(r)) if r is not None else None,
                                       ptr(_c(g)), ptr(_c(b)), eps, ptr(y), ptr(s) if r is not None else None,
-                                      ptr(stats), stream_ptr()), "ln_fwd_train")
+                                      ptr(stats), float(p_r), float(p_out), int(seed) & (2 ** 64 - 1),
+                                      stream_ptr()), "ln_fwd_train")
     return y, s, stats
 
 
-def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tensor):
-    """(ds bf16, dg f32 [N], db f32 [N]) of y = LN(s) g + b."""
+def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tensor, p_r: float = 0.0,
+           p_out: float = 0.0, seed: int = 0, dg: Optional[torch.Tensor] = None,
+           db: Optional[torch.Tensor] = None):
+    """(ds bf16, dres bf16 or None, dg f32 [N], db f32 [N]) of y = drop_o(LN(s) g + b),
+    s = x + drop_r(r): ds = dx, dres = dr (None when p_r == 0: dr = ds).  dg / db given (f32,
+    contiguous: the parameters' .grad) are accumulated into, else fresh."""
     Nn = s.shape[-1]
     M = s.numel() // Nn
     ds = torch.empty_like(s)
-    dg = torch.empty(Nn, device=s.device, dtype=torch.float32)
-    db = torch.empty_like(dg)
+    dres = torch.empty_like(s) if p_r > 0 else None
+    acc = dg is not None
+    if dg is None:
+        dg = torch.empty(Nn, device=s.device, dtype=torch.float32)
+        db = torch.empty_like(dg)
+    assert db is not None and dg.is_contiguous() and db.is_contiguous() and dg.dtype == db.dtype == torch.float32
     wsb = N.lib().snvrag_ln_bwd_ws_bytes(M, Nn)
     ws = torch.empty(wsb, device=s.device, dtype=torch.uint8)
-    check(N.lib().snvrag_ln_bwd(M, Nn, ptr(_c(dy)), ptr(_c(s)), ptr(_c(stats)), ptr(_c(g)), ptr(ds), ptr(dg),
-                                ptr(db), ptr(ws), wsb, stream_ptr()), "ln_bwd")
-    return ds, dg, db
+    check(N.lib().snvrag_ln_bwd(M, Nn, ptr(_c(dy)), ptr(_c(s)), ptr(_c(stats)), ptr(_c(g)), ptr(ds), ptr(dres),
+                                ptr(dg), ptr(db), int(acc), float(p_r), float(p_out), int(seed) & (2 ** 64 - 1),
+                                ptr(ws), wsb, stream_ptr()), "ln_bwd")
+    return ds, dres, dg, db
 
 
-def linear_dw(dy: torch.Tensor, x: torch.Tensor, bias: bool = False, splits: int = 0):
-    """(dW f32 [N, K] = dy^T x, db f32 [N] = column sums of dy or None) for bf16 dy [M, N],
-    x [M, K] (csrc/dw.hip; N, K multiples of 128)."""
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, bias: bool = False, splits: int = 0,
+              dw: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
+    """dW f32 [N, K] += dy^T x and (bias) db f32 [N] += column sums of dy, for bf16 dy [M, N] and
+    x [M, K] whose rows may be strided (a column slice of a fused output: dy[:, a:b]); N, K
+    multiples of 128 (csrc/dw.hip).  dw / db are ACCUMULATED into when given (f32, contiguous:
+    e.g. a parameter's .grad), else zero-initialised.  Returns (dw, db or None)."""
     N.require_gpu(dy, x)
     assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[0] == x.shape[0]
+    assert dy.stride(1) == 1 and x.stride(1) == 1
     M, Nn = dy.shape
     Kk = x.shape[1]
-    dw = torch.zeros(Nn, Kk, device=dy.device, dtype=torch.float32)
-    db = torch.zeros(Nn, device=dy.device, dtype=torch.float32) if bias else None
-    check(N.lib().snvrag_linear_dw(M, Nn, Kk, ptr(_c(dy)), ptr(_c(x)), ptr(dw), ptr(db), int(splits), stream_ptr()),
-          "linear_dw")
+    if dw is None:
+        dw = torch.zeros(Nn, Kk, device=dy.device, dtype=torch.float32)
+    assert dw.dtype == torch.float32 and dw.is_contiguous() and tuple(dw.shape) == (Nn, Kk)
+    if bias and db is None:
+        db = torch.zeros(Nn, device=dy.device, dtype=torch.float32)
+    if db is not None:
+        assert db.dtype == torch.float32 and db.is_contiguous() and db.numel() == Nn
+    check(N.lib().snvrag_linear_dw(M, Nn, Kk, ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(dw), ptr(db),
+                                   int(splits), stream_ptr()), "linear_dw")
     return dw, db
 
 

@@ -148,7 +148,9 @@ class GradBucketer:
         self._hooks = []
         if self.active:
             for i, p in enumerate(flat.params):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+                hook = self._make_hook(i)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                p._snv_grad_ready = hook           # gradients accumulated in place by the HIP ops
 
     def _close(self, idxs, start, end):
         if idxs:

@@ -27,6 +27,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .. import autograd_ops
 from .optim_schedule import DeviceConfusion, FocalLoss, ScheduledOptim
 from .optimizer import FlatParams, FusedAdam, GradBucketer
 
@@ -100,7 +101,8 @@ class BERTTrainerWithValidationOptimized:
         self.ddp.enabled = last
         output = self.model(data)
         total, parts = self.loss(output, data)
-        total.backward()
+        with autograd_ops.direct_weight_grads():
+            total.backward()
         self.accum_step += 1
         if last:
             scale = self.ddp.finish()

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -141,13 +141,14 @@ _SIGS = {
     "snvrag_sgemm_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),
     "snvrag_sgemm_forward": ([i64, C.c_int, C.c_int, C.c_int, C.c_int, f32, vp, vp, vp, vp, vp, i64, f32, vp, vp, vp,
                               vp], C.c_int),
-    "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, vp], C.c_int),
+    "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, f32, f32, C.c_uint64, vp], C.c_int),
     "snvrag_ln_bwd_ws_bytes": ([i64, C.c_int], sz),
-    "snvrag_ln_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
+    "snvrag_ln_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, f32, f32, C.c_uint64, vp, sz, vp],
+                      C.c_int),
     "snvrag_colsum_ws_bytes": ([i64, C.c_int], sz),
     "snvrag_colsum_bf16": ([i64, C.c_int, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_dw_splits": ([i64, i64, i64], C.c_int),
-    "snvrag_linear_dw": ([i64, i64, i64, vp, vp, vp, vp, C.c_int, vp], C.c_int),
+    "snvrag_linear_dw": ([i64, i64, i64, vp, i64, vp, i64, vp, vp, C.c_int, vp], C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

@@ -69,11 +69,40 @@ def _conv1d(x: torch.Tensor, conv) -> torch.Tensor:
     return out + conv.bias[:, None]
 
 
-def pos_feat(pfm, pos: torch.Tensor) -> torch.Tensor:
-    """PositionFeatModule.forward (fusion.py:317-332), f32, BatchNorm in the module's mode."""
+def _batchnorm(bn, x: torch.Tensor, n_updates: int = 1) -> torch.Tensor:
+    """nn.BatchNorm1d over [B, C, L] in torch ops (f32).  Train mode: batch statistics (biased
+    variance) for the output, and the running statistics advanced as by ``n_updates`` forward
+    calls on this same batch (the reference's repeated emb_fusion calls, fusion.py:351-369).
+    The library (MIOpen) batch-norm backward at these shapes (C = 4 channels over B x 1030
+    positions) differs from the reference's CPU autograd by 2-24 % relative in the f32 parity
+    mode; these ops' autograd matches it to ~1e-6."""
+    if not (bn.training or bn.running_mean is None):
+        mean, var = bn.running_mean, bn.running_var
+    else:
+        dims = (0, 2)
+        mean = x.mean(dims)
+        var = (x - mean[None, :, None]).pow(2).mean(dims)
+        if bn.training and bn.track_running_stats:
+            with torch.no_grad():
+                n = x.numel() // x.shape[1]
+                var_u = var.detach() * (n / max(n - 1, 1))
+                for _ in range(n_updates):
+                    bn.num_batches_tracked += 1
+                    m = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+                    bn.running_mean.mul_(1 - m).add_(mean.detach(), alpha=m)
+                    bn.running_var.mul_(1 - m).add_(var_u, alpha=m)
+    y = (x - mean[None, :, None]) * torch.rsqrt(var[None, :, None] + bn.eps)
+    if bn.affine:
+        y = y * bn.weight[None, :, None] + bn.bias[None, :, None]
+    return y
+
+
+def pos_feat(pfm, pos: torch.Tensor, n_updates: int = 1) -> torch.Tensor:
+    """PositionFeatModule.forward (fusion.py:317-332), f32, BatchNorm in the module's mode
+    (train: running statistics advanced ``n_updates`` times, see _batchnorm)."""
     out = pos.float().unsqueeze(1)
-    out = pfm.norm1(F.leaky_relu(_conv1d(out, pfm.conv1), 0.05))
-    out = pfm.norm2(F.leaky_relu(_conv1d(out, pfm.conv2), 0.05))
+    out = _batchnorm(pfm.norm1, F.leaky_relu(_conv1d(out, pfm.conv1), 0.05), n_updates)
+    out = _batchnorm(pfm.norm2, F.leaky_relu(_conv1d(out, pfm.conv2), 0.05), n_updates)
     return F.leaky_relu(_conv1d(out, pfm.conv3), 0.05).squeeze(1)
 
 
@@ -92,13 +121,10 @@ def _ln(x: torch.Tensor, m) -> torch.Tensor:
 
 def emb_fusion(ef, embs: torch.Tensor, pos: torch.Tensor, af: torch.Tensor, n_calls: int) -> torch.Tensor:
     """EmbeddingFusionModule.forward (fusion.py:351-369) for n_calls stacked [B, L, D] inputs.
-    pos_feat runs once per reference call (its BatchNorm running statistics update each time;
-    the batch-statistics output is identical)."""
-    pf = pos_feat(ef.pos_feat, pos)
-    if ef.pos_feat.training:
-        with torch.no_grad():
-            for _ in range(n_calls - 1):
-                pos_feat(ef.pos_feat, pos)
+    The reference runs pos_feat once per call: its batch-statistics output is the same each time
+    and its BatchNorm running statistics advance each time, so it runs once here with n_calls
+    running-statistics updates."""
+    pf = pos_feat(ef.pos_feat, pos, n_calls)
     rep = lambda t: t.repeat(n_calls, 1)
     y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1).to(train_dtype())
     return hip_add_layernorm(embs, y, ef.norm)
@@ -138,13 +164,17 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     # attention-probability dropout (attention.py:28-29), counter-based mask shared with the backward
     att = hip_attention(qkv, nseq, L, a.heads, a.dims, a.dropout.p if training else 0.0)
     o = hip_linear(att, a.output_layer.weight, a.output_layer.bias).reshape(x.shape)
-    x = _drop(hip_add_layernorm(x, o, blk.input_sublayer.norm), p, training)
+    # the dropouts around the norms are fused into the LayerNorm kernels: SublayerConnection's
+    # dropout(norm(x + sublayer(x))) (sublayer.py:15-16) as the output dropout, FeedForward's
+    # final dropout (feed_forward.py:21) on the residual operand, and TransformerBlock's own
+    # dropout (transformer.py:35) folded into the output sublayer's: two independent keep masks
+    # in a row are one Bernoulli((1 - p)^2) mask scaled by 1 / (1 - p)^2
+    po = p if training else 0.0
+    x = hip_add_layernorm(x, o, blk.input_sublayer.norm, p_out=po)
     ff = blk.feed_forward
     h = F.leaky_relu(hip_linear(x, ff.w_1.weight, ff.w_1.bias), 0.1)
-    f = _drop(F.leaky_relu(hip_linear(hip_add_layernorm(h, None, ff.norm), ff.w_2.weight, ff.w_2.bias), 0.1),
-              p, training)
-    x = _drop(hip_add_layernorm(x, f, blk.output_sublayer.norm), p, training)
-    return _drop(x, p, training)
+    f = F.leaky_relu(hip_linear(hip_add_layernorm(h, None, ff.norm), ff.w_2.weight, ff.w_2.bias), 0.1)
+    return hip_add_layernorm(x, f, blk.output_sublayer.norm, p_r=po, p_out=1.0 - (1.0 - po) ** 2)
 
 
 @dataclass

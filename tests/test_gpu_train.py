@@ -187,6 +187,57 @@ def test_linear_dw_kernel_vs_fp32(M, N, K_, splits):
     assert (db.double() - ref_b).abs().max().item() < tol
     dw2, none = K.linear_dw(dy, x)
     assert none is None and (dw2.double() - ref_w).abs().max().item() < tol
+    if N % 256 == 0:
+        # a column slice of dy (strided rows), accumulated onto existing values (a .grad buffer)
+        h = N // 2
+        acc_w = torch.randn(N - h, K_, generator=g).to(DEV)
+        acc_b = torch.randn(N - h, generator=g).to(DEV)
+        want_w = acc_w.double() + ref_w[h:]
+        want_b = acc_b.double() + ref_b[h:]
+        K.linear_dw(dy[:, h:], x, dw=acc_w, db=acc_b, splits=splits)
+        assert (acc_w.double() - want_w).abs().max().item() < tol
+        assert (acc_b.double() - want_b).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("p_r,p_out", [(0.1, 0.19), (0.0, 0.1), (0.3, 0.0)])
+def test_layernorm_fused_dropout_vs_torch(p_r, p_out):
+    """drop_o(LN(x + drop_r(r))) with the masks fused into the LN kernels (csrc/train.hip) ==
+    torch on the same masks (tests/attn_helpers.py restates the hash): output, dx, dr, dg, db;
+    with direct_weight_grads the LN parameter gradients land in their .grad buffers (added)."""
+    from attn_helpers import ln_keep_mask
+    from src import autograd_ops as A
+    from src import kernels as K
+    M, N = 1031, 384
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16).requires_grad_(True)
+    r = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16).requires_grad_(True)
+    ln = torch.nn.LayerNorm(N).to(DEV)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    seed = 0x1234_5678_9ABC
+    gy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    y = A._HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, p_r, p_out, seed)
+    y.backward(gy)
+    mr = torch.from_numpy(ln_keep_mask(seed, 0, M, N, p_r)).to(DEV).float() / (1 - p_r)
+    mo = torch.from_numpy(ln_keep_mask(seed, 1, M, N, p_out)).to(DEV).float() / (1 - p_out)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    lr = torch.nn.LayerNorm(N).to(DEV)
+    lr.load_state_dict(ln.state_dict())
+    s = (xr + rr * mr).to(torch.bfloat16).float()          # the kernel keeps s in bf16
+    yr = lr(s) * mo
+    yr.backward(gy.float())
+    rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()
+    assert rel(y, yr.detach()) < 1e-2
+    assert rel(x.grad, xr.grad) < 2e-2 and rel(r.grad, rr.grad) < 2e-2
+    assert rel(ln.weight.grad, lr.weight.grad) < 1e-2 and rel(ln.bias.grad, lr.bias.grad) < 1e-2
+    # direct accumulation into the parameters' .grad
+    w0, b0 = ln.weight.grad.clone(), ln.bias.grad.clone()
+    with A.direct_weight_grads():
+        A._HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, p_r, p_out, seed).backward(gy)
+    torch.testing.assert_close(ln.weight.grad, 2 * w0, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(ln.bias.grad, 2 * b0, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,N,resid", [(1000, 384, True), (517, 1536, False), (64, 64, True)])
@@ -391,6 +442,7 @@ def test_train_gradients_f32_mode_vs_reference_autograd():
             assert got.norm().item() <= 2 * rn + 1e-6 * gnorm_all, name
             continue
         rel = ((got - ref).norm() / rn).item()
+        print(f"{name:60s} rel {rel:.2e} |ref| {rn:.3e}")
         worst = max(worst, (rel, name))
         checked += 1
     assert worst[0] <= 1e-3, worst
@@ -685,3 +737,48 @@ def test_train_entry_point_save_best_and_resume(tmp_path, capsys):
     with open(mcsv) as f:
         rows2 = list(csv.DictReader(f))
     assert [(r["epoch"], r["mode"]) for r in rows2[4:]] == [("2", "train"), ("2", "val")]
+
+
+def test_direct_weight_grads_match_autograd_accumulation():
+    """autograd_ops.direct_weight_grads (the trainer's backward): Linear dW / db accumulated by
+    the dW kernel straight into the FlatParams gradient buffer equal autograd's own
+    accumulation of the returned gradients, including a second micro-batch on top of the first
+    (gradient accumulation) and the GradBucketer readiness callbacks."""
+    from src import autograd_ops as A
+    from src.main.optimizer import FlatParams
+    from src.model import build_model
+    g = load_golden("train_tiny")
+    torch.manual_seed(3)
+    m = build_model(g["cfg"]["vocab"], 128, 1, 2, dropout=0.0).to(DEV).train()   # D % 128 == 0
+    x = _train_inputs(g)
+    B, L = x["hap_1"].shape
+    for k in ("rag_emb_h1", "rag_emb_h2"):
+        x[k] = torch.randn(B, 1, L, 128, device=DEV) * 0.5
+    fp = FlatParams(m.parameters())
+    seen = []
+    for p in fp.params:
+        p._snv_grad_ready = lambda t: seen.append(t)
+
+    def loss():
+        from src.autograd_ops import focal_loss
+        out = m(x)
+        mk = x["mask"].bool()
+        return 3 * focal_loss(out[0], x["hap_1_label"], mk, 2.0, 1.0) + 4 * focal_loss(out[2], x["gt_label"], mk, 2.0, 1.0)
+
+    fp.zero_grad()
+    loss().backward()
+    ref = fp.grad.clone()
+    assert not seen
+    fp.zero_grad()
+    with A.direct_weight_grads():
+        loss().backward()
+    got = fp.grad.clone()
+    assert len(seen) > 0
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 1e-5, rel
+    with A.direct_weight_grads():
+        loss().backward()
+    rel2 = ((fp.grad - 2 * ref).norm() / (2 * ref).norm()).item()
+    assert rel2 < 1e-5, rel2
+    for p in fp.params:
+        del p._snv_grad_ready

@@ -1,6 +1,7 @@
 """Host-side logic of the product package against the reference fixtures (CPU only)."""
 
 import json
+import math
 import re
 from pathlib import Path
 
@@ -141,3 +142,22 @@ def test_infer_geometry_matches_oracle():
         exp = data_np.infer_geometry(h1, h2, gt, mask, W, n_var, 1020)
         for a, b in zip(got, exp):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_attention_dropout_mask_statistics(p):
+    """The counter-based attention-dropout keep mask (csrc/attn_common.h, restated in
+    tests/attn_helpers.py) behaves like i.i.d. Bernoulli(1 - p): the drop rate, and no
+    dependence between the two keys of one hash, neighbouring queries, or heads."""
+    from attn_helpers import keep_mask
+    m = ~keep_mask(20240917, 2, 3, 1030, p)                  # dropped
+    n = m.size
+    assert abs(m.mean() - p) < 4 * math.sqrt(p * (1 - p) / n) + 2 ** -16
+    def cond(a, b):                                           # P(b dropped | a dropped)
+        return (a & b).sum() / max(a.sum(), 1)
+    tol = 6 * math.sqrt(p * (1 - p) / (n * p / 2))
+    assert abs(cond(m[..., 0::2], m[..., 1::2]) - p) < tol   # the two halves of one hash
+    assert abs(cond(m[..., :-1, :], m[..., 1:, :]) - p) < tol    # neighbouring queries
+    assert abs(cond(m[..., :, :-2], m[..., :, 2:]) - p) < tol    # neighbouring hashes
+    assert abs(cond(m[:, 0], m[:, 1]) - p) < tol               # heads
+    assert abs(cond(m[0], m[1]) - p) < tol                     # sequences

@@ -140,3 +140,37 @@ def test_trainer_metric_rows_and_early_stopping_match_reference(tmp_path):
     assert rows[0] == list(z["header"])
     np.testing.assert_array_equal(np.array(rows[1:]), z["rows"])
     assert stops == list(z["stops"]) and bests == list(z["is_best_before"])
+
+
+def test_pos_feat_batchnorm_matches_module_with_repeated_updates():
+    """train_forward._batchnorm (the pos_feat BatchNorms in torch ops) == nn.BatchNorm1d in
+    train mode: output, input / affine gradients (f64), and the running statistics after n
+    reference calls on the same batch; eval mode uses the running statistics."""
+    import copy
+    from src.train_forward import _batchnorm
+    torch.manual_seed(0)
+    bn = torch.nn.BatchNorm1d(4).double()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = copy.deepcopy(bn)
+    x = (torch.randn(2, 4, 1030, dtype=torch.float64) * 3 + 1).requires_grad_(True)
+    xr = x.detach().clone().requires_grad_(True)
+    g = torch.randn(2, 4, 1030, dtype=torch.float64)
+    y = _batchnorm(bn, x, n_updates=4)
+    yr = ref(xr)
+    for _ in range(3):
+        with torch.no_grad():
+            ref(xr)
+    torch.testing.assert_close(y, yr, rtol=1e-12, atol=1e-12)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-12, atol=1e-14)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-12, atol=1e-14)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 4
+    bn.eval()
+    ref.eval()
+    torch.testing.assert_close(_batchnorm(bn, x.detach()), ref(x.detach()), rtol=1e-12, atol=1e-12)

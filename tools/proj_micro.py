@@ -60,5 +60,12 @@ for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, o
     env("SNVRAG_SG_WAVES4", e) if e else None
     ms = timeit(fn)
     print(f"{name:18s} {ms:.4f} ms  {f / ms / 1e9:.1f} TFLOP/s", flush=True)
+for dz in ("0", "10000", "20000", "30000"):
+    env("SNVRAG_SG_DESYNC", dz)
+    ms = timeit(lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out))
+    print(f"sgemm desync {dz:6s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
+    ms = timeit(lambda: K.sgemm(x, sg4, 4 * D, sv4, act=1, out=out4))
+    print(f"gelu 4D desync {dz:6s} {ms:.4f} ms  {fl * 4 / 3 / ms / 1e9:.1f} TFLOP/s", flush=True)
+env("SNVRAG_SG_DESYNC", None)
 # the wave-count switch is read once per process: run again with SNVRAG_SG_WAVES4=1 for 4 waves
 print("(4-wave variant)" if os.environ.get("SNVRAG_SG_WAVES4") else "(8-wave variant)", flush=True)

@@ -31,5 +31,11 @@ for s in ${STEPS:-new ab gpu smoke bench}; do
     pmc)   step attn_pmc 300 env TAG=${ATAG:-attn} bash tools/pmc_attn.sh ;;
     knn)   step knn_probe 300 python tools/knn_probe.py ;;
     tail)  step tail_micro 300 python tools/tail_micro.py ;;
+    proj)  step proj_micro 300 python tools/proj_micro.py ;;
+    tattn) step train_attn_micro 300 python tools/train_attn_micro.py ;;
+    train) step train_only 300 python tools/train_only.py
+           step train_prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_train -o run -- python3 tools/train_only.py
+           rm -f $OUT/prof_train/*/*.db $OUT/prof_train/*.db
+           python3 tools/prof_top.py $OUT/prof_train 40 ;;
   esac
 done

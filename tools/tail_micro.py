@@ -71,18 +71,30 @@ ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
 xs = c["x"].clone()
 out = torch.empty_like(c["x"])
 fl9, fl8 = 18.0 * M * D * D, 16.0 * M * D * D
-def tail_var(v):
+def tail_var(v, desync=-1):
     def fn():
         os.environ["SNVRAG_TAIL_VARIANT"] = str(v)
+        if desync < 0:
+            os.environ.pop("SNVRAG_TAIL_DESYNC", None)         # the library default
+        else:
+            os.environ["SNVRAG_TAIL_DESYNC"] = str(desync)
         K.tail_forward(c["att"], xs, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
     return fn
 
 
+for _ in range(30):                                  # clock warm-up before the first timing
+    tail_var(0)()
 for name, fn, fl in (
         ("tail.hip PRE", tail_var(0), fl9),
+        ("tail.hip PRE residual at group 3", tail_var(5), fl9),
         ("tail.hip PRE PF=8", tail_var(1), fl9),
         ("tail.hip PRE no-DMA (diag)", tail_var(2), fl9),
         ("tail.hip PRE no sched groups", tail_var(3), fl9),
+        ("tail.hip PRE (again)", tail_var(0), fl9),
+        ("tail.hip PRE no desync", tail_var(0, 0), fl9),
+        ("tail.hip PRE desync 12k", tail_var(0, 12000), fl9),
+        ("tail.hip PRE desync 25k", tail_var(0, 25000), fl9),
+        ("tail.hip PRE desync 40k", tail_var(0, 40000), fl9),
         ("tail.hip FFN only", lambda: (os.environ.__setitem__("SNVRAG_TAIL_VARIANT", "0"),
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
     ms = timeit(fn)
@@ -97,7 +109,7 @@ st = torch.zeros(nwg * 4 * 10, dtype=torch.int64, device=dev)
 N.lib().snvrag_tail_stamps(st.data_ptr())
 for _ in range(20):                                  # warm the clock up on the default kernel
     tail_var(0)()
-tail_var(4)()
+tail_var(4, int(os.environ.get("TM_DESYNC", "-1")))()
 torch.cuda.synchronize()
 N.lib().snvrag_tail_stamps(None)
 os.environ["SNVRAG_TAIL_VARIANT"] = "0"
