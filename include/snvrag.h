@@ -442,6 +442,13 @@ int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, void* ws, si
 int snvrag_dw_splits(int64_t M, int64_t N, int64_t K);
 int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x, int64_t ldx,
                      float* dw, float* db, int splits, void* stream);
+/* The same over a fused output of n_parts equal parts (the q/k/v Linear layers of one N = 3D
+ * GEMM, multi_head_attention.py:44): part i's dW rows / db entries accumulate into
+ * dw_parts[i] [N / n_parts, K] / db_parts[i] (host arrays of device pointers; db_parts nullable).
+ * 1 <= n_parts <= 4, (N / n_parts) % 128 == 0. */
+int snvrag_linear_dw_parts(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x,
+                           int64_t ldx, int n_parts, float* const* dw_parts, float* const* db_parts, int splits,
+                           void* stream);
 
 /* Inference post-processing (replaces infer_embedding_rag.py:145-152): probs_h1/h2 [M, 2]
  * f32 head probabilities -> p1, p2 [M] = softmax(probs)[..., 1] (the reference's second

@@ -21,6 +21,7 @@
 #include "attn_common.h"
 
 #include <cmath>
+#include <utility>
 
 namespace snvrag {
 
@@ -175,21 +176,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq(int L, int H, const bf16* __r
     bf16x8 dsb[2];
     // hash input of (q, key pair (64 t + 4 lg) / 2); (kt, r) adds 8 kt + r / 2
     const uint32_t drow = drop_row(dbase, (uint32_t)q, (uint32_t)(32 * t + 2 * lg));
+    // straight-line element math (raw v_exp_f32, no per-element branches); only the ragged
+    // last key tile masks keys >= L
+    auto elem = [&](auto mask_tag) {
+      constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        float dm[2] = {1.f, 1.f};
-        if (drop.thresh) drop_split(drop, drop_mix24(drow + (uint32_t)(8 * kt + (r >> 1)) * DROP_C2), dm[0], dm[1]);
+        for (int r = 0; r < 4; r += 2) {
+          float dm[2] = {1.f, 1.f};
+          if (drop.thresh) drop_split(drop, drop_mix24(drow + (uint32_t)(8 * kt + (r >> 1)) * DROP_C2), dm[0], dm[1]);
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int key = t * 64 + 16 * kt + 4 * lg + r + e;
-          const float p = key < L ? exp2f(s[kt][r + e] * c_log2e - lse_q) : 0.f;
-          // dropout: dP = (dO V^T) o mask / (1 - p); D_q = rowsum(dO o O) is unchanged (O = P' V)
-          const float dpv = dp[kt][r + e] * dm[e];
-          dsb[kt >> 1][(kt & 1) * 4 + r + e] = (bf16)(p * (dpv - dq_));
+          for (int e = 0; e < 2; ++e) {
+            float p = __builtin_amdgcn_exp2f(s[kt][r + e] * c_log2e - lse_q);
+            if constexpr (MASK) p = t * 64 + 16 * kt + 4 * lg + r + e < L ? p : 0.f;
+            // dropout: dP = (dO V^T) o mask / (1 - p); D_q = rowsum(dO o O) is unchanged (O = P' V)
+            const float dpv = dp[kt][r + e] * dm[e];
+            dsb[kt >> 1][(kt & 1) * 4 + r + e] = (bf16)(p * (dpv - dq_));
+          }
         }
-      }
+    };
+    if ((t + 1) * 64 <= L) elem(std::false_type{});
+    else elem(std::true_type{});
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -304,17 +312,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv(int L, int H, const bf16* __
           mkv[qt][2 + rr] = (odd ? h_hi >> 16 : h_hi & 0xFFFFu) >= drop.thresh ? drop.scale : 0.f;
         }
     }
+    // straight-line element math (raw v_exp_f32); only the ragged last query tile masks q >= L
+    auto elem = [&](auto mask_tag) {
+      constexpr bool MASK = decltype(mask_tag)::value;
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
+      for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * qt + 4 * lg + r;
-        const float p = (t * 64 + ql < L) ? exp2f(s[qt][r] * c_log2e - ls[ql]) : 0.f;
-        // dropout: dV uses the kept, rescaled probabilities; dP is masked the same way
-        const float mk = drop.thresh ? mkv[qt][r] : 1.f;
-        pb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * mk);
-        dsb[qt >> 1][(qt & 1) * 4 + r] = (bf16)(p * (dp[qt][r] * mk - ls[64 + ql]));
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * qt + 4 * lg + r;
+          float p = __builtin_amdgcn_exp2f(s[qt][r] * c_log2e - ls[ql]);
+          if constexpr (MASK) p = t * 64 + ql < L ? p : 0.f;
+          // dropout: dV uses the kept, rescaled probabilities; dP is masked the same way
+          const float mk = drop.thresh ? mkv[qt][r] : 1.f;
+          const float pm = p * mk;
+          pb[qt >> 1][(qt & 1) * 4 + r] = (bf16)pm;
+          dsb[qt >> 1][(qt & 1) * 4 + r] = (bf16)fmaf(pm, dp[qt][r], -p * ls[64 + ql]);
+        }
+    };
+    if ((t + 1) * 64 <= L) elem(std::false_type{});
+    else elem(std::true_type{});
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll

@@ -36,13 +36,24 @@ __device__ __forceinline__ bf16x4 dw_tr(const char* p) {
 
 // grid: (N / 128, K / 128, S); 256 threads = 4 waves, wave (wn, wk) owns the 64 x 64 sub-tile
 // n0 + 64 wn, k0 + 64 wk (2 x 2 MFMA tiles of 32 x 32).
+// Output of the launch: dW rows (and db entries) n live in part n / seg of up to 4 separately
+// allocated buffers (the q/k/v weights of one fused N = 3D output), each [seg, K] / [seg].
+struct DwOut {
+  float* w[4];
+  float* b[4];
+  int seg;
+};
+
 __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16* __restrict__ dy, long ldy,
-                                                 const bf16* __restrict__ x, long ldx, float* __restrict__ dw,
-                                                 float* __restrict__ db, int chunk) {
+                                                 const bf16* __restrict__ x, long ldx, DwOut out, int chunk) {
   __shared__ __attribute__((aligned(16))) char smem[2 * DW_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
+  const int part = n0 / out.seg;                     // a 128-row tile lies in one part (seg % 128 == 0)
+  const int nbase = part * out.seg;                  // first n of the part
+  float* __restrict__ dw = out.w[part];
+  float* __restrict__ db = out.b[part];
   const int m_begin = blockIdx.z * chunk;
   const int m_end = min(M, m_begin + chunk);
   if (m_begin >= m_end) return;                      // whole workgroup, before any barrier
@@ -128,7 +139,7 @@ __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int nn = n0 + 64 * wn + 32 * a + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
-        unsafeAtomicAdd(dw + (long)nn * K + kk, acc[a][b][e]);
+        unsafeAtomicAdd(dw + (long)(nn - nbase) * K + kk, acc[a][b][e]);
       }
     }
   if (do_db) {
@@ -136,7 +147,7 @@ __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       const float v = dbs[a] + __shfl_xor(dbs[a], 32, 64);
-      if (lane < 32) unsafeAtomicAdd(db + n0 + 64 * wn + 32 * a + lane, v);
+      if (lane < 32) unsafeAtomicAdd(db + (n0 - nbase) + 64 * wn + 32 * a + lane, v);
     }
   }
 }
@@ -153,22 +164,50 @@ extern "C" int snvrag_dw_splits(int64_t M, int64_t N, int64_t K) {
   return (int)s;
 }
 
-extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x,
-                                int64_t ldx, float* dw, float* db, int splits, void* stream) {
-  SNV_CHECK_ARG(dy && x && dw, "null pointer");
-  SNV_CHECK_ARG(M >= 0 && N % DW_T == 0 && K % DW_T == 0 && N > 0 && K > 0, "N and K must be multiples of 128");
-  SNV_CHECK_ARG(ldy >= N && ldx >= K && ldy % 8 == 0 && ldx % 8 == 0, "leading dims: >= N / K, multiples of 8");
-  SNV_CHECK_ARG(((uintptr_t)dy % 16) == 0 && ((uintptr_t)x % 16) == 0, "operands must be 16-byte aligned");
-  hipStream_t s = as_stream(stream);
-  // dw / db are accumulated: the caller zeroes them (or passes a running sum)
+static int launch_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x, int64_t ldx,
+                     const DwOut& out, int splits, hipStream_t s) {
   if (M == 0) return 0;
   if (splits <= 0) splits = snvrag_dw_splits(M, N, K);
   const int chunk = (int)((((M + splits - 1) / splits) + DW_R - 1) / DW_R * DW_R);
   const int S = (int)((M + chunk - 1) / chunk);
   evlog_begin(s);
   hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
-                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, dw, db, chunk);
+                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
   SNV_LAUNCH_CHECK();
   evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
   return 0;
+}
+
+static int dw_check(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x, int64_t ldx) {
+  SNV_CHECK_ARG(dy && x, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && N % DW_T == 0 && K % DW_T == 0 && N > 0 && K > 0, "N and K must be multiples of 128");
+  SNV_CHECK_ARG(ldy >= N && ldx >= K && ldy % 8 == 0 && ldx % 8 == 0, "leading dims: >= N / K, multiples of 8");
+  SNV_CHECK_ARG(((uintptr_t)dy % 16) == 0 && ((uintptr_t)x % 16) == 0, "operands must be 16-byte aligned");
+  return 0;
+}
+
+extern "C" int snvrag_linear_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x,
+                                int64_t ldx, float* dw, float* db, int splits, void* stream) {
+  if (int rc = dw_check(M, N, K, dy, ldy, x, ldx)) return rc;
+  SNV_CHECK_ARG(dw, "null pointer");
+  // dw / db are accumulated: the caller zeroes them (or passes a running sum)
+  DwOut out{{dw, nullptr, nullptr, nullptr}, {db, nullptr, nullptr, nullptr}, (int)N};
+  return launch_dw(M, N, K, dy, ldy, x, ldx, out, splits, as_stream(stream));
+}
+
+extern "C" int snvrag_linear_dw_parts(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ldy, const void* x,
+                                      int64_t ldx, int n_parts, float* const* dw_parts, float* const* db_parts,
+                                      int splits, void* stream) {
+  if (int rc = dw_check(M, N, K, dy, ldy, x, ldx)) return rc;
+  SNV_CHECK_ARG(n_parts >= 1 && n_parts <= 4 && N % n_parts == 0 && (N / n_parts) % DW_T == 0,
+                "1-4 equal parts of N, each a multiple of 128");
+  SNV_CHECK_ARG(dw_parts, "null pointer");
+  DwOut out{{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}, (int)(N / n_parts)};
+  for (int i = 0; i < n_parts; ++i) {
+    SNV_CHECK_ARG(dw_parts[i], "null dW part");
+    out.w[i] = dw_parts[i];
+    out.b[i] = db_parts ? db_parts[i] : nullptr;
+    SNV_CHECK_ARG(!db_parts || db_parts[i], "null db part");
+  }
+  return launch_dw(M, N, K, dy, ldy, x, ldx, out, splits, as_stream(stream));
 }

@@ -36,6 +36,58 @@ __device__ __forceinline__ int gcd_u(int a, int b) {   // a, b >= 0; gcd(0, b) =
 }
 
 // ------------------------------------------------------------------- LUT ---
+// General-path Delta (query offsets A_q and/or panel offsets A_r: every position's squared
+// distances need their own D-length reductions) spread over (position chunk of 64, query)
+// workgroups: lut_kernel alone ran one workgroup per query, i.e. nq of 256 CUs at training's
+// 48 queries (1.15 ms per step).  delta [nq][n_sites_pad] (sites), cpart [nq][nch]: the chunk's
+// sum of the constant-term contributions (4 wave partials in fixed order: deterministic).
+constexpr int LUT_CH = 64;
+__host__ __device__ inline int lut_nch_max(int n_sites_pad) { return n_sites_pad / LUT_CH + 4; }
+
+__global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int64_t* __restrict__ tok_q,
+                                                        const float* __restrict__ W, const float* __restrict__ Aq,
+                                                        long aq_period, const float* __restrict__ Ar,
+                                                        const uint8_t* __restrict__ site_mask, int n_sites,
+                                                        int n_sites_pad, int tok0, int tok1, int mask_tok,
+                                                        float* __restrict__ delta, float* __restrict__ cpart) {
+  const int c = blockIdx.x, q = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = lut_nch_max(n_sites_pad);
+  const long arow = Aq ? ((aq_period > 0 ? q % aq_period : q) * (long)L) : 0;
+  __shared__ float wc[4];
+  float cacc = 0.f;
+  for (int i = 0; i < LUT_CH / 4; ++i) {
+    const int l = c * LUT_CH + 4 * i + wave;
+    if (l >= L) break;
+    const int t = (int)tok_q[(long)q * L + l];
+    const bool is_site = l >= 1 && l <= n_sites;
+    const bool varying = is_site && !site_mask[l - 1];
+    int rt;                                        // panel token at l when not varying
+    if (l == 0) rt = 2; else if (is_site) rt = mask_tok; else if (l == n_sites + 1) rt = 3; else rt = 0;
+    float t0 = 0.f, t1 = 0.f, tc = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float u = W[(long)t * D + d];
+      if (Aq) u += Aq[(arow + l) * D + d];
+      if (Ar) u -= Ar[(long)l * D + d];
+      if (varying) {
+        const float a = u - W[(long)tok0 * D + d], b = u - W[(long)tok1 * D + d];
+        t0 = fmaf(a, a, t0);
+        t1 = fmaf(b, b, t1);
+      } else {
+        const float cc = u - W[(long)rt * D + d];
+        tc = fmaf(cc, cc, tc);
+      }
+    }
+    t0 = wave_sum(t0); t1 = wave_sum(t1); tc = wave_sum(tc);
+    if (lane == 0) {
+      if (is_site) delta[(long)q * n_sites_pad + l - 1] = varying ? (t1 - t0) : 0.f;
+      cacc += varying ? t0 : tc;
+    }
+  }
+  if (lane == 0) wc[wave] = cacc;
+  __syncthreads();
+  if (threadIdx.x == 0) cpart[(long)q * nch + c] = (wc[0] + wc[1]) + (wc[2] + wc[3]);
+}
+
 // One workgroup per query.  Positions l = 0..L-1 contribute to the constant
 // C_q; unmasked sites s (l = s + 1) contribute Delta_q[s].
 __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* __restrict__ tok_q,
@@ -44,11 +96,11 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
                                                   const uint8_t* __restrict__ site_mask, int n_sites,
                                                   int n_sites_pad, int nq, int tok0, int tok1, int mask_tok,
                                                   int limbs, int8_t* __restrict__ lut, int* __restrict__ exps,
-                                                  float* __restrict__ consts) {
+                                                  float* __restrict__ consts, const float* __restrict__ gdelta,
+                                                  const float* __restrict__ gcpart) {
   extern __shared__ float sdelta[];              // [n_sites_pad] + [4] scratch
   float* red = sdelta + n_sites_pad;
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long arow = Aq ? ((aq_period > 0 ? q % aq_period : q) * (long)L) : 0;
   float cacc = 0.f;
   // Without AF terms u = W[t]: every squared distance depends on (token, panel token)
   // only, so the block tabulates them once (same lane order and wave_sum as the
@@ -90,7 +142,16 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
       if (lane == 0) cacc = cpart;
     }
   }
-  for (int l = wave; l < L && !done; l += 4) {
+  if (!fast) {
+    // general path: Delta and the constant's chunk sums from lut_delta_kernel
+    for (int s = tid; s < n_sites; s += 256) sdelta[s] = gdelta[(long)q * n_sites_pad + s];
+    if (tid == 0) {
+      const int nch = (L + LUT_CH - 1) / LUT_CH, stride = lut_nch_max(n_sites_pad);
+      for (int c = 0; c < nch; ++c) cacc += gcpart[(long)q * stride + c];
+    }
+  }
+  // no offsets but a token outside the tabulated range: the per-position loop
+  for (int l = wave; l < L && fast && !done; l += 4) {
     const int t = (int)tok_q[(long)q * L + l];
     const bool is_site = l >= 1 && l <= n_sites;
     const bool varying = is_site && !site_mask[l - 1];
@@ -98,9 +159,7 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
     if (l == 0) rt = 2; else if (is_site) rt = mask_tok; else if (l == n_sites + 1) rt = 3; else rt = 0;
     float t0 = 0.f, t1 = 0.f, tc = 0.f;
     for (int d = lane; d < D; d += 64) {
-      float u = W[(long)t * D + d];
-      if (Aq) u += Aq[(arow + l) * D + d];
-      if (Ar) u -= Ar[(long)l * D + d];
+      const float u = W[(long)t * D + d];
       if (varying) {
         const float a = u - W[(long)tok0 * D + d], b = u - W[(long)tok1 * D + d];
         t0 = fmaf(a, a, t0);
@@ -840,10 +899,16 @@ using namespace snvrag;
 static size_t lut_tail_offset(int64_t nq, int32_t n_sites_pad) {
   return (size_t)((nq + 15) / 16) * 3 * (n_sites_pad / 64) * 1024;
 }
-extern "C" size_t snvrag_knn_lut_bytes(int64_t nq, int32_t n_sites_pad, int limbs) {
+static size_t lut_ws_offset(int64_t nq, int32_t n_sites_pad, int limbs) {
   const size_t main = (size_t)((nq + 15) / 16) * limbs * (n_sites_pad / 64) * 64 * 16;
-  if (limbs != 2) return main;
-  return lut_tail_offset(nq, n_sites_pad) + (size_t)((nq + 15) / 16) * 16 * 4 + 16;
+  const size_t end = limbs != 2 ? main : lut_tail_offset(nq, n_sites_pad) + (size_t)((nq + 15) / 16) * 16 * 4 + 16;
+  return (end + 255) / 256 * 256;
+}
+
+// the LUT, then (256-B aligned) the general-path workspace: delta [nq][n_sites_pad] f32 and the
+// constant's chunk sums [nq][lut_nch_max] f32
+extern "C" size_t snvrag_knn_lut_bytes(int64_t nq, int32_t n_sites_pad, int limbs) {
+  return lut_ws_offset(nq, n_sites_pad, limbs) + (size_t)nq * (n_sites_pad + lut_nch_max(n_sites_pad)) * 4;
 }
 
 extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
@@ -861,9 +926,18 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
     char* tail = (char*)lut_out + lut_tail_offset(nq, n_sites_pad);
     SNV_HIP(hipMemsetAsync(tail, 0, (size_t)((nq + 15) / 16) * 16 * 4 + 16, s));
   }
+  float* gdelta = (float*)((char*)lut_out + lut_ws_offset(nq, n_sites_pad, limbs));
+  float* gcpart = gdelta + (size_t)nq * n_sites_pad;
+  if (Aq || Ar) {
+    SNV_CHECK_ARG(L <= (int64_t)LUT_CH * lut_nch_max(n_sites_pad), "sequence longer than the padded window + 256");
+    hipLaunchKernelGGL(lut_delta_kernel, dim3((unsigned)((L + LUT_CH - 1) / LUT_CH), (unsigned)nq), dim3(256), 0, s,
+                       (int)L, (int)D, tok_q, W, Aq, (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0,
+                       tok1, mask_tok, gdelta, gcpart);
+    SNV_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(lut_kernel, dim3((unsigned)nq), dim3(256), sh, s, (int)L, (int)D, tok_q, W, Aq,
                      (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, (int)nq, tok0, tok1, mask_tok,
-                     limbs, (int8_t*)lut_out, exp_out, const_out);
+                     limbs, (int8_t*)lut_out, exp_out, const_out, gdelta, gcpart);
   SNV_LAUNCH_CHECK();
   if (nq % 16)
     hipLaunchKernelGGL(lut_zero_pad_kernel, dim3(64), dim3(256), 0, s, (int8_t*)lut_out, (int)nq,

@@ -651,8 +651,11 @@ __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w,
 template <int D, int EPI, int ACT, bool RANK, int WAVES = 4, bool CAT = false>
 static int sg_launch(SgArgs a, hipStream_t s) {
   auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES, CAT>;
+  // first-round phase step (tail.hip's de-synchronised rounds): 10 k cycles for the 8-wave
+  // projections (QKV at M = 527 360: 0.559 -> 0.540 ms; 20 k / 30 k: 0.557 / 0.584,
+  // tools/proj_micro.py); SNVRAG_SG_DESYNC overrides
   const char* dz = getenv("SNVRAG_SG_DESYNC");
-  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 && dz ? atoi(dz) : 0;
+  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 ? (dz ? atoi(dz) : (WAVES == 8 ? 10000 : 0)) : 0;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

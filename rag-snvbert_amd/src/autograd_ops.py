@@ -223,7 +223,7 @@ def direct_weight_grads(enabled: bool = True):
 
 
 def _grad_buffer(p) -> Optional[torch.Tensor]:
-    g = p.grad if (p is not None and p.requires_grad) else None
+    g = p.grad if (p is not None and p.is_leaf and p.requires_grad) else None
     return g if (g is not None and g.dtype == torch.float32 and g.is_contiguous()) else None
 
 
@@ -306,10 +306,15 @@ class _HipLinear(torch.autograd.Function):
                 (not ctx.has_bias or all(_grad_buffer(b) is not None for b in pbs)):
             # accumulate into the flat gradient buffer: one dW launch per weight (its column
             # slice of dy), bias sums fused
-            off = 0
-            for w, b, sz in zip(pws, pbs, sizes):
-                K.linear_dw(g2[:, off:off + sz], x2, dw=w.grad, db=b.grad if ctx.has_bias else None)
-                off += sz
+            if ctx.n == 1:
+                K.linear_dw(g2, x2, dw=pws[0].grad, db=pbs[0].grad if ctx.has_bias else None)
+            elif len(set(sizes)) == 1 and ctx.n <= 4:
+                K.linear_dw_parts(g2, x2, [w.grad for w in pws], [b.grad for b in pbs] if ctx.has_bias else None)
+            else:
+                off = 0
+                for w, b, sz in zip(pws, pbs, sizes):
+                    K.linear_dw(g2[:, off:off + sz], x2, dw=w.grad, db=b.grad if ctx.has_bias else None)
+                    off += sz
             for t in list(pws) + (list(pbs) if ctx.has_bias else []):
                 _grad_ready(t)
             return (gx, None, *([None] * ctx.n), *([None] * ctx.n))

@@ -608,6 +608,28 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, bias: bool = False, splits: int
     return dw, db
 
 
+def linear_dw_parts(dy: torch.Tensor, x: torch.Tensor, dws, dbs=None, splits: int = 0) -> None:
+    """dws[i] f32 [N / n, K] += dy[:, i N/n : (i+1) N/n]^T x (and dbs[i] += its column sums) in ONE
+    launch over the fused output (csrc/dw.hip, snvrag_linear_dw_parts): the q/k/v weights'
+    gradient buffers of one N = 3D projection."""
+    N.require_gpu(dy, x)
+    assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dy.shape[0] == x.shape[0]
+    assert dy.stride(1) == 1 and x.stride(1) == 1
+    M, Nn = dy.shape
+    Kk = x.shape[1]
+    n = len(dws)
+    for t in dws:
+        assert t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == (Nn // n, Kk)
+    if dbs is not None:
+        for t in dbs:
+            assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == Nn // n
+    import ctypes
+    wp = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dws])
+    bp = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dbs]) if dbs is not None else None
+    check(N.lib().snvrag_linear_dw_parts(M, Nn, Kk, ptr(dy), dy.stride(0), ptr(x), x.stride(0), n, wp, bp,
+                                         int(splits), stream_ptr()), "linear_dw_parts")
+
+
 def colsum(x: torch.Tensor) -> torch.Tensor:
     """f32 column sums of a bf16 matrix [..., N] (bias gradients)."""
     Nn = x.shape[-1]

@@ -149,6 +149,8 @@ _SIGS = {
     "snvrag_colsum_bf16": ([i64, C.c_int, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_dw_splits": ([i64, i64, i64], C.c_int),
     "snvrag_linear_dw": ([i64, i64, i64, vp, i64, vp, i64, vp, vp, C.c_int, vp], C.c_int),
+    "snvrag_linear_dw_parts": ([i64, i64, i64, vp, i64, vp, i64, C.c_int, C.POINTER(vp), C.POINTER(vp), C.c_int, vp],
+                               C.c_int),
     "snvrag_evlog_enable": ([C.c_int], C.c_int),
     "snvrag_evlog_pause": ([C.c_int], C.c_int),
     "snvrag_evlog_reset": ([], C.c_int),

@@ -187,6 +187,13 @@ def test_linear_dw_kernel_vs_fp32(M, N, K_, splits):
     assert (db.double() - ref_b).abs().max().item() < tol
     dw2, none = K.linear_dw(dy, x)
     assert none is None and (dw2.double() - ref_w).abs().max().item() < tol
+    if N % 384 == 0:
+        # one launch over three equal parts with separate (accumulated) output buffers
+        parts_w = [torch.ones(N // 3, K_, device=DEV) for _ in range(3)]
+        parts_b = [torch.ones(N // 3, device=DEV) for _ in range(3)]
+        K.linear_dw_parts(dy, x, parts_w, parts_b)
+        assert (torch.cat(parts_w).double() - 1 - ref_w).abs().max().item() < tol
+        assert (torch.cat(parts_b).double() - 1 - ref_b).abs().max().item() < tol
     if N % 256 == 0:
         # a column slice of dy (strided rows), accumulated onto existing values (a .grad buffer)
         h = N // 2
@@ -768,17 +775,55 @@ def test_direct_weight_grads_match_autograd_accumulation():
     fp.zero_grad()
     loss().backward()
     ref = fp.grad.clone()
+    fp.zero_grad()
+    loss().backward()
+    floor = ((fp.grad - ref).norm() / ref.norm()).item()   # run-to-run (float atomics)
     assert not seen
     fp.zero_grad()
     with A.direct_weight_grads():
         loss().backward()
     got = fp.grad.clone()
     assert len(seen) > 0
+    names = {id(p): n for n, p in m.named_parameters()}
+    worst = sorted(((((fp.view(got, i) - fp.view(ref, i)).norm() / (fp.view(ref, i).norm() + 1e-30)).item(),
+                     names[id(p)]) for i, p in enumerate(fp.params)), reverse=True)[:8]
     rel = ((got - ref).norm() / ref.norm()).item()
-    assert rel < 1e-5, rel
+    assert rel < 1e-5 + 10 * floor, (rel, floor, worst)
     with A.direct_weight_grads():
         loss().backward()
     rel2 = ((fp.grad - 2 * ref).norm() / (2 * ref).norm()).item()
     assert rel2 < 1e-5, rel2
     for p in fp.params:
         del p._snv_grad_ready
+
+
+def test_stream_gemm_repacks_after_optimizer_step():
+    """The K = 384 stream-GEMM weight packs (autograd_ops._sg_stream / _sg_stream_t: forward and
+    dX) are cached per parameter version and optimizer epoch: after a FusedAdam step on the flat
+    buffer (a HIP kernel, outside torch's version counter) the next forward and backward use the
+    updated weights, not the stale packs."""
+    from src.autograd_ops import hip_linear
+    from src.main.optimizer import FlatParams, FusedAdam
+    torch.manual_seed(7)
+    lin = torch.nn.Linear(384, 384).to(DEV)
+    fp = FlatParams(lin.parameters())
+    opt = FusedAdam(fp, lr=0.05)
+    x = torch.randn(2048, 384, device=DEV).to(torch.bfloat16).requires_grad_(True)
+
+    def check():
+        x.grad = None
+        y = hip_linear(x, lin.weight, lin.bias)
+        w = lin.weight.detach().to(torch.bfloat16).float()
+        ref = x.detach().float() @ w.t() + lin.bias.detach()
+        assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+        g = torch.randn_like(y)
+        y.backward(g)
+        gx_ref = g.float() @ w
+        assert ((x.grad.float() - gx_ref).norm() / gx_ref.norm()).item() < 1e-2
+
+    check()
+    before = lin.weight.detach().clone()
+    fp.grad.normal_()
+    opt.step()
+    assert (lin.weight.detach() - before).abs().max().item() > 1e-3     # the weights moved
+    check()

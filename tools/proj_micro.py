@@ -60,7 +60,7 @@ for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, o
     env("SNVRAG_SG_WAVES4", e) if e else None
     ms = timeit(fn)
     print(f"{name:18s} {ms:.4f} ms  {f / ms / 1e9:.1f} TFLOP/s", flush=True)
-for dz in ("0", "10000", "20000", "30000"):
+for dz in ("0", "5000", "10000", "15000"):
     env("SNVRAG_SG_DESYNC", dz)
     ms = timeit(lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out))
     print(f"sgemm desync {dz:6s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)

@@ -33,6 +33,7 @@ for s in ${STEPS:-new ab gpu smoke bench}; do
     tail)  step tail_micro 300 python tools/tail_micro.py ;;
     proj)  step proj_micro 300 python tools/proj_micro.py ;;
     tattn) step train_attn_micro 300 python tools/train_attn_micro.py ;;
+    exp)   step exp_rate 120 ./tools/micro/exp_rate ;;
     train) step train_only 300 python tools/train_only.py
            step train_prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_train -o run -- python3 tools/train_only.py
            rm -f $OUT/prof_train/*/*.db $OUT/prof_train/*.db
