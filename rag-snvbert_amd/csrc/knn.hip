@@ -55,9 +55,10 @@ __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int6
   const long arow = Aq ? ((aq_period > 0 ? q % aq_period : q) * (long)L) : 0;
   __shared__ float wc[4];
   float cacc = 0.f;
-  for (int i = 0; i < LUT_CH / 4; ++i) {
-    const int l = c * LUT_CH + 4 * i + wave;
-    if (l >= L) break;
+  // the last chunk also takes every position past the grid (padding tokens of a sequence longer
+  // than the window: constant-term contributions only), so the grid is capped at nch
+  const int lend = c == (int)gridDim.x - 1 ? L : min(L, (c + 1) * LUT_CH);
+  for (int l = c * LUT_CH + wave; l < lend; l += 4) {
     const int t = (int)tok_q[(long)q * L + l];
     const bool is_site = l >= 1 && l <= n_sites;
     const bool varying = is_site && !site_mask[l - 1];
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
     // general path: Delta and the constant's chunk sums from lut_delta_kernel
     for (int s = tid; s < n_sites; s += 256) sdelta[s] = gdelta[(long)q * n_sites_pad + s];
     if (tid == 0) {
-      const int nch = (L + LUT_CH - 1) / LUT_CH, stride = lut_nch_max(n_sites_pad);
+      const int stride = lut_nch_max(n_sites_pad), nch = min((L + LUT_CH - 1) / LUT_CH, stride);
       for (int c = 0; c < nch; ++c) cacc += gcpart[(long)q * stride + c];
     }
   }
@@ -929,8 +930,8 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
   float* gdelta = (float*)((char*)lut_out + lut_ws_offset(nq, n_sites_pad, limbs));
   float* gcpart = gdelta + (size_t)nq * n_sites_pad;
   if (Aq || Ar) {
-    SNV_CHECK_ARG(L <= (int64_t)LUT_CH * lut_nch_max(n_sites_pad), "sequence longer than the padded window + 256");
-    hipLaunchKernelGGL(lut_delta_kernel, dim3((unsigned)((L + LUT_CH - 1) / LUT_CH), (unsigned)nq), dim3(256), 0, s,
+    const int64_t nch = std::min<int64_t>((L + LUT_CH - 1) / LUT_CH, lut_nch_max(n_sites_pad));
+    hipLaunchKernelGGL(lut_delta_kernel, dim3((unsigned)nch, (unsigned)nq), dim3(256), 0, s,
                        (int)L, (int)D, tok_q, W, Aq, (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0,
                        tok1, mask_tok, gdelta, gcpart);
     SNV_LAUNCH_CHECK();

@@ -792,7 +792,9 @@ def test_direct_weight_grads_match_autograd_accumulation():
     with A.direct_weight_grads():
         loss().backward()
     rel2 = ((fp.grad - 2 * ref).norm() / (2 * ref).norm()).item()
-    assert rel2 < 1e-5, rel2
+    worst2 = sorted(((((fp.view(fp.grad, i) - 2 * fp.view(ref, i)).norm() / (2 * fp.view(ref, i).norm() + 1e-30)).item(),
+                      names[id(p)]) for i, p in enumerate(fp.params)), reverse=True)[:8]
+    assert rel2 < 1e-5 + 10 * floor, (rel2, floor, worst2)
     for p in fp.params:
         del p._snv_grad_ready
 
