@@ -185,6 +185,16 @@ int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const
                    const uint8_t* site_mask, int32_t n_sites, int32_t n_sites_pad,
                    int tok0, int tok1, int mask_tok, int limbs,
                    void* lut_out, int32_t* exp_out, float* const_out, void* stream);
+/* The same LUT with the PANEL side's token table Wp separate from the query side's W:
+ * Delta_q[s] = ||u - Wp[tok1]||^2 - ||u - Wp[tok0]||^2, u = W[tok_q[s+1]] + Aq - Ar.  The
+ * reference caches a window's panel embeddings once per window visit and keeps searching them
+ * while the weights train (embedding_rag_dataset.py:334-377, jit_cache_win_idx); Wp / Ar are
+ * then the snapshot taken when that window's cache was built, W / Aq the current weights. */
+int snvrag_knn_lut_panel(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
+                         const float* Wp, const float* Aq, int64_t aq_period, const float* Ar,
+                         const uint8_t* site_mask, int32_t n_sites, int32_t n_sites_pad,
+                         int tok0, int tok1, int mask_tok, int limbs,
+                         void* lut_out, int32_t* exp_out, float* const_out, void* stream);
 
 /* Scan: every block scans a contiguous range of the panel and keeps an exact
  * per-query top-k (k <= 32) of its range; partial lists (ascending uint64 keys

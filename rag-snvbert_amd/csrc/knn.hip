@@ -45,7 +45,8 @@ constexpr int LUT_CH = 64;
 __host__ __device__ inline int lut_nch_max(int n_sites_pad) { return n_sites_pad / LUT_CH + 4; }
 
 __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int64_t* __restrict__ tok_q,
-                                                        const float* __restrict__ W, const float* __restrict__ Aq,
+                                                        const float* __restrict__ W, const float* __restrict__ Wp,
+                                                        const float* __restrict__ Aq,
                                                         long aq_period, const float* __restrict__ Ar,
                                                         const uint8_t* __restrict__ site_mask, int n_sites,
                                                         int n_sites_pad, int tok0, int tok1, int mask_tok,
@@ -70,11 +71,11 @@ __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int6
       if (Aq) u += Aq[(arow + l) * D + d];
       if (Ar) u -= Ar[(long)l * D + d];
       if (varying) {
-        const float a = u - W[(long)tok0 * D + d], b = u - W[(long)tok1 * D + d];
+        const float a = u - Wp[(long)tok0 * D + d], b = u - Wp[(long)tok1 * D + d];
         t0 = fmaf(a, a, t0);
         t1 = fmaf(b, b, t1);
       } else {
-        const float cc = u - W[(long)rt * D + d];
+        const float cc = u - Wp[(long)rt * D + d];
         tc = fmaf(cc, cc, tc);
       }
     }
@@ -92,7 +93,8 @@ __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int6
 // One workgroup per query.  Positions l = 0..L-1 contribute to the constant
 // C_q; unmasked sites s (l = s + 1) contribute Delta_q[s].
 __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* __restrict__ tok_q,
-                                                  const float* __restrict__ W, const float* __restrict__ Aq,
+                                                  const float* __restrict__ W, const float* __restrict__ Wp,
+                                                  const float* __restrict__ Aq,
                                                   long aq_period, const float* __restrict__ Ar,
                                                   const uint8_t* __restrict__ site_mask, int n_sites,
                                                   int n_sites_pad, int nq, int tok0, int tok1, int mask_tok,
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
       float acc = 0.f;
       if (t < 7)
         for (int d = lane; d < D; d += 64) {
-          const float a = W[(long)t * D + d] - W[(long)rt * D + d];
+          const float a = W[(long)t * D + d] - Wp[(long)rt * D + d];
           acc = fmaf(a, a, acc);
         }
       acc = wave_sum(acc);
@@ -162,11 +164,11 @@ __global__ __launch_bounds__(256) void lut_kernel(int L, int D, const int64_t* _
     for (int d = lane; d < D; d += 64) {
       const float u = W[(long)t * D + d];
       if (varying) {
-        const float a = u - W[(long)tok0 * D + d], b = u - W[(long)tok1 * D + d];
+        const float a = u - Wp[(long)tok0 * D + d], b = u - Wp[(long)tok1 * D + d];
         t0 = fmaf(a, a, t0);
         t1 = fmaf(b, b, t1);
       } else {
-        const float c = u - W[(long)rt * D + d];
+        const float c = u - Wp[(long)rt * D + d];
         tc = fmaf(c, c, tc);
       }
     }
@@ -916,7 +918,16 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
                               const float* Aq, int64_t aq_period, const float* Ar, const uint8_t* site_mask,
                               int32_t n_sites, int32_t n_sites_pad, int tok0, int tok1, int mask_tok, int limbs,
                               void* lut_out, int32_t* exp_out, float* const_out, void* stream) {
-  SNV_CHECK_ARG(tok_q && W && site_mask && lut_out && exp_out, "null pointer");
+  return snvrag_knn_lut_panel(nq, L, D, tok_q, W, W, Aq, aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0, tok1,
+                              mask_tok, limbs, lut_out, exp_out, const_out, stream);
+}
+
+extern "C" int snvrag_knn_lut_panel(int64_t nq, int64_t L, int64_t D, const int64_t* tok_q, const float* W,
+                                    const float* Wp, const float* Aq, int64_t aq_period, const float* Ar,
+                                    const uint8_t* site_mask, int32_t n_sites, int32_t n_sites_pad, int tok0,
+                                    int tok1, int mask_tok, int limbs, void* lut_out, int32_t* exp_out,
+                                    float* const_out, void* stream) {
+  SNV_CHECK_ARG(tok_q && W && Wp && site_mask && lut_out && exp_out, "null pointer");
   SNV_CHECK_ARG(limbs == 1 || limbs == 2, "limbs must be 1 or 2");
   SNV_CHECK_ARG(n_sites_pad % 64 == 0 && n_sites_pad >= n_sites && n_sites + 2 <= L, "site padding");
   SNV_CHECK_ARG(n_sites_pad <= 20 * 64, "window longer than 1280 sites");
@@ -932,11 +943,11 @@ extern "C" int snvrag_knn_lut(int64_t nq, int64_t L, int64_t D, const int64_t* t
   if (Aq || Ar) {
     const int64_t nch = std::min<int64_t>((L + LUT_CH - 1) / LUT_CH, lut_nch_max(n_sites_pad));
     hipLaunchKernelGGL(lut_delta_kernel, dim3((unsigned)nch, (unsigned)nq), dim3(256), 0, s,
-                       (int)L, (int)D, tok_q, W, Aq, (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0,
+                       (int)L, (int)D, tok_q, W, Wp, Aq, (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0,
                        tok1, mask_tok, gdelta, gcpart);
     SNV_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(lut_kernel, dim3((unsigned)nq), dim3(256), sh, s, (int)L, (int)D, tok_q, W, Aq,
+  hipLaunchKernelGGL(lut_kernel, dim3((unsigned)nq), dim3(256), sh, s, (int)L, (int)D, tok_q, W, Wp, Aq,
                      (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, (int)nq, tok0, tok1, mask_tok,
                      limbs, (int8_t*)lut_out, exp_out, const_out, gdelta, gcpart);
   SNV_LAUNCH_CHECK();

@@ -22,7 +22,18 @@ Drop-in surface:
 Index: per window, the panel's allele codes are uploaded once to HBM
 (``PanelIndex``); unlike the reference's fp32 embedding cache (:334-377) the
 index does not depend on the mask or the weights, so a mask refresh or a weight
-update never forces a rebuild — ``jit_cache_win_idx`` is kept for API parity.
+update never forces a rebuild.
+
+Panel-embedding staleness (``panel_cache``).  The reference embeds a window's panel once,
+in eval mode, when a batch of that window arrives and the cache holds another window
+(``jit_cache_win_idx != win_idx``, :334-377; reset at every epoch start and by
+``clear_jit_cache``), then keeps searching those embeddings while the weights train over the
+window's following batches.  ``panel_cache="window"`` (default) reproduces that: on the same
+trigger the token table W and the panel's AF embedding A_r are snapshotted (10 x D and L x D
+floats instead of the reference's [n_haps, L, D] cache) and the search ranks the current
+(dropped-out) query embeddings against the snapshot (``snvrag_knn_lut_panel``: panel side
+W_snap, query side W).  ``panel_cache="fresh"`` searches the panel under the current weights
+at every batch.  Eval mode (validation, inference) has no weight updates: both are the same.
 """
 
 from __future__ import annotations
@@ -46,8 +57,12 @@ class EmbeddingRAGDataset(TrainDataset):
                  ref_gt: Optional[np.ndarray] = None, ref_pos: Optional[np.ndarray] = None,
                  embedding_layer=None, build_ref_data: bool = True, n_gpu: int = 1,
                  maf_mask_percentage: int = 10, use_dynamic_mask: bool = False, name: str = "default",
-                 index_cache_bytes: int = 64 << 30):
+                 index_cache_bytes: int = 64 << 30, panel_cache: str = "window"):
         super().__init__(vocab, vcf, pos, panel, freq, window, type_to_idx, pop_to_idx, pos_to_idx)
+        if panel_cache not in ("window", "fresh"):
+            raise ValueError("panel_cache must be 'window' (the reference's per-window snapshot) or 'fresh'")
+        self.panel_cache = panel_cache
+        self._panel_snap = None          # (window, W snapshot, A_r snapshot) of the cached window
         self.maf_mask_percentage, self.use_dynamic_mask = maf_mask_percentage, use_dynamic_mask
         self.current_epoch, self.name = 0, name
         self.ref_tokens_complete: List[np.ndarray] = []
@@ -98,6 +113,7 @@ class EmbeddingRAGDataset(TrainDataset):
 
     def clear_jit_cache(self) -> None:
         self.jit_cache_win_idx = -1
+        self._panel_snap = None
         self._index_cache.clear()
 
     def regenerate_masks(self, seed: int) -> None:
@@ -233,8 +249,11 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     rag_idx = torch.empty(2 * B, k, device=dev, dtype=torch.long)
     rag_groups = []
     dense_out = None
+    stale = train and getattr(ds, "panel_cache", "fresh") == "window"
     for w in windows:
         rows = groups.get(w, [])
+        # the reference's cache trigger (:334-336): another window cached, or reset at epoch start
+        new_snap = stale and (ds.jit_cache_win_idx != w or ds._panel_snap is None or ds._panel_snap[0] != w)
         index = ds.panel_index(w, dev)
         rows_t = torch.tensor(rows, device=dev, dtype=torch.long)
         tok = torch.cat([h1[rows_t], h2[rows_t]], 0).contiguous()
@@ -250,6 +269,15 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         with torch.no_grad():
             Ar_emb = eng.af_embedding(ref_af.unsqueeze(0), True).float()[0].contiguous() \
                 if P.af is not None else None
+            Wp, stale_w = None, False
+            if stale:
+                if new_snap:   # eval-mode panel embedding of this window under the weights of now
+                    ds._panel_snap = (w, P.W.detach().float().clone(), Ar_emb)
+                _, W_s, Ar_s = ds._panel_snap
+                # weights unchanged since the snapshot (its first batch): the plain search is the same
+                stale_w = not (torch.equal(W_s, P.W) and (Ar_s is None or torch.equal(Ar_s, Ar_emb)))
+                if stale_w:
+                    Wp, Ar_emb = W_s, Ar_s
             Aq_drop = None
             if p_drop > 0 and len(rows):
                 # train mode: the reference embeds the queries WITH dropout before the distance
@@ -261,10 +289,11 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
             if shard is not None:
                 from ..retrieval.shards import any_rank, kernel_ops, sharded_neighbours
                 drop_any = any_rank(p_drop > 0, dev, shard.group)
-                exact = P.af is not None and not drop_any and any_rank(not same, dev, shard.group)
+                # a snapshot A_r differs from the queries' current AF embedding even for equal AF
+                exact = P.af is not None and not drop_any and (stale_w or any_rank(not same, dev, shard.group))
                 ops = kernel_ops(index, P.W, site_mask, k, limbs,
                                  aq_fn=lambda a: eng.af_embedding(a, True).float().contiguous(),
-                                 Ar=Ar_emb if (exact or drop_any) else None)
+                                 Ar=Ar_emb if (exact or drop_any) else None, Wp=Wp)
                 if drop_any and Aq_drop is None:
                     # a rank without queries of this window (or p = 0 while another rank drops):
                     # its rows still enter the exact-LUT launch, as undropped offsets
@@ -283,10 +312,11 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                 if Aq_drop is not None:
                     Aq, aq_period = Aq_drop, 2 * len(rows)
                     Ar = Ar_emb if Ar_emb is not None else torch.zeros(L, D, device=dev)
-                elif not same and P.af is not None:
+                elif (stale_w or not same) and P.af is not None:
                     Aq = eng.af_embedding(afw, True).float().contiguous()
                     Ar = Ar_emb
-                idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=aq_period, Ar=Ar)
+                idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=aq_period, Ar=Ar,
+                                      Wp=Wp)
         nb = len(rows)
         if nb == 0:
             continue

@@ -281,8 +281,10 @@ def gt_head(p1, p2, ref, het, hom, period: int, w: "N.GtW") -> torch.Tensor:
 # ---------------------------------------------------------------------- kNN --
 def knn_lut(tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, n_sites: int, n_sites_pad: int,
             limbs: int = 2, Aq: Optional[torch.Tensor] = None, aq_period: int = 0,
-            Ar: Optional[torch.Tensor] = None, tok0: int = 5, tok1: int = 6, mask_tok: int = 4):
-    """Returns (lut bytes tensor, exps int32 [nq], consts f32 [nq])."""
+            Ar: Optional[torch.Tensor] = None, tok0: int = 5, tok1: int = 6, mask_tok: int = 4,
+            Wp: Optional[torch.Tensor] = None):
+    """Returns (lut bytes tensor, exps int32 [nq], consts f32 [nq]).  ``Wp``: the panel side's
+    token table when it differs from the queries' (a cached panel embedding, snvrag_knn_lut_panel)."""
     N.require_gpu(tok_q)
     nq, L = tok_q.shape
     D = W.shape[1]
@@ -290,9 +292,15 @@ def knn_lut(tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, n_sit
     lut = torch.empty(nbytes, device=tok_q.device, dtype=torch.int8)
     exps = torch.empty(nq, device=tok_q.device, dtype=torch.int32)
     consts = torch.empty(nq, device=tok_q.device, dtype=torch.float32)
-    check(N.lib().snvrag_knn_lut(nq, L, D, ptr(_c(tok_q)), ptr(_c(W)), ptr(Aq), aq_period, ptr(Ar),
-                                 ptr(_c(site_mask)), n_sites, n_sites_pad, tok0, tok1, mask_tok, limbs,
-                                 ptr(lut), ptr(exps), ptr(consts), stream_ptr()), "knn_lut")
+    if Wp is not None and Wp is not W:
+        assert Wp.shape == W.shape and Wp.dtype == torch.float32
+        check(N.lib().snvrag_knn_lut_panel(nq, L, D, ptr(_c(tok_q)), ptr(_c(W)), ptr(_c(Wp)), ptr(Aq), aq_period,
+                                           ptr(Ar), ptr(_c(site_mask)), n_sites, n_sites_pad, tok0, tok1, mask_tok,
+                                           limbs, ptr(lut), ptr(exps), ptr(consts), stream_ptr()), "knn_lut_panel")
+    else:
+        check(N.lib().snvrag_knn_lut(nq, L, D, ptr(_c(tok_q)), ptr(_c(W)), ptr(Aq), aq_period, ptr(Ar),
+                                     ptr(_c(site_mask)), n_sites, n_sites_pad, tok0, tok1, mask_tok, limbs,
+                                     ptr(lut), ptr(exps), ptr(consts), stream_ptr()), "knn_lut")
     return lut, exps, consts
 
 

@@ -94,6 +94,8 @@ _SIGS = {
     "snvrag_knn_lut_bytes": ([i64, i32, C.c_int], sz),
     "snvrag_knn_lut": ([i64, i64, i64, vp, vp, vp, i64, vp, vp, i32, i32, C.c_int, C.c_int, C.c_int,
                         C.c_int, vp, vp, vp, vp], C.c_int),
+    "snvrag_knn_lut_panel": ([i64, i64, i64, vp, vp, vp, vp, i64, vp, vp, i32, i32, C.c_int, C.c_int, C.c_int,
+                              C.c_int, vp, vp, vp, vp], C.c_int),
     "snvrag_knn_scan_parts": ([i64, i32], C.c_int),
     "snvrag_knn_scan": ([vp, i64, i64, i32, vp, i32, C.c_int, C.c_int, i64, vp, i32, vp, vp], C.c_int),
     "snvrag_knn_threshold": ([vp, i32, C.c_int, vp, vp], C.c_int),

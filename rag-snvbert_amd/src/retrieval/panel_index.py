@@ -67,9 +67,10 @@ class PanelIndex:
 
     # ------------------------------------------------------------------ search --
     def lut(self, tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, limbs: int = 2,
-            Aq: Optional[torch.Tensor] = None, aq_period: int = 0, Ar: Optional[torch.Tensor] = None):
+            Aq: Optional[torch.Tensor] = None, aq_period: int = 0, Ar: Optional[torch.Tensor] = None,
+            Wp: Optional[torch.Tensor] = None):
         return K.knn_lut(tok_q.long().contiguous(), W, site_mask, self.n_sites, self.n_sites_pad, limbs,
-                         Aq, aq_period, Ar)
+                         Aq, aq_period, Ar, Wp=Wp)
 
     SAMPLE_MIN = 1 << 17       # panels at least this large get a threshold pre-pass
 
@@ -98,10 +99,12 @@ class PanelIndex:
 
     def search(self, tok_q: torch.Tensor, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: int = 2,
                Aq: Optional[torch.Tensor] = None, aq_period: int = 0, Ar: Optional[torch.Tensor] = None,
-               return_keys: bool = False):
-        """idx int64 [nq, k] (-1 pads when the panel has < k haplotypes), dist f32 [nq, k] (squared L2)."""
+               return_keys: bool = False, Wp: Optional[torch.Tensor] = None):
+        """idx int64 [nq, k] (-1 pads when the panel has < k haplotypes), dist f32 [nq, k] (squared L2).
+        ``Wp`` / ``Ar``: the panel side's token table / AF embedding when they differ from the
+        queries' (a cached, stale panel embedding: snvrag_knn_lut_panel)."""
         nq = tok_q.shape[0]
-        lut, exps, consts = self.lut(tok_q, W, site_mask, limbs, Aq, aq_period, Ar)
+        lut, exps, consts = self.lut(tok_q, W, site_mask, limbs, Aq, aq_period, Ar, Wp=Wp)
         keys = self.scan_keys(lut, nq, limbs, k)
         idx, dist = K.knn_decode(keys, exps, consts)
         if return_keys:

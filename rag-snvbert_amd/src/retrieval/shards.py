@@ -174,9 +174,10 @@ def sharded_neighbours(tok: torch.Tensor, k: int, ops: ShardOps, af_rows: Option
 
 def kernel_ops(index, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: int = 2,
                aq_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
-               Ar: Optional[torch.Tensor] = None) -> ShardOps:
+               Ar: Optional[torch.Tensor] = None, Wp: Optional[torch.Tensor] = None) -> ShardOps:
     """The HIP kernels over this rank's ``PanelIndex`` shard.  With query AF rows, the LUTs
-    take the exact A_q != A_r form (``aq_fn`` maps AF rows to their AF embeddings)."""
+    take the exact A_q != A_r form (``aq_fn`` maps AF rows to their AF embeddings).  ``Wp``:
+    the panel side's (cached) token table when it differs from ``W``."""
     from .. import kernels as K
 
     def keys(tok_all, af_all, aq_all=None):
@@ -184,13 +185,13 @@ def kernel_ops(index, W: torch.Tensor, site_mask: torch.Tensor, k: int, limbs: i
         if aq_all is not None:
             # per-query offsets (dropped-out train queries): Ar is the panel's AF embedding or 0
             ar = Ar if Ar is not None else torch.zeros(aq_all.shape[1:], device=aq_all.device)
-            lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, aq_all.contiguous(), nq, ar)
+            lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, aq_all.contiguous(), nq, ar, Wp=Wp)
             return index.scan_keys(lut, nq, limbs, k), exps, consts
         if af_all is None:
-            lut, exps, consts = index.lut(tok_all, W, site_mask, limbs)
+            lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, Wp=Wp)
             return index.scan_keys(lut, nq, limbs, k), exps, consts
         Aq = aq_fn(af_all)
-        lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, Aq, nq, Ar)
+        lut, exps, consts = index.lut(tok_all, W, site_mask, limbs, Aq, nq, Ar, Wp=Wp)
         return index.scan_keys(lut, nq, limbs, k), exps, consts
 
     def codes(uniq):

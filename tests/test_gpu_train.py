@@ -609,6 +609,71 @@ def test_train_mode_retrieval_query_dropout():
     assert same >= 0.5
 
 
+def test_train_panel_cache_window_snapshot_semantics():
+    """panel_cache="window" (default): train-mode retrieval searches the panel embedded under the
+    weights of the window's FIRST batch (the reference's JIT cache, embedding_rag_dataset.py:
+    334-377, rebuilt only on a window change or a reset), while the queries are embedded under the
+    current weights; "fresh" searches under the current weights.  Both checked against the
+    reference algorithm written out in torch (eval-mode panel embedding, cdist, smallest k) after
+    a weight update between two batches of one window; the overlap of the two neighbour sets is
+    the staleness the reference trains with (printed)."""
+    import copy
+    from src.dataset.synthetic import make_rag_dataset
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.model import build_model
+    k, nb = 6, 4
+    ds, vocab = make_rag_dataset(n_samples=nb, n_sites=300, n_windows=2, n_ref_samples=60, seed=5, name="train")
+    torch.manual_seed(0)
+    m = build_model(len(vocab), 64, 1, 4, dropout=0.0).to(DEV).train()
+    emb = m.bert.embedding
+    rows = [i for i in range(len(ds)) if ds[i]["window_idx"] == 0][:nb]
+    batch = lambda: embedding_rag_collate_fn([ds[i] for i in rows])
+
+    def reference_search(panel_emb_layer, query_emb_layer, b):
+        """embedding_rag_dataset.py:339-402 in torch (float64 distances)."""
+        toks = torch.as_tensor(ds.ref_tokens_complete[0], device=DEV)
+        masked = ds._apply_mask_to_tokens_gpu(toks, torch.as_tensor(ds.window_masks[0], device=DEV))
+        af_r = torch.as_tensor(ds.ref_af_windows[0], device=DEV).float().unsqueeze(0).expand(masked.shape[0], -1)
+        was = [panel_emb_layer.training, query_emb_layer.training]
+        panel_emb_layer.eval(); query_emb_layer.eval()
+        with torch.no_grad():
+            pe_ = panel_emb_layer(masked, af=af_r, pos=True).double().flatten(1)
+            q = query_emb_layer(b["hap_1"].to(DEV), af=b["af"].to(DEV).float(), pos=True).double().flatten(1)
+        panel_emb_layer.train(was[0]); query_emb_layer.train(was[1])
+        d = torch.cdist(q, pe_)
+        return d, d.topk(k, largest=False).values
+
+    def check(idx, d, top):
+        got = torch.gather(d, 1, idx).sort(1).values
+        torch.testing.assert_close(got, top, rtol=1e-5, atol=1e-6)
+
+    assert ds.panel_cache == "window"
+    ds.clear_jit_cache()
+    first = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=k)        # snapshot taken here
+    old = copy.deepcopy(emb)
+    with torch.no_grad():                                                     # a training step's update
+        for p_ in emb.parameters():
+            p_.add_(torch.randn_like(p_) * 0.3 * (p_.std() if p_.numel() > 1 else 1.0))
+    b = batch()
+    stale = ds.process_batch_retrieval(b, emb, DEV, k_retrieve=k)["rag_idx_h1"]
+    d_stale, top_stale = reference_search(old, emb, b)
+    check(stale, d_stale, top_stale)
+    ds.panel_cache = "fresh"
+    fresh = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=k)["rag_idx_h1"]
+    d_fresh, top_fresh = reference_search(emb, emb, b)
+    check(fresh, d_fresh, top_fresh)
+    overlap = np.mean([len(set(a.tolist()) & set(c.tolist())) / k for a, c in zip(stale.cpu(), fresh.cpu())])
+    print(f"neighbour overlap, snapshot vs current panel embedding after one update: {overlap:.3f}")
+    # a window change rebuilds the snapshot (jit_cache_win_idx != win_idx): back on window 0 the
+    # panel side is the current weights again
+    ds.panel_cache = "window"
+    other = [i for i in range(len(ds)) if ds[i]["window_idx"] == 1][:2]
+    ds.process_batch_retrieval(embedding_rag_collate_fn([ds[i] for i in other]), emb, DEV, k_retrieve=k)
+    again = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=k)["rag_idx_h1"]
+    check(again, d_fresh, top_fresh)
+    assert first["rag_idx_h1"].shape == (nb, k)
+
+
 def _ref_trainer_handoff(data, device):
     """pretrain_with_val_optimized.py:180-195 — the reference trainer copies these keys to the
     device and forwards ONLY rag_emb_h1/h2 of what retrieval added."""
