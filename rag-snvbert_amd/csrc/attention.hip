@@ -283,15 +283,6 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
   constexpr int NCB = (NKT + 1) / 2;
   bf16x8 pb[NCB][2];
   bf16x8 pd[TRAIN ? NCB : 1][2];                 // TRAIN: the dropped-out PV operand
-  float dmp[2] = {1.f, 1.f};                     // TRAIN: dropout multipliers of a key pair
-  // TRAIN: hash input of (query 16 qt + li, this lane's first key pair (kbase + 4 lg) / 2); the
-  // pair of (kt, j) adds the compile-time 8 kt + (j & 3) / 2
-  uint32_t drow[TRAIN ? 2 : 1];
-  if constexpr (TRAIN) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-      drow[qt] = drop_row(tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li), (uint32_t)((kbase >> 1) + 2 * lg));
-  }
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
@@ -299,21 +290,32 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int kt = 2 * cb + (j >> 2);
-        if constexpr (TRAIN) {
-          const float p = kt < NKT ? __builtin_amdgcn_exp2f(tr.c * s[kt < NKT ? kt : 0][qt][j & 3]) : 0.f;
-          pb[cb][qt][j] = (bf16)p;
-          // keys 2i, 2i + 1 share one hash: computed at the even j, used at both
-          if ((j & 1) == 0) {
-            if (tr.drop.thresh)
-              drop_split(tr.drop, drop_mix24(drow[qt] + (uint32_t)(8 * kt + ((j & 3) >> 1)) * DROP_C2), dmp[0], dmp[1]);
-            else
-              dmp[0] = dmp[1] = 1.f;
-          }
-          pd[cb][qt][j] = (bf16)(p * dmp[j & 1]);
-        } else {
+        if constexpr (TRAIN)
+          pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(tr.c * s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
+        else
           pb[cb][qt][j] = kt < NKT ? (bf16)__builtin_amdgcn_exp2f(s[kt < NKT ? kt : 0][qt][j & 3]) : (bf16)0.f;
-        }
       }
+  if constexpr (TRAIN) {
+    // dropout: keys 2i, 2i + 1 (one packed dword of P) share one hash; the kept halves pass the
+    // AND, the 1 / (1 - p) scale is applied to O after the loop.  Hash input of (query
+    // 16 qt + li, this lane's first key pair (kbase + 4 lg) / 2); dword i of block cb adds the
+    // pair offset 8 kt + (i & 1), kt = 2 cb + i / 2
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const uint32_t drow = drop_row(tr.dbase, (uint32_t)(tr.q0 + 16 * qt + li), (uint32_t)((kbase >> 1) + 2 * lg));
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        u32x4 w = __builtin_bit_cast(u32x4, pb[cb][qt]);
+        if (tr.drop.thresh) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            w[i] = drop_pair_apply(w[i], drop_mix24(drow + (uint32_t)(8 * (2 * cb + (i >> 1)) + (i & 1)) * DROP_C2),
+                                   tr.drop.thresh);
+        }
+        pd[cb][qt] = __builtin_bit_cast(bf16x8, w);
+      }
+    }
+  }
   const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
 #pragma unroll
@@ -330,6 +332,15 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) st.ls[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[cb][qt], st.ls[qt], 0, 0, 0);
   }
+}
+
+// TRAIN with dropout: the kept probabilities entered PV unscaled; O *= 1 / (1 - p) once
+__device__ __forceinline__ void drop_scale_o(State& st, const AttnDrop& drop) {
+  if (!drop.thresh) return;
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) st.o[e][qt] *= drop.scale;
 }
 
 template <bool FIRST, bool TRAIN = false>
@@ -493,6 +504,7 @@ __global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __r
 #undef A32_LOAD
 #undef A32_STORE
   if (!active) return;
+  if constexpr (TRAIN) drop_scale_o(st, drop);
 
   bool bad = false;
 #pragma unroll
@@ -647,6 +659,7 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
     }
   }
   if (!active) return;
+  if constexpr (TRAIN) drop_scale_o(st, drop);
 
   bool bad = false;
 #pragma unroll

@@ -81,6 +81,17 @@ __device__ __forceinline__ void drop_split(const AttnDrop& d, uint32_t h, float&
   m0 = (h & 0xFFFFu) >= d.thresh ? d.scale : 0.f;
   m1 = (h >> 16) >= d.thresh ? d.scale : 0.f;
 }
+// probabilities of a key pair after dropout: w = the packed bf16 pair (key 2i low half, 2i + 1
+// high half), h = the pair's hash.  A half is dropped iff its hash half < thresh, i.e. iff
+// (hash half - thresh) is negative, whose bits 16..31 are then all ones: one byte permute
+// gathers those bits of both differences into a drop mask and the kept halves pass unscaled
+// (the 1 / (1 - p) scale is applied once to the output).  4 VALU ops per pair instead of two
+// compares, two selects, two multiplies and a second conversion.
+__device__ __forceinline__ uint32_t drop_pair_apply(uint32_t w, uint32_t h, uint32_t thresh) {
+  const uint32_t xlo = (h & 0xFFFFu) - thresh, xhi = (h >> 16) - thresh;
+  const uint32_t m = __builtin_amdgcn_perm(xhi, xlo, 0x07060302u);   // [xlo.b2, xlo.b3, xhi.b2, xhi.b3]
+  return w & ~m;
+}
 // dropout multiplier of probability (q, k): 0 or 1 / (1 - p)
 __device__ __forceinline__ float drop_mul(const AttnDrop& d, uint32_t base, uint32_t q, uint32_t k) {
   const uint32_t h = drop_hash(base, q, k >> 1);
