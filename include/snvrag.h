@@ -433,6 +433,17 @@ int snvrag_confusion(int64_t M, int C, const float* probs, const int64_t* labels
 int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
                         float eps, void* y, void* s_out, float* stats, float p_r, float p_out, uint64_t seed,
                         void* stream);
+/* The same with FeedForward's LeakyReLUs fused (feed_forward.py:20-21): slope_x != 0 (no
+ * residual): y = LN(lrelu(x)), s_out unused (the backward's s is x itself); slope_r != 0:
+ * s = x + drop(lrelu(r)).  Backward: slope_x: s = the pre-activation x, ds = d/dx through the
+ * activation; slope_r: r_pre = the pre-activation r, dres = d/dr (always written). */
+int snvrag_ln_fwd_train_act(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
+                            float eps, void* y, void* s_out, float* stats, float p_r, float p_out, uint64_t seed,
+                            float slope_x, float slope_r, void* stream);
+int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
+                      void* ds, void* dres, const void* r_pre, float* dg, float* db, int accumulate, float p_r,
+                      float p_out, uint64_t seed, float slope_x, float slope_r, void* ws, size_t ws_bytes,
+                      void* stream);
 size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N);
 int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
                   void* ds, void* dres, float* dg, float* db, int accumulate, float p_r, float p_out,

@@ -560,10 +560,17 @@ template <bool PRESCALED, bool TRAIN = false>
 __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
                                                   int* __restrict__ n_fallback, long total_rows,
-                                                  float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{}) {
+                                                  float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{},
+                                                  int desync = 0) {
   using namespace a32;
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int nwg = gridDim.x, orig = blockIdx.x;
+  // first round: the k-th workgroup of each CU starts k * desync cycles late, so the waves that
+  // share a SIMD are not all in their exp phase (or all in their MFMA phase) at once
+  if (desync > 0 && orig < 1024) {
+    const long wait = (long)desync * (orig >> 8), t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(4);
+  }
   const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
   const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
@@ -979,6 +986,8 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
     const bool dma = !(reg && reg[0] == '1');
     const char* pipe = getenv("SNVRAG_ATTN_PIPE");    // A/B: the software-pipelined kernel (1, 2 = sched hints)
+    const char* dz = getenv("SNVRAG_ATTN_DESYNC");       // A/B: first-round stagger (cycles)
+    const int desync = dz ? atoi(dz) : 0;
     if (pipe && pipe[0] != '0' && L >= a32::KT) {
       const bool sch = pipe[0] == '2';
       if (pre)
@@ -990,10 +999,10 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     } else if (dma) {
       if (pre)
         hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
+                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{}, desync);
       else
         hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
+                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{}, desync);
     } else if (pre)
       hipLaunchKernelGGL(attn32_bf16<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
                          (bf16*)out, ldo, 1.0f, nqb, cnt);

@@ -157,8 +157,14 @@ __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16
 using namespace snvrag;
 
 extern "C" int snvrag_dw_splits(int64_t M, int64_t N, int64_t K) {
+  // Every split adds one f32 partial per output element (no-return atomics): the atomic volume
+  // is splits x N x K, comparable to the MFMA time at these shapes, so the split count targets
+  // ~2 workgroups per CU (~1 when there are few output tiles), not a full 4-deep occupancy.
+  // Measured at M = 49 440 (tools/dw_micro.py): 1536 x 384 104.8 us at 14 splits vs 132.2 at 29,
+  // 384 x 384 48.7 us at 28 vs 73.0 at 114; 15 splits of 36 tiles (540 > 512 workgroups) 120.1 us.
   const long tiles = (N / DW_T) * (K / DW_T);
-  long s = (1024 + tiles - 1) / std::max<long>(tiles, 1);            // ~4 workgroups per CU
+  const long target = tiles >= 16 ? 512 : 256;
+  long s = target / std::max<long>(tiles, 1);                         // whole rounds: <= target workgroups
   const long max_s = (M + 8 * DW_R - 1) / (8 * DW_R);                // >= 8 stages per chunk
   s = std::min(std::max(s, 1L), std::max(max_s, 1L));
   return (int)s;

@@ -206,15 +206,21 @@ __device__ __forceinline__ void st8bf(bf16* p, const float* v) {
 // dropouts around the norms, transformer.py / sublayer.py): keep (m, n) iff half (n & 1) of
 // mix24(base + m * C1 + (n >> 1) * C2) >= thresh, base = drop_base(seed, stream) with stream 0
 // for the residual operand r and 1 for the output (attn_common.h's hash over (row, column)).
+// sl_x / sl_r: LeakyReLU slopes applied to the input x (no residual) / to the residual operand r
+// BEFORE its dropout (0: none) — the FeedForward's activations (feed_forward.py:20-21) fused into
+// the LayerNorm kernels instead of separate elementwise passes; sign(LeakyReLU(v)) = sign(v), so
+// the backward's derivative comes from the saved pre-activation.
 struct LnDrop {
   uint32_t th_r, th_o;          // round(p * 2^16); 0: off
   float sc_r, sc_o;             // 1 / (1 - p)
   uint32_t base_r, base_o;
+  float sl_x, sl_r;
 };
-static LnDrop make_ln_drop(float p_r, float p_o, uint64_t seed) {
+static LnDrop make_ln_drop(float p_r, float p_o, uint64_t seed, float sl_x = 0.f, float sl_r = 0.f) {
   const AttnDrop a = make_attn_drop(p_r, seed), b = make_attn_drop(p_o, seed);
-  return LnDrop{a.thresh, b.thresh, a.scale, b.scale, drop_base(seed, 0u), drop_base(seed, 1u)};
+  return LnDrop{a.thresh, b.thresh, a.scale, b.scale, drop_base(seed, 0u), drop_base(seed, 1u), sl_x, sl_r};
 }
+__device__ __forceinline__ float ln_lrelu(float v, float sl) { return v > 0.f ? v : v * sl; }
 // multipliers of the 8 columns 8 cc .. 8 cc + 7 of row m: 4 hashes
 __device__ __forceinline__ void ln_drop8(uint32_t base, uint32_t th, float sc, long m, int cc, float (&mk)[8]) {
   const uint32_t row = base + (uint32_t)m * DROP_C1 + (uint32_t)(4 * cc) * DROP_C2;
@@ -242,9 +248,17 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
     const int cc = lane + 64 * c;
     if (cc < nc) {
       ld8bf(x + m * N + 8 * cc, v[c]);
+      if (dr.sl_x != 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)ln_lrelu(v[c][j], dr.sl_x);
+      }
       if (r) {
         float t[8];
         ld8bf(r + m * N + 8 * cc, t);
+        if (dr.sl_r != 0.f) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] = (float)(bf16)ln_lrelu(t[j], dr.sl_r);
+        }
         if (dr.th_r) {
           float mk[8];
           ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
@@ -289,10 +303,14 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
 // RPB rows per block (one wave each, looping): the block's dg/db partials go to
 // part[blockIdx.x][2][N].  Output dropout: dy is masked on load; residual dropout: dr = ds
 // masked (the gradient of r), written next to ds.
+// sl_x: s is the PRE-activation input x (y = LN(lrelu(x))), the normalised value is rebuilt as
+// lrelu(s) and ds carries the activation's derivative; sl_r: rp is the pre-activation residual r
+// and dres = ds o mask o lrelu'(r) (always written).
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per_wave, const bf16* __restrict__ dy,
                                                      const bf16* __restrict__ s, const float2* __restrict__ stats,
                                                      const float* __restrict__ g, bf16* __restrict__ ds,
-                                                     bf16* __restrict__ dres, float* __restrict__ part, LnDrop dr) {
+                                                     bf16* __restrict__ dres, float* __restrict__ part, LnDrop dr,
+                                                     const bf16* __restrict__ rp) {
   extern __shared__ float red[];                      // [4 waves][2][N]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nc = N / 8;
@@ -307,6 +325,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
     if (m >= M) break;
     const float2 st = stats[m];
     float xh[LN_MAXC][8], gy[LN_MAXC][8];
+    uint32_t neg[LN_MAXC];                           // sl_x: bit j = pre-activation x[j] <= 0
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int c = 0; c < LN_MAXC; ++c) {
@@ -314,6 +333,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
       if (cc < nc) {
         float dv[8];
         ld8bf(s + m * N + 8 * cc, xh[c]);
+        if (dr.sl_x != 0.f) {
+          neg[c] = 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            neg[c] |= (xh[c][j] > 0.f ? 0u : 1u) << j;
+            xh[c][j] = (float)(bf16)ln_lrelu(xh[c][j], dr.sl_x);
+          }
+        }
         ld8bf(dy + m * N + 8 * cc, dv);
         if (dr.th_o) {
           float mk[8];
@@ -341,12 +368,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = st.y * (gy[c][j] - a1 - xh[c][j] * a2);
-        st8bf(ds + m * N + 8 * cc, o);
-        if (dres) {
-          float mk[8];
-          ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+        if (dr.sl_x != 0.f) {
+          float dx[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+          for (int j = 0; j < 8; ++j) dx[j] = ((neg[c] >> j) & 1u) ? o[j] * dr.sl_x : o[j];
+          st8bf(ds + m * N + 8 * cc, dx);
+        } else {
+          st8bf(ds + m * N + 8 * cc, o);
+        }
+        if (dres) {
+          if (dr.th_r) {
+            float mk[8];
+            ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+          }
+          if (rp) {
+            float rv[8];
+            ld8bf(rp + m * N + 8 * cc, rv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = rv[j] > 0.f ? o[j] : o[j] * dr.sl_r;
+          }
           st8bf(dres + m * N + 8 * cc, o);
         }
       }
@@ -464,6 +506,14 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, int row
 extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
                                    float eps, void* y, void* s_out, float* stats, float p_r, float p_out,
                                    uint64_t seed, void* stream) {
+  return snvrag_ln_fwd_train_act(M, N, x, r, g, b, eps, y, s_out, stats, p_r, p_out, seed, 0.f, 0.f, stream);
+}
+
+extern "C" int snvrag_ln_fwd_train_act(int64_t M, int N, const void* x, const void* r, const float* g,
+                                       const float* b, float eps, void* y, void* s_out, float* stats, float p_r,
+                                       float p_out, uint64_t seed, float slope_x, float slope_r, void* stream) {
+  SNV_CHECK_ARG(slope_x == 0.f || !r, "an input activation is for a norm without a residual");
+  SNV_CHECK_ARG(slope_r == 0.f || r, "a residual activation needs a residual");
   SNV_CHECK_ARG(x && g && b && y && stats, "null pointer");
   SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
   SNV_CHECK_ARG(!r || s_out, "a residual needs s_out");
@@ -472,7 +522,7 @@ extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* 
   if (M == 0) return 0;
   hipLaunchKernelGGL(ln_fwd_train_kernel, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N,
                      (const bf16*)x, (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats,
-                     make_ln_drop(p_r, p_out, seed));
+                     make_ln_drop(p_r, p_out, seed, slope_x, slope_r));
   SNV_LAUNCH_CHECK();
   return 0;
 }
@@ -485,11 +535,21 @@ extern "C" size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N) {
 extern "C" int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
                              void* ds, void* dres, float* dg, float* db, int accumulate, float p_r, float p_out,
                              uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+  SNV_CHECK_ARG(!dres || p_r > 0.f, "dres is the residual-dropout gradient (p_r > 0)");
+  return snvrag_ln_bwd_act(M, N, dy, s, stats, g, ds, dres, nullptr, dg, db, accumulate, p_r, p_out, seed, 0.f, 0.f,
+                           ws, ws_bytes, stream);
+}
+
+extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
+                                 void* ds, void* dres, const void* r_pre, float* dg, float* db, int accumulate,
+                                 float p_r, float p_out, uint64_t seed, float slope_x, float slope_r, void* ws,
+                                 size_t ws_bytes, void* stream) {
   SNV_CHECK_ARG(dy && s && stats && g && ds && dg && db && ws, "null pointer");
   SNV_CHECK_ARG(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "N must be a multiple of 8, <= 2048");
   SNV_CHECK_ARG(ws_bytes >= snvrag_ln_bwd_ws_bytes(M, N), "workspace too small");
   SNV_CHECK_ARG(p_r >= 0.f && p_r < 1.f && p_out >= 0.f && p_out < 1.f, "dropout probabilities must be in [0, 1)");
-  SNV_CHECK_ARG(!dres || p_r > 0.f, "dres is the residual-dropout gradient (p_r > 0)");
+  SNV_CHECK_ARG(slope_r == 0.f || (dres && r_pre), "a residual activation needs dres and the pre-activation r");
+  SNV_CHECK_ARG(!dres || p_r > 0.f || slope_r != 0.f, "dres is the residual operand's own gradient");
   if (M == 0) return 0;
   hipStream_t st = as_stream(stream);
   const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
@@ -497,7 +557,7 @@ extern "C" int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, co
   float* part = (float*)ws;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nblk), dim3(256), 4 * 2 * N * sizeof(float), st, (long)M, N, rpw,
                      (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, (bf16*)dres, part,
-                     make_ln_drop(p_r, p_out, seed));
+                     make_ln_drop(p_r, p_out, seed, slope_x, slope_r), (const bf16*)(slope_r != 0.f ? r_pre : nullptr));
   SNV_LAUNCH_CHECK();
   // dg = sum over blocks of part[:, 0, :], db of part[:, 1, :] (written or accumulated)
   hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)part,

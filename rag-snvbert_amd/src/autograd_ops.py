@@ -373,31 +373,37 @@ class _HipAddLayerNorm(torch.autograd.Function):
     the backward)."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, p_r, p_out, seed):
+    def forward(ctx, x, r, weight, bias, eps, p_r, p_out, seed, slope_x=0.0, slope_r=0.0):
         x = x.to(torch.bfloat16).contiguous()
         r = r.to(torch.bfloat16).contiguous() if r is not None else None
         y, s, stats = K.ln_fwd_train(x, r, weight.detach().float().contiguous(),
-                                     bias.detach().float().contiguous(), eps, p_r, p_out, seed)
-        ctx.save_for_backward(s, stats, weight)
+                                     bias.detach().float().contiguous(), eps, p_r, p_out, seed, slope_x, slope_r)
+        if slope_r != 0.0:
+            ctx.save_for_backward(s, stats, weight, r)
+        else:
+            ctx.save_for_backward(s, stats, weight)
         ctx.has_r = r is not None
         ctx.drop = (p_r, p_out, seed)
+        ctx.slopes = (slope_x, slope_r)
         ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        s, stats, weight = ctx.saved_tensors
+        s, stats, weight, *rp = ctx.saved_tensors
         p_r, p_out, seed = ctx.drop
+        slope_x, slope_r = ctx.slopes
         w, b = ctx.params
         direct = _DIRECT_GRADS and _grad_buffer(w) is not None and _grad_buffer(b) is not None
         ds, dres, dg, db = K.ln_bwd(gy.to(torch.bfloat16).contiguous(), s, stats, weight.detach().float().contiguous(),
-                                    p_r, p_out, seed, dg=w.grad if direct else None, db=b.grad if direct else None)
+                                    p_r, p_out, seed, dg=w.grad if direct else None, db=b.grad if direct else None,
+                                    slope_x=slope_x, slope_r=slope_r, r_pre=rp[0] if rp else None)
         dr = (dres if dres is not None else ds) if ctx.has_r else None
         if direct:
             _grad_ready(w)
             _grad_ready(b)
-            return ds, dr, None, None, None, None, None, None
-        return ds, dr, dg, db, None, None, None, None
+            return ds, dr, None, None, None, None, None, None, None, None
+        return ds, dr, dg, db, None, None, None, None, None, None
 
 
 def _drop_seed() -> int:
@@ -405,20 +411,26 @@ def _drop_seed() -> int:
 
 
 def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln, p_r: float = 0.0,
-                      p_out: float = 0.0) -> torch.Tensor:
-    """bf16 drop_o(LayerNorm(x + drop_r(r))) with the parameters of nn.LayerNorm ``ln``
-    (N % 8 == 0, N <= 2048); p_r / p_out: dropout on the residual operand / the output
-    (training; the masks are a counter-based hash of a seed from torch's RNG).  f32 parity
-    mode: torch's f32 LayerNorm and F.dropout."""
+                      p_out: float = 0.0, act_x: float = 0.0, act_r: float = 0.0) -> torch.Tensor:
+    """bf16 drop_o(LayerNorm(lrelu_x(x) + drop_r(lrelu_r(r)))) with the parameters of nn.LayerNorm
+    ``ln`` (N % 8 == 0, N <= 2048); p_r / p_out: dropout on the residual operand / the output
+    (training; the masks are a counter-based hash of a seed from torch's RNG); act_x / act_r:
+    LeakyReLU slopes (0: none) fused into the norm (act_x only without a residual).  f32 parity
+    mode: torch's f32 LeakyReLU, LayerNorm and F.dropout."""
     if train_dtype() == torch.float32:
+        xx = torch.nn.functional.leaky_relu(x.float(), act_x) if act_x else x.float()
         rr = r.float() if r is not None else None
+        if rr is not None and act_r:
+            rr = torch.nn.functional.leaky_relu(rr, act_r)
         if rr is not None and p_r > 0:
             rr = torch.nn.functional.dropout(rr, p_r, True)
-        s = x.float() + rr if rr is not None else x.float()
+        s = xx + rr if rr is not None else xx
         y = torch.nn.functional.layer_norm(s, (s.shape[-1],), ln.weight, ln.bias, ln.eps)
         return torch.nn.functional.dropout(y, p_out, True) if p_out > 0 else y
+    assert not (act_x and r is not None), "act_x is for a norm without a residual"
     seed = _drop_seed() if (p_r > 0 or p_out > 0) else 0
-    return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, float(p_r), float(p_out), seed)
+    return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, float(p_r), float(p_out), seed,
+                                  float(act_x), float(act_r))
 
 
 class _HipAttention(torch.autograd.Function):

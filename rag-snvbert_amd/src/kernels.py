@@ -554,32 +554,37 @@ def infer_post(probs_h1: torch.Tensor, probs_h2: torch.Tensor):
 
 
 def ln_fwd_train(x: torch.Tensor, r: Optional[torch.Tensor], g: torch.Tensor, b: torch.Tensor, eps: float,
-                 p_r: float = 0.0, p_out: float = 0.0, seed: int = 0):
-    """(y bf16, s bf16 = x + drop(r) (x itself when r is None), stats f32 [M, 2]); y carries the
-    output dropout p_out (masks: counter-based hash of seed, row, column)."""
+                 p_r: float = 0.0, p_out: float = 0.0, seed: int = 0, slope_x: float = 0.0, slope_r: float = 0.0):
+    """(y bf16, s bf16 = act_x(x) + drop(act_r(r)) (x itself when r is None), stats f32 [M, 2]); y
+    carries the output dropout p_out (masks: counter-based hash of seed, row, column).  slope_x /
+    slope_r: LeakyReLU on x (no residual; s is then the pre-activation x) / on r before its dropout."""
     N.require_gpu(x)
     Nn = x.shape[-1]
     M = x.numel() // Nn
     y = torch.empty_like(x)
     s = torch.empty_like(x) if r is not None else x
     stats = torch.empty(M, 2, device=x.device, dtype=torch.float32)
-    check(N.lib().snvrag_ln_fwd_train(M, Nn, ptr(_c(x)), ptr(_c(r)) if r is not None else None,
-                                      ptr(_c(g)), ptr(_c(b)), eps, ptr(y), ptr(s) if r is not None else None,
-                                      ptr(stats), float(p_r), float(p_out), int(seed) & (2 ** 64 - 1),
-                                      stream_ptr()), "ln_fwd_train")
+    check(N.lib().snvrag_ln_fwd_train_act(M, Nn, ptr(_c(x)), ptr(_c(r)) if r is not None else None,
+                                          ptr(_c(g)), ptr(_c(b)), eps, ptr(y), ptr(s) if r is not None else None,
+                                          ptr(stats), float(p_r), float(p_out), int(seed) & (2 ** 64 - 1),
+                                          float(slope_x), float(slope_r), stream_ptr()), "ln_fwd_train")
     return y, s, stats
 
 
 def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tensor, p_r: float = 0.0,
            p_out: float = 0.0, seed: int = 0, dg: Optional[torch.Tensor] = None,
-           db: Optional[torch.Tensor] = None):
+           db: Optional[torch.Tensor] = None, slope_x: float = 0.0, slope_r: float = 0.0,
+           r_pre: Optional[torch.Tensor] = None):
     """(ds bf16, dres bf16 or None, dg f32 [N], db f32 [N]) of y = drop_o(LN(s) g + b),
-    s = x + drop_r(r): ds = dx, dres = dr (None when p_r == 0: dr = ds).  dg / db given (f32,
-    contiguous: the parameters' .grad) are accumulated into, else fresh."""
+    s = x + drop_r(r): ds = dx, dres = dr (None when p_r == 0 and no residual activation: dr =
+    ds).  dg / db given (f32, contiguous: the parameters' .grad) are accumulated into, else fresh.
+    slope_x: s is the pre-activation x of y = LN(lrelu(x)); slope_r: r_pre is the pre-activation
+    residual (dres through the activation)."""
     Nn = s.shape[-1]
     M = s.numel() // Nn
     ds = torch.empty_like(s)
-    dres = torch.empty_like(s) if p_r > 0 else None
+    dres = torch.empty_like(s) if (p_r > 0 or slope_r != 0.0) else None
+    assert slope_r == 0.0 or r_pre is not None
     acc = dg is not None
     if dg is None:
         dg = torch.empty(Nn, device=s.device, dtype=torch.float32)
@@ -587,9 +592,10 @@ def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tens
     assert db is not None and dg.is_contiguous() and db.is_contiguous() and dg.dtype == db.dtype == torch.float32
     wsb = N.lib().snvrag_ln_bwd_ws_bytes(M, Nn)
     ws = torch.empty(wsb, device=s.device, dtype=torch.uint8)
-    check(N.lib().snvrag_ln_bwd(M, Nn, ptr(_c(dy)), ptr(_c(s)), ptr(_c(stats)), ptr(_c(g)), ptr(ds), ptr(dres),
-                                ptr(dg), ptr(db), int(acc), float(p_r), float(p_out), int(seed) & (2 ** 64 - 1),
-                                ptr(ws), wsb, stream_ptr()), "ln_bwd")
+    check(N.lib().snvrag_ln_bwd_act(M, Nn, ptr(_c(dy)), ptr(_c(s)), ptr(_c(stats)), ptr(_c(g)), ptr(ds), ptr(dres),
+                                    ptr(_c(r_pre)) if r_pre is not None else None, ptr(dg), ptr(db), int(acc),
+                                    float(p_r), float(p_out), int(seed) & (2 ** 64 - 1), float(slope_x),
+                                    float(slope_r), ptr(ws), wsb, stream_ptr()), "ln_bwd")
     return ds, dres, dg, db
 
 

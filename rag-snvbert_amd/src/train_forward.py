@@ -172,9 +172,11 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     po = p if training else 0.0
     x = hip_add_layernorm(x, o, blk.input_sublayer.norm, p_out=po)
     ff = blk.feed_forward
-    h = F.leaky_relu(hip_linear(x, ff.w_1.weight, ff.w_1.bias), 0.1)
-    f = F.leaky_relu(hip_linear(hip_add_layernorm(h, None, ff.norm), ff.w_2.weight, ff.w_2.bias), 0.1)
-    return hip_add_layernorm(x, f, blk.output_sublayer.norm, p_r=po, p_out=1.0 - (1.0 - po) ** 2)
+    # feed_forward.py:20-21: both LeakyReLUs run inside the LayerNorm kernels (w_1's on the FFN
+    # norm's input, w_2's on the output sublayer's residual operand, before its dropout)
+    h = hip_linear(x, ff.w_1.weight, ff.w_1.bias)
+    f = hip_linear(hip_add_layernorm(h, None, ff.norm, act_x=0.1), ff.w_2.weight, ff.w_2.bias)
+    return hip_add_layernorm(x, f, blk.output_sublayer.norm, p_r=po, p_out=1.0 - (1.0 - po) ** 2, act_r=0.1)
 
 
 @dataclass

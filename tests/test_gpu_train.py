@@ -274,6 +274,59 @@ def test_hip_add_layernorm_fwd_bwd(M, N, resid):
     assert rel(ln.weight.grad, wr.grad) < 1e-3 and rel(ln.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("M,N,mode", [(300, 1536, "x"), (257, 384, "r"), (64, 384, "r_drop")])
+def test_hip_add_layernorm_fused_leaky_relu(M, N, mode):
+    """FeedForward's LeakyReLUs fused into the LayerNorm kernels (feed_forward.py:20-21): mode x:
+    y = LN(lrelu(x)) (the FFN norm on w_1's pre-activation output); r: y = LN(x + lrelu(r)) (the
+    output sublayer on w_2's pre-activation output); r_drop: the same with residual dropout
+    (checked against the un-fused kernel path on identical masks: same seed).  Forward and every
+    gradient vs torch f32 autograd on the same bf16 inputs, 1e-2 relative (bf16 outputs)."""
+    from src.autograd_ops import hip_add_layernorm
+    import src.autograd_ops as A
+    g = torch.Generator(device="cpu").manual_seed(N + M)
+    ln = torch.nn.LayerNorm(N).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(N, generator=g) * 0.5 + 1)
+        ln.bias.copy_(torch.randn(N, generator=g) * 0.1)
+    x = (torch.randn(M, N, generator=g) * 2).to(DEV, torch.bfloat16).requires_grad_(True)
+    r = (torch.randn(M, N, generator=g) * 2).to(DEV, torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()
+    if mode == "r_drop":
+        seed = 1234
+        orig = A._drop_seed
+        A._drop_seed = lambda: seed
+        try:
+            y = hip_add_layernorm(x, r, ln, p_r=0.2, act_r=0.1)
+            y.backward(gy)
+            gx, gr, gw = x.grad.clone(), r.grad.clone(), ln.weight.grad.clone()
+            x.grad = r.grad = None
+            ln.weight.grad = ln.bias.grad = None
+            ra = torch.nn.functional.leaky_relu(r, 0.1)            # the un-fused path, same seed
+            y2 = hip_add_layernorm(x, ra, ln, p_r=0.2)
+            y2.backward(gy)
+        finally:
+            A._drop_seed = orig
+        assert rel(y, y2) < 1e-3 and rel(gx, x.grad) < 1e-3 and rel(gr, r.grad) < 1e-2 and rel(gw, ln.weight.grad) < 1e-3
+        return
+    y = hip_add_layernorm(x, None, ln, act_x=0.1) if mode == "x" else hip_add_layernorm(x, r, ln, act_r=0.1)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    wr, br = ln.weight.detach().clone().requires_grad_(True), ln.bias.detach().clone().requires_grad_(True)
+    if mode == "x":
+        s = torch.nn.functional.leaky_relu(xr, 0.1)
+    else:
+        s = xr + torch.nn.functional.leaky_relu(rr, 0.1)
+    yr = torch.nn.functional.layer_norm(s, (N,), wr, br, ln.eps)
+    yr.backward(gy.float())
+    assert rel(y, yr.detach()) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    if mode == "r":
+        assert rel(r.grad, rr.grad) < 1e-2
+    assert rel(ln.weight.grad, wr.grad) < 2e-3 and rel(ln.bias.grad, br.grad) < 2e-3
+
+
 def test_focal_loss_kernel_vs_oracle_and_reference():
     from src import kernels as K
     z = load_golden("focal")
