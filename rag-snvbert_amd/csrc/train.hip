@@ -14,6 +14,8 @@
 //             written for the next step's MFMA GEMMs.
 //   confusion: cal_pr (optim_schedule.py:167-203) as device counters (no per-batch D2H).
 #include "common.h"
+
+#include <cstdlib>
 #include "attn_common.h"
 
 #include <cmath>
@@ -186,6 +188,7 @@ extern "C" int snvrag_confusion(int64_t M, int C, const float* probs, const int6
 // One wave per row, lanes over 8-column chunks.
 namespace snvrag {
 constexpr int LN_MAXC = 4;   // 8-col chunks per lane: N <= 64 * 8 * 4 = 2048
+constexpr int LN_BWD_RPW = 8;  // rows per wave of ln_bwd (up to 2048 blocks)
 
 __device__ __forceinline__ void ld8bf(const bf16* p, float* v) {
   const u32x4 a = *reinterpret_cast<const u32x4*>(p);
@@ -232,6 +235,7 @@ __device__ __forceinline__ void ln_drop8(uint32_t base, uint32_t th, float sc, l
   }
 }
 
+template <int NC>
 __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ r, const float* __restrict__ g,
                                                            const float* __restrict__ b, float eps,
@@ -241,10 +245,10 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
   const int lane = threadIdx.x & 63;
   if (m >= M) return;
   const int nc = N / 8;
-  float v[LN_MAXC][8];
+  float v[NC][8];
   float sum = 0.f;
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int cc = lane + 64 * c;
     if (cc < nc) {
       ld8bf(x + m * N + 8 * cc, v[c]);
@@ -275,13 +279,13 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
   const float mean = wave_sum(sum) / N;
   float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
     if (lane + 64 * c < nc)
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; q += d * d; }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / N + eps);
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int cc = lane + 64 * c;
     if (cc < nc) {
       float o[8];
@@ -306,6 +310,10 @@ __global__ __launch_bounds__(256) void ln_fwd_train_kernel(long M, int N, const 
 // sl_x: s is the PRE-activation input x (y = LN(lrelu(x))), the normalised value is rebuilt as
 // lrelu(s) and ds carries the activation's derivative; sl_r: rp is the pre-activation residual r
 // and dres = ds o mask o lrelu'(r) (always written).
+// NC 8-column chunks per lane (N <= 512 NC * ... : the register arrays sized to the row), and every
+// wave steps through its rows TWO at a time so the two rows' loads and wave reductions overlap
+// (a row alone is latency-bound on its two reductions).
+template <int NC, int RP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per_wave, const bf16* __restrict__ dy,
                                                      const bf16* __restrict__ s, const float2* __restrict__ stats,
                                                      const float* __restrict__ g, bf16* __restrict__ ds,
@@ -314,88 +322,105 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
   extern __shared__ float red[];                      // [4 waves][2][N]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nc = N / 8;
-  float dgp[LN_MAXC][8], dbp[LN_MAXC][8];
+  float dgp[NC][8], dbp[NC][8];
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dgp[c][j] = dbp[c][j] = 0.f;
   const long r0 = ((long)blockIdx.x * 4 + wave) * rows_per_wave;
-  for (int i = 0; i < rows_per_wave; ++i) {
-    const long m = r0 + i;
-    if (m >= M) break;
-    const float2 st = stats[m];
-    float xh[LN_MAXC][8], gy[LN_MAXC][8];
-    uint32_t neg[LN_MAXC];                           // sl_x: bit j = pre-activation x[j] <= 0
-    float a1 = 0.f, a2 = 0.f;
+  const long r1 = min(M, r0 + rows_per_wave);
+  for (long m0 = r0; m0 < r1; m0 += RP) {
+    const bool two = RP == 2 && m0 + 1 < r1;         // wave-uniform
+    float xh[RP][NC][8], gy[RP][NC][8];
+    uint32_t neg[RP][NC];                             // sl_x: bit j = pre-activation x[j] <= 0
+    float a1[RP], a2[RP];
+    float2 st[RP];
 #pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-      const int cc = lane + 64 * c;
-      if (cc < nc) {
-        float dv[8];
-        ld8bf(s + m * N + 8 * cc, xh[c]);
-        if (dr.sl_x != 0.f) {
-          neg[c] = 0u;
+    for (int u = 0; u < RP; ++u) {
+      a1[u] = a2[u] = 0.f;
+      const long m = two ? m0 + u : m0;               // a lone last row is processed twice, counted once
+      st[u] = stats[m];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int cc = lane + 64 * c;
+        if (cc < nc) {
+          float dv[8];
+          ld8bf(s + m * N + 8 * cc, xh[u][c]);
+          if (dr.sl_x != 0.f) {
+            neg[u][c] = 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              neg[u][c] |= (xh[u][c][j] > 0.f ? 0u : 1u) << j;
+              xh[u][c][j] = (float)(bf16)ln_lrelu(xh[u][c][j], dr.sl_x);
+            }
+          }
+          ld8bf(dy + m * N + 8 * cc, dv);
+          if (dr.th_o) {
+            float mk[8];
+            ln_drop8(dr.base_o, dr.th_o, dr.sc_o, m, cc, mk);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dv[j] *= mk[j];
+          }
+          const bool cnt = u == 0 || two;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            neg[c] |= (xh[c][j] > 0.f ? 0u : 1u) << j;
-            xh[c][j] = (float)(bf16)ln_lrelu(xh[c][j], dr.sl_x);
+            xh[u][c][j] = (xh[u][c][j] - st[u].x) * st[u].y;
+            gy[u][c][j] = dv[j] * g[8 * cc + j];
+            a1[u] += gy[u][c][j];
+            a2[u] += gy[u][c][j] * xh[u][c][j];
+            if (cnt) {
+              dgp[c][j] += dv[j] * xh[u][c][j];
+              dbp[c][j] += dv[j];
+            }
           }
-        }
-        ld8bf(dy + m * N + 8 * cc, dv);
-        if (dr.th_o) {
-          float mk[8];
-          ln_drop8(dr.base_o, dr.th_o, dr.sc_o, m, cc, mk);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dv[j] *= mk[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[c][j] = (xh[c][j] - st.x) * st.y;
-          gy[c][j] = dv[j] * g[8 * cc + j];
-          a1 += gy[c][j];
-          a2 += gy[c][j] * xh[c][j];
-          dgp[c][j] += dv[j] * xh[c][j];
-          dbp[c][j] += dv[j];
         }
       }
     }
-    a1 = wave_sum(a1) / N;
-    a2 = wave_sum(a2) / N;
 #pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-      const int cc = lane + 64 * c;
-      if (cc < nc) {
-        float o[8];
+    for (int u = 0; u < RP; ++u) {
+      a1[u] = wave_sum(a1[u]) / N;
+      a2[u] = wave_sum(a2[u]) / N;
+    }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = st.y * (gy[c][j] - a1 - xh[c][j] * a2);
-        if (dr.sl_x != 0.f) {
-          float dx[8];
+    for (int u = 0; u < RP; ++u) {
+      if (u == 1 && !two) break;
+      const long m = m0 + u;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) dx[j] = ((neg[c] >> j) & 1u) ? o[j] * dr.sl_x : o[j];
-          st8bf(ds + m * N + 8 * cc, dx);
-        } else {
-          st8bf(ds + m * N + 8 * cc, o);
-        }
-        if (dres) {
-          if (dr.th_r) {
-            float mk[8];
-            ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+      for (int c = 0; c < NC; ++c) {
+        const int cc = lane + 64 * c;
+        if (cc < nc) {
+          float o[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+          for (int j = 0; j < 8; ++j) o[j] = st[u].y * (gy[u][c][j] - a1[u] - xh[u][c][j] * a2[u]);
+          if (dr.sl_x != 0.f) {
+            float dx[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dx[j] = ((neg[u][c] >> j) & 1u) ? o[j] * dr.sl_x : o[j];
+            st8bf(ds + m * N + 8 * cc, dx);
+          } else {
+            st8bf(ds + m * N + 8 * cc, o);
           }
-          if (rp) {
-            float rv[8];
-            ld8bf(rp + m * N + 8 * cc, rv);
+          if (dres) {
+            if (dr.th_r) {
+              float mk[8];
+              ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = rv[j] > 0.f ? o[j] : o[j] * dr.sl_r;
+              for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+            }
+            if (rp) {
+              float rv[8];
+              ld8bf(rp + m * N + 8 * cc, rv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = rv[j] > 0.f ? o[j] : o[j] * dr.sl_r;
+            }
+            st8bf(dres + m * N + 8 * cc, o);
           }
-          st8bf(dres + m * N + 8 * cc, o);
         }
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int cc = lane + 64 * c;
     if (cc < nc)
 #pragma unroll
@@ -520,15 +545,22 @@ extern "C" int snvrag_ln_fwd_train_act(int64_t M, int N, const void* x, const vo
   SNV_CHECK_ARG(p_r >= 0.f && p_r < 1.f && p_out >= 0.f && p_out < 1.f, "dropout probabilities must be in [0, 1)");
   SNV_CHECK_ARG(r || p_r == 0.f, "residual dropout without a residual");
   if (M == 0) return 0;
-  hipLaunchKernelGGL(ln_fwd_train_kernel, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N,
-                     (const bf16*)x, (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats,
-                     make_ln_drop(p_r, p_out, seed, slope_x, slope_r));
+  const LnDrop dr = make_ln_drop(p_r, p_out, seed, slope_x, slope_r);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N, (const bf16*)x,
+                       (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats, dr);
+  };
+  const int nch = cdiv(N / 8, 64);
+  if (nch == 1) go(ln_fwd_train_kernel<1>);
+  else if (nch == 2) go(ln_fwd_train_kernel<2>);
+  else if (nch == 3) go(ln_fwd_train_kernel<3>);
+  else go(ln_fwd_train_kernel<4>);
   SNV_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N) {
-  const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
+  const long nblk = std::min<long>(cdiv(M, 4 * LN_BWD_RPW), 2048);
   return (size_t)nblk * 2 * N * sizeof(float);
 }
 
@@ -552,12 +584,21 @@ extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s
   SNV_CHECK_ARG(!dres || p_r > 0.f || slope_r != 0.f, "dres is the residual operand's own gradient");
   if (M == 0) return 0;
   hipStream_t st = as_stream(stream);
-  const long nblk = std::min<long>(cdiv(M, 4 * 16), 2048);
+  const long nblk = std::min<long>(cdiv(M, 4 * LN_BWD_RPW), 2048);
   const int rpw = (int)((M + nblk * 4 - 1) / (nblk * 4));
   float* part = (float*)ws;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nblk), dim3(256), 4 * 2 * N * sizeof(float), st, (long)M, N, rpw,
-                     (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, (bf16*)dres, part,
-                     make_ln_drop(p_r, p_out, seed, slope_x, slope_r), (const bf16*)(slope_r != 0.f ? r_pre : nullptr));
+  const LnDrop dr = make_ln_drop(p_r, p_out, seed, slope_x, slope_r);
+  const bf16* rp = (const bf16*)(slope_r != 0.f ? r_pre : nullptr);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), 4 * 2 * N * sizeof(float), st, (long)M, N, rpw,
+                       (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, (bf16*)dres, part, dr, rp);
+  };
+  const int nch = cdiv(N / 8, 64);
+  // one row per wave step (2 rows: 174 -> 209 us at N = 1536, tools/ln_micro.py)
+  if (nch == 1) go(ln_bwd_kernel<1, 1>);
+  else if (nch == 2) go(ln_bwd_kernel<2, 1>);
+  else if (nch == 3) go(ln_bwd_kernel<3, 1>);
+  else go(ln_bwd_kernel<4, 1>);
   SNV_LAUNCH_CHECK();
   // dg = sum over blocks of part[:, 0, :], db of part[:, 1, :] (written or accumulated)
   hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)part,
