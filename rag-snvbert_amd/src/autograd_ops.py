@@ -366,6 +366,70 @@ def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
     return _HipLinear.apply(x, len(ws), *ws, *bs)
 
 
+class _HipLinearRank2(torch.autograd.Function):
+    """z = Linear(cat([x, c1, c2], -1)) = x W[:, :D]^T + b + c1 W[:, D] + c2 W[:, D + 1] (bf16 out)
+    with the two extra input columns as per-row rank-1 terms in the stream GEMM's epilogue
+    (fusion.py:355-360's cat(emb, pos_feat, af) and foundation_model.py's cat(x, af, af_p)):
+    no [M, N] f32 products and adds in torch.  Backward: dX on the stream / row-panel GEMM,
+    dW[:, :D] and db on the dW kernel, dW[:, D:] = dz^T [c1 c2] and dc = dz W[:, D:] as two
+    skinny products."""
+
+    @staticmethod
+    def forward(ctx, x, c1, c2, W, b):
+        D = x.shape[-1]
+        n_out = W.shape[0]
+        x2 = x.reshape(-1, D).to(torch.bfloat16).contiguous()
+        M = x2.shape[0]
+        r1 = c1.reshape(-1).float().contiguous()
+        r2 = c2.reshape(-1).float().contiguous()
+        assert r1.numel() == M and r2.numel() == M
+        wsp, _ = _sg_stream([W[:, :D]], [b], n_out)
+        vec = K.sgemm_vec(b, W[:, D], W[:, D + 1])                   # [bias | w_c1 | w_c2]
+        z = K.sgemm(x2, wsp, n_out, vec, rank=(r1, r2, M))
+        ctx.save_for_backward(x2, r1, r2, W)
+        ctx.in_shape, ctx.in_dtype, ctx.D = x.shape, x.dtype, D
+        return z.reshape(*x.shape[:-1], n_out)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x2, r1, r2, W = ctx.saved_tensors
+        D, n_out = ctx.D, W.shape[0]
+        g2 = gz.reshape(-1, n_out).to(torch.bfloat16).contiguous()
+        gx = gc1 = gc2 = gW = gb = None
+        wd = W[:, :D]
+        if ctx.needs_input_grad[0]:
+            if _sg_ok(g2, D):
+                wsp, vec = _sg_stream_t(wd, D)
+                gx = K.sgemm(g2, wsp, D, vec)
+            else:
+                gx = K.linear(g2, bf16_of(wd, transposed=True))
+            gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
+        wc = W[:, D:].detach().to(torch.bfloat16)                     # [N, 2]
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            gcc = _mm_f32(g2, wc.contiguous())                         # [M, 2]
+            gc1 = gcc[:, 0].reshape(ctx.in_shape[:-1]) if ctx.needs_input_grad[1] else None
+            gc2 = gcc[:, 1].reshape(ctx.in_shape[:-1]) if ctx.needs_input_grad[2] else None
+        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            gwd, gb = K.linear_dw(g2, x2, bias=True)
+            cc = torch.stack([r1, r2], 1).to(torch.bfloat16)           # [M, 2]
+            gW = torch.cat([gwd, _mm_f32(g2.t(), cc)], 1)
+        return gx, gc1, gc2, gW, gb
+
+
+def hip_linear_rank2(x: torch.Tensor, lin, c1: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
+    """Linear(cat([x, c1[..., None], c2[..., None]], -1)) with nn.Linear ``lin`` [N, D + 2]:
+    the stream GEMM with rank-1 epilogue terms (bf16 out) when D = 384 and N % 64 == 0 and the
+    dW kernel's shapes fit (N % 128 == 0), else the f32 torch form."""
+    D = x.shape[-1]
+    W = lin.weight
+    n_out = W.shape[0]
+    if (train_dtype() == torch.float32 or D != 384 or n_out % 128 or lin.bias is None
+            or os.environ.get("SNVRAG_TRAIN_NO_SG")):
+        y = hip_linear(x, W[:, :D], lin.bias).float()
+        return y + c1.unsqueeze(-1) * W[:, D] + c2.unsqueeze(-1) * W[:, D + 1]
+    return _HipLinearRank2.apply(x, c1, c2, W, lin.bias)
+
+
 class _HipAddLayerNorm(torch.autograd.Function):
     """y = drop_o(LayerNorm(x + drop_r(r))) (r optional) in bf16 with f32 statistics
     (snvrag_ln_fwd_train / snvrag_ln_bwd): one pass each way instead of torch's f32 conversion +

@@ -38,7 +38,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import hip_add_layernorm, hip_attention, hip_linear, rag_mean_train, tiny_embedding, train_dtype
+from .autograd_ops import (hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2, rag_mean_train,
+                           tiny_embedding, train_dtype)
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -107,11 +108,9 @@ def pos_feat(pfm, pos: torch.Tensor, n_updates: int = 1) -> torch.Tensor:
 
 
 def _linear_cat2(x: torch.Tensor, lin, c1: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
-    """Linear(cat([x, c1, c2], -1)) with the two extra input columns as rank-1 terms (f32)."""
-    D = x.shape[-1]
-    W = lin.weight
-    y = hip_linear(x, W[:, :D], lin.bias).float()
-    return y + c1.unsqueeze(-1) * W[:, D] + c2.unsqueeze(-1) * W[:, D + 1]
+    """Linear(cat([x, c1, c2], -1)) with the two extra input columns as rank-1 terms: in the
+    stream GEMM's epilogue (bf16 out, autograd_ops.hip_linear_rank2), or f32 in torch."""
+    return hip_linear_rank2(x, lin, c1, c2)
 
 
 def _ln(x: torch.Tensor, m) -> torch.Tensor:
@@ -126,8 +125,9 @@ def emb_fusion(ef, embs: torch.Tensor, pos: torch.Tensor, af: torch.Tensor, n_ca
     running-statistics updates."""
     pf = pos_feat(ef.pos_feat, pos, n_calls)
     rep = lambda t: t.repeat(n_calls, 1)
-    y = F.leaky_relu(_linear_cat2(embs, ef.fusion, rep(pf), rep(af)), 0.1).to(train_dtype())
-    return hip_add_layernorm(embs, y, ef.norm)
+    # fusion.py:360-366: LeakyReLU(0.1) of the fusion Linear runs inside the LayerNorm kernel
+    y = _linear_cat2(embs, ef.fusion, rep(pf), rep(af)).to(train_dtype())
+    return hip_add_layernorm(embs, y, ef.norm, act_r=0.1)
 
 
 def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p: torch.Tensor, p: float,

@@ -327,6 +327,36 @@ def test_hip_add_layernorm_fused_leaky_relu(M, N, mode):
     assert rel(ln.weight.grad, wr.grad) < 2e-3 and rel(ln.bias.grad, br.grad) < 2e-3
 
 
+@pytest.mark.parametrize("N", [384, 1536])
+def test_hip_linear_rank2_vs_torch(N):
+    """Linear(cat([x, c1, c2])) with the two extra columns as stream-GEMM epilogue rank terms
+    (fusion.py:355-360, the hap head's af_fusion[0]): output and the gradients of x, c1, c2, W and
+    b vs torch f32 autograd of the concatenated form on the same bf16-rounded operands, 1e-2
+    relative (bf16 output and bf16 dz)."""
+    from src.autograd_ops import hip_linear_rank2
+    g = torch.Generator(device="cpu").manual_seed(N)
+    M, D = 2 * 1030 + 6, 384
+    lin = torch.nn.Linear(D + 2, N).to(DEV)
+    x = (torch.randn(M, D, generator=g)).to(DEV, torch.bfloat16).requires_grad_(True)
+    c1 = torch.randn(M, generator=g).to(DEV).requires_grad_(True)
+    c2 = torch.rand(M, generator=g).to(DEV).requires_grad_(True)
+    gz = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    z = hip_linear_rank2(x, lin, c1, c2)
+    assert z.dtype == torch.bfloat16
+    z.backward(gz)
+    xr = x.detach().float().requires_grad_(True)
+    c1r, c2r = c1.detach().clone().requires_grad_(True), c2.detach().clone().requires_grad_(True)
+    Wr = lin.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = lin.bias.detach().clone().requires_grad_(True)
+    zr = torch.nn.functional.linear(torch.cat([xr, c1r[:, None], c2r[:, None]], -1), Wr, br)
+    zr.backward(gz.float())
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()
+    assert rel(z, zr.detach()) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(c1.grad, c1r.grad) < 1e-2 and rel(c2.grad, c2r.grad) < 1e-2
+    assert rel(lin.weight.grad, Wr.grad) < 1e-2 and rel(lin.bias.grad, br.grad) < 1e-2
+
+
 def test_focal_loss_kernel_vs_oracle_and_reference():
     from src import kernels as K
     z = load_golden("focal")

@@ -1,0 +1,34 @@
+"""torch.profiler over the bench's training step (B = 24, window 512, d384/L12): the ATen ops
+(and the HIP-kernel autograd nodes) by device time, to find the elementwise work left outside the
+hand-written kernels."""
+import os
+import sys
+
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [REPO, os.path.join(REPO, "rag-snvbert_amd")]
+from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn  # noqa: E402
+from src.dataset.synthetic import make_rag_dataset  # noqa: E402
+from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized  # noqa: E402
+from src.model import build_model  # noqa: E402
+
+dev = torch.device("cuda")
+ds, vocab = make_rag_dataset(n_samples=24, n_sites=512, n_windows=1, n_ref_samples=5000, seed=7, name="train")
+batch = embedding_rag_collate_fn([ds[i] for i in range(24)])
+torch.manual_seed(0)
+model = build_model(len(vocab), 384, 12, 12).to(dev)
+tr = BERTTrainerWithValidationOptimized(model, None, None, vocab, lr=7.5e-5, warmup_steps=100, grad_accum_steps=1,
+                                        log_freq=0)
+tr.rag_train_dataset = ds
+tr.rag_k = 8
+for _ in range(2):
+    tr.train_step(dict(batch))
+torch.cuda.synchronize()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    for _ in range(3):
+        tr.train_step(dict(batch))
+    torch.cuda.synchronize()
+print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45,
+                                                           max_name_column_width=40, max_shapes_column_width=60))
