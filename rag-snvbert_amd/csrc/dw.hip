@@ -18,6 +18,8 @@
 // staged, double buffered (the next stage's loads in flight under this stage's MFMAs).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace snvrag {
 
 constexpr int DW_T = 128;                 // output tile (n and k)
@@ -152,6 +154,152 @@ __global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16
   }
 }
 
+// dw_dma_kernel: the same tiles, fragments and epilogue with the 32-row stages brought in by
+// LDS-DMA (buffer_load ... lds, 1 KiB = 4 rows of one operand per wave instruction) through a
+// 4-slot ring, 3 stages in flight, one barrier per stage.  The register-staged kernel above moves
+// every operand byte through VGPRs and a ds_write_b128 (≈79 B/clk/CU of LDS store transfer) with
+// one stage of look-ahead; here the XOR swizzle of dw_swz is applied to the SOURCE column of each
+// lane (the LDS side of a DMA piece is contiguous) and rows past the chunk read the buffer's zeros.
+constexpr int DWD_NS = 4;
+
+__global__ __launch_bounds__(256) void dw_dma_kernel(int M, int N, int K, const bf16* __restrict__ dy, long ldy,
+                                                     const bf16* __restrict__ x, long ldx, DwOut out, int chunk) {
+  // one __shared__ object per ring slot: the compiler's LDS-DMA wait tracking then knows that a
+  // stage's ds_reads do not alias the DMA just issued into another slot (with one array it puts a
+  // vmcnt(0) before every read, draining the whole ring each stage)
+  __shared__ __attribute__((aligned(16))) char sl0[DW_STAGE], sl1[DW_STAGE], sl2[DW_STAGE], sl3[DW_STAGE];
+  static_assert(DWD_NS == 4, "four slot objects");
+  auto slot_ptr = [&](int i) -> char* { return i == 0 ? sl0 : i == 1 ? sl1 : i == 2 ? sl2 : sl3; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
+  const int part = n0 / out.seg;
+  const int nbase = part * out.seg;
+  float* __restrict__ dw = out.w[part];
+  float* __restrict__ db = out.b[part];
+  const int m_begin = blockIdx.z * chunk;
+  const int m_end = min(M, m_begin + chunk);
+  if (m_begin >= m_end) return;                      // whole workgroup, before any barrier
+  const int nst = (m_end - m_begin + DW_R - 1) / DW_R;
+
+  // sources: this chunk's rows only (the resource ends at m_end: later rows read zeros)
+  const long rows = m_end - m_begin;
+  const long by = (rows - 1) * ldy * 2 + (long)DW_T * 2, bx = (rows - 1) * ldx * 2 + (long)DW_T * 2;
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dy + (long)m_begin * ldy + n0), (short)0, (int)(by < 0x7fffffffL ? by : 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + (long)m_begin * ldx + k0), (short)0, (int)(bx < 0x7fffffffL ? bx : 0x7fffffffL), 0x00020000);
+  // piece j (0..7) of an operand = rows 4 j .. 4 j + 3; wave w issues pieces 2 w, 2 w + 1 of dY and
+  // of X.  Lane l lands at byte 16 l of the piece: row 4 j + l / 16, 16-B unit u = l % 16 of the
+  // 256-B row, i.e. 32-B block u / 2 which dw_swz fills from column block (u / 2) ^ (row & 7)
+  int voy[2], vox[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = 2 * wave + i, row = 4 * j + (lane >> 4), u = lane & 15;
+    const int cb = (((u >> 1) ^ (row & 7)) << 5) + ((u & 1) << 4);     // source byte within the row
+    voy[i] = (int)(row * ldy * 2) + cb;
+    vox[i] = (int)(row * ldx * 2) + cb;
+  }
+  const int sty = (int)(DW_R * ldy * 2), stx = (int)(DW_R * ldx * 2);
+  auto issue = [&](int st, int slot) __attribute__((always_inline)) {
+    char* s = slot_ptr(slot);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * wave + i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) char*)(s + j * 1024), 16,
+                                               voy[i], st * sty, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) char*)(s + DW_R * 256 + j * 1024),
+                                               16, vox[i], st * stx, 0, 0);
+    }
+  };
+  auto wait = [&](int y) {                           // 4 DMA per stage per wave
+    if (y >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (y == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int rowb = 8 * (g >> 1) + q;
+  const int colb = 2 * (16 * (g & 1) + 4 * p);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  const bool do_db = db != nullptr && blockIdx.y == 0 && wk == 0;
+  float dbs[2] = {0.f, 0.f};
+  auto compute = [&](const char* s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r0 = 16 * ks + rowb;
+        const int ca = 128 * wn + 64 * t + colb;
+        const int cb = 128 * wk + 64 * t + colb;
+        const bf16x4 a0 = dw_tr(s + dw_swz(r0, ca)), a1 = dw_tr(s + dw_swz(r0 + 4, ca));
+        const bf16x4 b0 = dw_tr(s + DW_R * 256 + dw_swz(r0, cb)), b1 = dw_tr(s + DW_R * 256 + dw_swz(r0 + 4, cb));
+        fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      if (do_db) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dbs[a] += (float)fa[a][j];
+      }
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < DWD_NS - 1; ++j)
+    if (j < nst) issue(j, j);
+  int st = 0;
+  for (; st + DWD_NS <= nst; st += DWD_NS) {
+#pragma unroll
+    for (int u = 0; u < DWD_NS; ++u) {
+      wait(min(DWD_NS - 2, nst - 1 - (st + u)));
+      __builtin_amdgcn_s_barrier();
+      if (st + u + DWD_NS - 1 < nst) issue(st + u + DWD_NS - 1, (u + DWD_NS - 1) % DWD_NS);
+      compute(slot_ptr(u));
+    }
+  }
+  for (; st < nst; ++st) {
+    wait(min(DWD_NS - 2, nst - 1 - st));
+    __builtin_amdgcn_s_barrier();
+    if (st + DWD_NS - 1 < nst) issue(st + DWD_NS - 1, (st + DWD_NS - 1) % DWD_NS);
+    switch (st % DWD_NS) {                           // compile-time slot objects
+      case 0: compute(sl0); break;
+      case 1: compute(sl1); break;
+      case 2: compute(sl2); break;
+      default: compute(sl3); break;
+    }
+  }
+
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int kk = k0 + 64 * wk + 32 * b + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int nn = n0 + 64 * wn + 32 * a + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+        unsafeAtomicAdd(dw + (long)(nn - nbase) * K + kk, acc[a][b][e]);
+      }
+    }
+  if (do_db) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const float v = dbs[a] + __shfl_xor(dbs[a], 32, 64);
+      if (lane < 32) unsafeAtomicAdd(db + (n0 - nbase) + 64 * wn + 32 * a + lane, v);
+    }
+  }
+}
+
 }  // namespace snvrag
 
 using namespace snvrag;
@@ -177,8 +325,12 @@ static int launch_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ld
   const int chunk = (int)((((M + splits - 1) / splits) + DW_R - 1) / DW_R * DW_R);
   const int S = (int)((M + chunk - 1) / chunk);
   evlog_begin(s);
-  hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
-                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
+  if (getenv("SNVRAG_DW_V1"))                         // A/B: the register-staged kernel
+    hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
+                       (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
+  else
+    hipLaunchKernelGGL(dw_dma_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0,
+                       s, (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
   SNV_LAUNCH_CHECK();
   evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
   return 0;
