@@ -404,15 +404,23 @@ class _HipLinearRank2(torch.autograd.Function):
             else:
                 gx = K.linear(g2, bf16_of(wd, transposed=True))
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
-        wc = W[:, D:].detach().to(torch.bfloat16)                     # [N, 2]
+        M = g2.shape[0]
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            gcc = _mm_f32(g2, wc.contiguous())                         # [M, 2]
+            # dc = dz W[:, D:] on the row-panel GEMM, the two columns padded to 8 outputs
+            wc = torch.zeros(8, n_out, device=g2.device, dtype=torch.bfloat16)
+            wc[:2] = W[:, D:].detach().t().to(torch.bfloat16)
+            gcc = K.linear(g2, wc, out_dtype=torch.float32)            # [M, 8]
             gc1 = gcc[:, 0].reshape(ctx.in_shape[:-1]) if ctx.needs_input_grad[1] else None
             gc2 = gcc[:, 1].reshape(ctx.in_shape[:-1]) if ctx.needs_input_grad[2] else None
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            # dW[:, :D] and db, then dW[:, D:] = dz^T [c1 c2] on the same dW kernel with the two row
+            # columns padded to one 128-wide operand (skinny library GEMMs over M took ~0.3 ms each)
             gwd, gb = K.linear_dw(g2, x2, bias=True)
-            cc = torch.stack([r1, r2], 1).to(torch.bfloat16)           # [M, 2]
-            gW = torch.cat([gwd, _mm_f32(g2.t(), cc)], 1)
+            cc = torch.zeros(M, 128, device=g2.device, dtype=torch.bfloat16)
+            cc[:, 0] = r1
+            cc[:, 1] = r2
+            gwc, _ = K.linear_dw(g2, cc)
+            gW = torch.cat([gwd, gwc[:, :2]], 1)
         return gx, gc1, gc2, gW, gb
 
 

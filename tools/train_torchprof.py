@@ -32,3 +32,9 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_sh
     torch.cuda.synchronize()
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45,
                                                            max_name_column_width=40, max_shapes_column_width=60))
+# ATen ops only (the Python-level torch work left around the HIP kernels), by device time incl. children
+rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key.startswith("aten::")]
+rows.sort(key=lambda e: -e.device_time_total)
+print("\nATen ops by device time (ms per step, calls per step, shapes)")
+for e in rows[:60]:
+    print(f"{e.device_time_total / 3e3:8.3f} ms {e.count / 3:6.1f}  {e.key:28s} {str(e.input_shapes)[:110]}")
