@@ -444,6 +444,20 @@ int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s, const flo
                       void* ds, void* dres, const void* r_pre, float* dg, float* db, int accumulate, float p_r,
                       float p_out, uint64_t seed, float slope_x, float slope_r, void* ws, size_t ws_bytes,
                       void* stream);
+/* Train-mode neighbour mean with the reference's dropout semantics (embedding_rag_dataset.py:
+ * 404-417, bert.py:176-179): out[q, l] = mean over q's valid neighbours j of
+ * drop(W[tok(u, l)] + pe[l] + Ar[l]), u = inv[q, j] (< 0: none) indexing the window's unique
+ * neighbours (their allele codes [U, ld_codes]); one dropout mask per unique neighbour (counter-
+ * based hash of seed, u, l, feature pair), never materialising the [U, L, D] embeddings.  The
+ * backward ACCUMULATES dW [V, D] (not the <pad> row) and dAr [L, D]. */
+int snvrag_nbr_mean_drop_fwd(int64_t nq, int k, int64_t L, int D, int n_sites, int64_t ld_codes, int V,
+                             const int32_t* inv, const uint8_t* codes, const float* W, const float* pe,
+                             const float* Ar, float p, uint64_t seed, int tok0, int sos, int eos, int pad,
+                             float* out, void* stream);
+int snvrag_nbr_mean_drop_bwd(int64_t nq, int k, int64_t L, int D, int n_sites, int64_t ld_codes, int V,
+                             const int32_t* inv, const uint8_t* codes, const float* W, const float* pe,
+                             const float* Ar, float p, uint64_t seed, int tok0, int sos, int eos, int pad,
+                             const float* dout, float* dW, float* dAr, void* stream);
 size_t snvrag_ln_bwd_ws_bytes(int64_t M, int N);
 int snvrag_ln_bwd(int64_t M, int N, const void* dy, const void* s, const float* stats, const float* g,
                   void* ds, void* dres, float* dg, float* db, int accumulate, float p_r, float p_out,

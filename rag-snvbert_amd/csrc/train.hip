@@ -526,6 +526,136 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(long M, int N, int row
     part[(long)blockIdx.x * N + n] = s;
   }
 }
+// ---------------------------------------------------------------------------------------------
+// Train-mode neighbour mean with the reference's dropout semantics (embedding_rag_dataset.py:
+// 404-417 + bert.py:176-179): every UNIQUE retrieved haplotype u of a window is re-encoded once,
+//   E[u, l] = drop_u,l( W[tok(u, l)] + pe[l] + Ar[l] ),   tok = <sos> | tok0 + code[u][l-1] | <eos> | <pad>,
+// and query q takes the mean over its valid neighbours: out[q, l] = (1 / nv_q) sum_j E[inv[q, j], l].
+// Fused: E is never materialised ([U, L, D] f32 is ~0.6 GB at B = 24, k = 8); every (query,
+// neighbour, position, feature) recomputes the embedding from the 10-row table and the dropout
+// keep bit from a counter-based hash of (seed, u, l, d pair) — the same bits in the backward,
+//   dW[tok(u, l)] += g,  dAr[l] += g,  g = dout[q, l] / nv_q * keep / (1 - p),
+// which accumulates per thread over its (l, d) and per token row with one atomic per block.
+struct NbrArgs {
+  int nq, k, L, D, n_sites, ld_codes, V;
+  const int* inv;               // [nq, k] unique-neighbour index, < 0: no neighbour
+  const uint8_t* codes;         // [U, ld_codes] allele codes of the unique neighbours
+  const float* W;               // [V, D] token table (f32)
+  const float* pe;              // [L, D]
+  const float* Ar;              // [L, D]
+  uint32_t thresh, base;        // keep iff hash half >= thresh (thresh 0: no dropout)
+  float scale;                  // 1 / (1 - p)
+  int tok0, sos, eos, pad;
+};
+
+__device__ __forceinline__ int nbr_tok(const NbrArgs& a, int u, int l) {
+  if (l == 0) return a.sos;
+  if (l <= a.n_sites) return a.tok0 + a.codes[(long)u * a.ld_codes + l - 1];
+  return l == a.n_sites + 1 ? a.eos : a.pad;
+}
+// keep multipliers (0 or scale) of features d, d + 1 (d even) of (u, l)
+__device__ __forceinline__ void nbr_keep2(const NbrArgs& a, int u, int l, int d, float& m0, float& m1) {
+  if (!a.thresh) { m0 = m1 = 1.f; return; }
+  const uint32_t h = drop_mix24(a.base + (uint32_t)u * DROP_C1 + (uint32_t)((l * a.D + d) >> 1) * DROP_C2);
+  m0 = (h & 0xFFFFu) >= a.thresh ? a.scale : 0.f;
+  m1 = (h >> 16) >= a.thresh ? a.scale : 0.f;
+}
+
+// grid (L, nq / 4): block = 4 queries x D / 2 feature pairs (threads: pair index, query)
+__global__ __launch_bounds__(256) void nbr_mean_drop_fwd_kernel(NbrArgs a, float* __restrict__ out) {
+  const int l = blockIdx.x, npair = a.D >> 1;
+  const int pidx = threadIdx.x % 64, qs = threadIdx.x / 64;
+  for (int q = blockIdx.y * 4 + qs; q < a.nq; q += gridDim.y * 4) {
+    int nv = 0;
+    for (int j = 0; j < a.k; ++j) nv += a.inv[q * a.k + j] >= 0;
+    const float inv_nv = 1.f / (float)max(nv, 1);
+    for (int pp = pidx; pp < npair; pp += 64) {
+      const int d = 2 * pp;
+      const float c0 = a.pe[(long)l * a.D + d] + a.Ar[(long)l * a.D + d];
+      const float c1 = a.pe[(long)l * a.D + d + 1] + a.Ar[(long)l * a.D + d + 1];
+      float s0 = 0.f, s1 = 0.f;
+      for (int j = 0; j < a.k; ++j) {
+        const int u = a.inv[q * a.k + j];
+        if (u < 0) continue;
+        const int t = nbr_tok(a, u, l);
+        float m0, m1;
+        nbr_keep2(a, u, l, d, m0, m1);
+        s0 = fmaf(m0, a.W[(long)t * a.D + d] + c0, s0);
+        s1 = fmaf(m1, a.W[(long)t * a.D + d + 1] + c1, s1);
+      }
+      float* o = out + ((long)q * a.L + l) * a.D + d;
+      o[0] = s0 * inv_nv;
+      o[1] = s1 * inv_nv;
+    }
+  }
+}
+
+// grid (cdiv(L, LB)): block = LB positions x D / 2 feature pairs; thread (pair, position group)
+// loops its positions, every query and neighbour; dAr[l] is owned by one thread (accumulated in
+// place), dW rows get one atomic per (block, token row, feature)
+constexpr int NBR_LB = 4;
+__global__ __launch_bounds__(256) void nbr_mean_drop_bwd_kernel(NbrArgs a, const float* __restrict__ dout,
+                                                                float* __restrict__ dW, float* __restrict__ dAr) {
+  extern __shared__ float wacc[];                    // [V][D] block partials of dW
+  const int npair = a.D >> 1;
+  for (int i = threadIdx.x; i < a.V * a.D; i += blockDim.x) wacc[i] = 0.f;
+  __syncthreads();
+  const int pidx = threadIdx.x % 64, lgp = threadIdx.x / 64;    // 4 position groups
+  for (int pp = pidx; pp < npair; pp += 64) {
+    const int d = 2 * pp;
+    for (int li = lgp; li < NBR_LB; li += 4) {
+      const int l = blockIdx.x * NBR_LB + li;
+      if (l >= a.L) break;
+      float ar0 = 0.f, ar1 = 0.f;
+      float w0[2] = {0.f, 0.f}, w1[2] = {0.f, 0.f};  // the two site tokens (tok0, tok0 + 1)
+      float ws0 = 0.f, ws1 = 0.f;                     // the position's single token (sos / eos / pad)
+      const bool site = l >= 1 && l <= a.n_sites;
+      for (int q = 0; q < a.nq; ++q) {
+        int nv = 0;
+        for (int j = 0; j < a.k; ++j) nv += a.inv[q * a.k + j] >= 0;
+        if (nv == 0) continue;
+        const float* g = dout + ((long)q * a.L + l) * a.D + d;
+        const float g0 = g[0] / (float)nv, g1 = g[1] / (float)nv;
+        for (int j = 0; j < a.k; ++j) {
+          const int u = a.inv[q * a.k + j];
+          if (u < 0) continue;
+          float m0, m1;
+          nbr_keep2(a, u, l, d, m0, m1);
+          const float e0 = g0 * m0, e1 = g1 * m1;
+          ar0 += e0;
+          ar1 += e1;
+          if (site) {
+            const int c = a.codes[(long)u * a.ld_codes + l - 1] & 1;
+            w0[c] += e0;
+            w1[c] += e1;
+          } else {
+            ws0 += e0;
+            ws1 += e1;
+          }
+        }
+      }
+      dAr[(long)l * a.D + d] += ar0;
+      dAr[(long)l * a.D + d + 1] += ar1;
+      if (site) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          atomicAdd(&wacc[(a.tok0 + c) * a.D + d], w0[c]);
+          atomicAdd(&wacc[(a.tok0 + c) * a.D + d + 1], w1[c]);
+        }
+      } else {
+        const int t = l == 0 ? a.sos : (l == a.n_sites + 1 ? a.eos : a.pad);
+        if (t != a.pad) {                              // nn.Embedding(padding_idx = <pad>): no gradient
+          atomicAdd(&wacc[t * a.D + d], ws0);
+          atomicAdd(&wacc[t * a.D + d + 1], ws1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.V * a.D; i += blockDim.x)
+    if (wacc[i] != 0.f) unsafeAtomicAdd(dW + i, wacc[i]);
+}
+
 }  // namespace snvrag
 
 extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
@@ -627,6 +757,50 @@ extern "C" int snvrag_colsum_bf16(int64_t M, int N, const void* x, float* out, v
   SNV_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)ws, out,
                      0);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+static int nbr_args(NbrArgs& a, int64_t nq, int k, int64_t L, int D, int n_sites, int64_t ld_codes, int V,
+                    const int32_t* inv, const uint8_t* codes, const float* W, const float* pe, const float* Ar,
+                    float p, uint64_t seed, int tok0, int sos, int eos, int pad) {
+  SNV_CHECK_ARG(inv && codes && W && pe && Ar, "null pointer");
+  SNV_CHECK_ARG(D % 2 == 0 && D <= 2048 && V >= 1 && V * D <= 16384, "D even, V x D <= 16384");
+  SNV_CHECK_ARG(n_sites + 2 <= L && ld_codes >= n_sites && k >= 1, "shape");
+  SNV_CHECK_ARG(p >= 0.f && p < 1.f, "dropout probability must be in [0, 1)");
+  SNV_CHECK_ARG(tok0 >= 0 && tok0 + 1 < V && sos < V && eos < V && pad < V, "token ids");
+  const AttnDrop dr = make_attn_drop(p, seed);
+  a = NbrArgs{(int)nq, k, (int)L, D, n_sites, (int)ld_codes, V, inv, codes, W, pe, Ar, dr.thresh,
+              drop_base(seed, 7u), dr.scale, tok0, sos, eos, pad};
+  return 0;
+}
+
+extern "C" int snvrag_nbr_mean_drop_fwd(int64_t nq, int k, int64_t L, int D, int n_sites, int64_t ld_codes, int V,
+                                        const int32_t* inv, const uint8_t* codes, const float* W, const float* pe,
+                                        const float* Ar, float p, uint64_t seed, int tok0, int sos, int eos, int pad,
+                                        float* out, void* stream) {
+  NbrArgs a;
+  if (int rc = nbr_args(a, nq, k, L, D, n_sites, ld_codes, V, inv, codes, W, pe, Ar, p, seed, tok0, sos, eos, pad))
+    return rc;
+  SNV_CHECK_ARG(out, "null pointer");
+  if (nq == 0) return 0;
+  const unsigned gy = (unsigned)std::min<int64_t>((nq + 3) / 4, 64);
+  hipLaunchKernelGGL(nbr_mean_drop_fwd_kernel, dim3((unsigned)L, gy), dim3(256), 0, as_stream(stream), a, out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_nbr_mean_drop_bwd(int64_t nq, int k, int64_t L, int D, int n_sites, int64_t ld_codes, int V,
+                                        const int32_t* inv, const uint8_t* codes, const float* W, const float* pe,
+                                        const float* Ar, float p, uint64_t seed, int tok0, int sos, int eos, int pad,
+                                        const float* dout, float* dW, float* dAr, void* stream) {
+  NbrArgs a;
+  if (int rc = nbr_args(a, nq, k, L, D, n_sites, ld_codes, V, inv, codes, W, pe, Ar, p, seed, tok0, sos, eos, pad))
+    return rc;
+  SNV_CHECK_ARG(dout && dW && dAr, "null pointer");
+  if (nq == 0) return 0;
+  hipLaunchKernelGGL(nbr_mean_drop_bwd_kernel, dim3((unsigned)cdiv(L, NBR_LB)), dim3(256),
+                     (size_t)V * D * sizeof(float), as_stream(stream), a, dout, dW, dAr);
   SNV_LAUNCH_CHECK();
   return 0;
 }

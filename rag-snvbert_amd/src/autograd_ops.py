@@ -438,6 +438,37 @@ def hip_linear_rank2(x: torch.Tensor, lin, c1: torch.Tensor, c2: torch.Tensor) -
     return _HipLinearRank2.apply(x, c1, c2, W, lin.bias)
 
 
+class _NbrMeanDrop(torch.autograd.Function):
+    """The train-mode neighbour K-mean with the reference's per-unique-neighbour dropout
+    (embedding_rag_dataset.py:404-417): K.nbr_mean_drop / nbr_mean_drop_bwd, differentiable in the
+    token table W and the panel AF embedding Ar (the mask regenerated from its seed)."""
+
+    @staticmethod
+    def forward(ctx, W, Ar, inv, codes, n_sites, pe, p, seed):
+        Wf, Arf = W.detach().float().contiguous(), Ar.detach().float().contiguous()
+        out = K.nbr_mean_drop(inv, codes, n_sites, Wf, pe, Arf, p, seed)
+        ctx.save_for_backward(inv, codes, Wf, pe, Arf)
+        ctx.cfg = (n_sites, p, seed, W.dtype, Ar.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        inv, codes, Wf, pe, Arf = ctx.saved_tensors
+        n_sites, p, seed, wdt, adt = ctx.cfg
+        dW = torch.zeros_like(Wf)
+        dAr = torch.zeros_like(Arf)
+        K.nbr_mean_drop_bwd(g.contiguous(), inv, codes, n_sites, Wf, pe, Arf, p, seed, dW, dAr)
+        return dW.to(wdt), dAr.to(adt), None, None, None, None, None, None
+
+
+def nbr_mean_drop(W, Ar, inv, codes, n_sites: int, pe, p: float) -> torch.Tensor:
+    """f32 [nq, L, D] neighbour means of the unique neighbours ``inv`` [nq, k] (int, < 0: none,
+    codes [U, ld] u8) under dropout p: one fused HIP launch each way instead of the [U, L, D]
+    embeddings, their dropout and a [nq, U] x [U, L D] product."""
+    return _NbrMeanDrop.apply(W, Ar, inv.to(torch.int32).contiguous(), codes.contiguous(), int(n_sites),
+                              pe.float().contiguous(), float(p), _drop_seed())
+
+
 class _HipAddLayerNorm(torch.autograd.Function):
     """y = drop_o(LayerNorm(x + drop_r(r))) (r optional) in bf16 with f32 statistics
     (snvrag_ln_fwd_train / snvrag_ln_bwd): one pass each way instead of torch's f32 conversion +

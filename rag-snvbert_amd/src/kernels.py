@@ -599,6 +599,36 @@ def ln_bwd(dy: torch.Tensor, s: torch.Tensor, stats: torch.Tensor, g: torch.Tens
     return ds, dres, dg, db
 
 
+def nbr_mean_drop(inv: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor, pe: torch.Tensor,
+                  Ar: torch.Tensor, p: float, seed: int, tok0: int = 5, sos: int = 2, eos: int = 3,
+                  pad: int = 0) -> torch.Tensor:
+    """f32 [nq, L, D]: each query's mean over its valid unique neighbours inv [nq, k] (int32, < 0:
+    none) of drop(W[tok] + pe + Ar), one dropout mask per unique neighbour (csrc/train.hip)."""
+    N.require_gpu(inv, codes, W)
+    nq, k = inv.shape
+    L, D = pe.shape
+    out = torch.empty(nq, L, D, device=W.device, dtype=torch.float32)
+    check(N.lib().snvrag_nbr_mean_drop_fwd(nq, k, L, D, n_sites, codes.shape[1], W.shape[0], ptr(_c(inv)),
+                                           ptr(_c(codes)), ptr(_c(W)), ptr(_c(pe)), ptr(_c(Ar)), float(p),
+                                           int(seed) & (2 ** 64 - 1), tok0, sos, eos, pad, ptr(out), stream_ptr()),
+          "nbr_mean_drop_fwd")
+    return out
+
+
+def nbr_mean_drop_bwd(dout: torch.Tensor, inv: torch.Tensor, codes: torch.Tensor, n_sites: int, W: torch.Tensor,
+                      pe: torch.Tensor, Ar: torch.Tensor, p: float, seed: int, dW: torch.Tensor, dAr: torch.Tensor,
+                      tok0: int = 5, sos: int = 2, eos: int = 3, pad: int = 0) -> None:
+    """Accumulates dW [V, D] and dAr [L, D] (f32) of :func:`nbr_mean_drop` for dout [nq, L, D] f32."""
+    nq, k = inv.shape
+    L, D = pe.shape
+    assert dW.dtype == dAr.dtype == torch.float32 and dW.is_contiguous() and dAr.is_contiguous()
+    check(N.lib().snvrag_nbr_mean_drop_bwd(nq, k, L, D, n_sites, codes.shape[1], W.shape[0], ptr(_c(inv)),
+                                           ptr(_c(codes)), ptr(_c(W)), ptr(_c(pe)), ptr(_c(Ar)), float(p),
+                                           int(seed) & (2 ** 64 - 1), tok0, sos, eos, pad,
+                                           ptr(_c(dout.float())), ptr(dW), ptr(dAr), stream_ptr()),
+          "nbr_mean_drop_bwd")
+
+
 def linear_dw(dy: torch.Tensor, x: torch.Tensor, bias: bool = False, splits: int = 0,
               dw: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
     """dW f32 [N, K] += dy^T x and (bias) db f32 [N] += column sums of dy, for bf16 dy [M, N] and

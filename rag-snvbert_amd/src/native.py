@@ -144,6 +144,10 @@ _SIGS = {
     "snvrag_sgemm_forward": ([i64, C.c_int, C.c_int, C.c_int, C.c_int, f32, vp, vp, vp, vp, vp, i64, f32, vp, vp, vp,
                               vp], C.c_int),
     "snvrag_ln_fwd_train": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, f32, f32, C.c_uint64, vp], C.c_int),
+    "snvrag_nbr_mean_drop_fwd": ([i64, C.c_int, i64, C.c_int, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, f32,
+                                  C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp], C.c_int),
+    "snvrag_nbr_mean_drop_bwd": ([i64, C.c_int, i64, C.c_int, C.c_int, i64, C.c_int, vp, vp, vp, vp, vp, f32,
+                                  C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp], C.c_int),
     "snvrag_ln_fwd_train_act": ([i64, C.c_int, vp, vp, vp, vp, f32, vp, vp, vp, f32, f32, C.c_uint64, f32, f32, vp],
                                 C.c_int),
     "snvrag_ln_bwd_act": ([i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, f32, f32, C.c_uint64, f32, f32,

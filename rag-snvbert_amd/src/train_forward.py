@@ -38,8 +38,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import (hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2, rag_mean_train,
-                           tiny_embedding, train_dtype)
+from .autograd_ops import (hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2, nbr_mean_drop,
+                           rag_mean_train, tiny_embedding, train_dtype)
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -273,6 +273,10 @@ def _unique_neighbour_embed(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor
         uniq, inv = torch.unique(idx.clamp(min=0), return_inverse=True)
         rows_codes = g.index.codes[uniq - g.index.ref_offset]
     U = uniq.numel()
+    if not dense and train_dtype() != torch.float32 and W.shape[0] * W.shape[1] <= 16384:
+        # fused: no [U, L, D] embeddings, one dropout mask per unique neighbour (csrc/train.hip)
+        inv_v = torch.where(valid, inv, torch.full_like(inv, -1))
+        return nbr_mean_drop(W, Ar, inv_v, rows_codes[:, :n_sites], n_sites, pe[:L], p)
     tok = torch.full((U, L), pad, device=idx.device, dtype=torch.long)
     tok[:, 0] = sos
     if n_sites + 1 < L:

@@ -357,6 +357,63 @@ def test_hip_linear_rank2_vs_torch(N):
     assert rel(lin.weight.grad, Wr.grad) < 1e-2 and rel(lin.bias.grad, br.grad) < 1e-2
 
 
+def test_fused_neighbour_mean_dropout_vs_torch():
+    """K.nbr_mean_drop (train-mode neighbour K-mean, one dropout mask per unique neighbour,
+    embedding_rag_dataset.py:404-417): p = 0 equals the torch form (embed the unique neighbours,
+    average per query) at 1e-5; with p = 0.3 the kept fraction is 0.7 and the mean is unbiased, and
+    the backward is the exact adjoint of the (linear in W, Ar) forward under the same mask:
+    <f(W + dW, Ar + dA) - f(W, Ar), R> = <gW(R), dW> + <gAr(R), dA>."""
+    from src import kernels as K
+    g = torch.Generator(device="cpu").manual_seed(11)
+    nq, k, U, L, D, n = 12, 8, 40, 300, 64, 290
+    inv = torch.randint(0, U, (nq, k), generator=g).to(torch.int32)
+    inv[3, 5:] = -1
+    codes = torch.randint(0, 2, (U, n), generator=g).to(torch.uint8)
+    W = torch.randn(10, D, generator=g)
+    W[0] = 0
+    pe = torch.randn(L, D, generator=g) * 0.1
+    Ar = torch.randn(L, D, generator=g) * 0.1
+    d = lambda t: t.to(DEV)
+    # torch reference at p = 0
+    tok = torch.zeros(U, L, dtype=torch.long)
+    tok[:, 0] = 2
+    tok[:, n + 1] = 3
+    tok[:, 1:1 + n] = 5 + codes.long()
+    E = W[tok] + pe + Ar                                   # [U, L, D]
+    ref = torch.stack([E[inv[q][inv[q] >= 0].long()].mean(0) for q in range(nq)])
+    out0 = K.nbr_mean_drop(d(inv), d(codes), n, d(W), d(pe), d(Ar), 0.0, 1)
+    torch.testing.assert_close(out0.cpu(), ref, rtol=1e-5, atol=1e-5)
+    # dropout: keep rate and unbiasedness (each element is kept-and-scaled or 0)
+    p = 0.3
+    outs = torch.stack([K.nbr_mean_drop(d(inv), d(codes), n, d(W), d(pe), d(Ar), p, s) for s in range(24)])
+    assert abs((outs.mean(0).cpu() - ref).abs().mean().item()) < 0.1 * ref.abs().mean().item()
+    one = K.nbr_mean_drop(d(inv[:, :1].contiguous()), d(codes), n, d(W), d(pe), d(Ar), p, 5).cpu()
+    base = E[inv[:, 0].long()]
+    kept = (one != 0) & (base != 0)
+    assert abs(kept.float().sum().item() / (base != 0).sum().item() - (1 - p)) < 0.01
+    torch.testing.assert_close(one[kept], (base / (1 - p))[kept], rtol=1e-5, atol=1e-5)
+    # adjoint identity under one fixed mask
+    R = torch.randn(nq, L, D, generator=g)
+    dW0 = torch.randn(10, D, generator=g) * 0.01
+    dA0 = torch.randn(L, D, generator=g) * 0.01
+    f0 = K.nbr_mean_drop(d(inv), d(codes), n, d(W), d(pe), d(Ar), p, 9).cpu().double()
+    f1 = K.nbr_mean_drop(d(inv), d(codes), n, d(W + dW0), d(pe), d(Ar + dA0), p, 9).cpu().double()
+    gW = torch.zeros(10, D, device=DEV)
+    gA = torch.zeros(L, D, device=DEV)
+    K.nbr_mean_drop_bwd(d(R), d(inv), d(codes), n, d(W), d(pe), d(Ar), p, 9, gW, gA)
+    gW = gW.cpu().double()
+    gW[0] = 0                                              # <pad>: no gradient (padding_idx)
+    dW_nopad = dW0.double().clone()
+    dW_nopad[0] = 0
+    lhs = ((f1 - f0) * R.double()).sum().item()
+    rhs = (gW * dW_nopad).sum().item() + (gA.cpu().double() * dA0.double()).sum().item()
+    # the <pad> row enters the forward (W[0]) but gets no gradient: exclude its contribution
+    pad_part = K.nbr_mean_drop(d(inv), d(codes), n, d(W + torch.cat([dW0[:1], torch.zeros(9, D)])), d(pe),
+                               d(Ar), p, 9).cpu().double()
+    lhs -= ((pad_part - f0) * R.double()).sum().item()
+    assert abs(lhs - rhs) < 1e-4 * max(1.0, abs(rhs)), (lhs, rhs)
+
+
 def test_focal_loss_kernel_vs_oracle_and_reference():
     from src import kernels as K
     z = load_golden("focal")
