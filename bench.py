@@ -383,6 +383,39 @@ def precision_leg(args, wl, eng, k, out_bf16):
     return res
 
 
+class _TrainFlops:
+    """Algorithmic FLOP of one training step, counted from the shapes the train graph hands its
+    MFMA nodes (src/train_forward.py): every Linear 6·M·K·N (forward, dX, dW), attention
+    12·L²·dh per head and sequence (forward QKᵀ + PV, backward dV, dP, dQ, dK — the backward's
+    recomputation of QKᵀ not counted).  The small torch layers (AF gate MLP, Conv1d, the 4-class
+    head projection) are left out, so the count is a lower bound."""
+    RULE = "6*M*K*N per Linear + 12*L^2*dh*heads*nseq per attention; recompute and small torch layers excluded"
+
+    def __enter__(self):
+        from src import train_forward as tf
+        self.tf, self.flops = tf, 0
+        self.saved = (tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention)
+
+        def lin(x, weight, bias=None):
+            n = sum(w.shape[0] for w in weight) if isinstance(weight, (list, tuple)) else weight.shape[0]
+            self.flops += 6 * (x.numel() // x.shape[-1]) * x.shape[-1] * n
+            return self.saved[0](x, weight, bias)
+
+        def lin2(x, ln, c1, c2):
+            self.flops += 6 * (x.numel() // x.shape[-1]) * ln.weight.shape[1] * ln.weight.shape[0]
+            return self.saved[1](x, ln, c1, c2)
+
+        def att(qkv, nseq, L, heads, dh, *a, **kw):
+            self.flops += 12 * L * L * dh * heads * nseq
+            return self.saved[2](qkv, nseq, L, heads, dh, *a, **kw)
+        tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention = lin, lin2, att
+        return self
+
+    def __exit__(self, *exc):
+        self.tf.hip_linear, self.tf.hip_linear_rank2, self.tf.hip_attention = self.saved
+        return False
+
+
 def train_bench(args, world, rank, dev):
     """Training throughput at configs[1] / configs[3] shape: per GPU B=24 samples, window 512
     sites (configs[1]; the encoder still runs L = 1030 tokens), k=8 neighbours from a
@@ -409,6 +442,8 @@ def train_bench(args, world, rank, dev):
     tr.rag_k = 8
     for _ in range(2):
         loss = tr.train_step(dict(batch))
+    with _TrainFlops() as fl:                     # one more warm-up step, its GEMM shapes counted
+        loss = tr.train_step(dict(batch))
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
@@ -424,7 +459,10 @@ def train_bench(args, world, rank, dev):
         el = float(t.item())
     masked = 2 * int(batch["mask"].sum())
     ms = el / args.train_steps * 1e3
+    tflops = fl.flops / (ms * 1e-3) / 1e12
     return {"ms_per_step": round(ms, 2), "samples_per_s": round(Bt * world * args.train_steps / el, 1),
+            "algorithmic_tflop_per_step": round(fl.flops / 1e12, 3), "achieved_tflops": round(tflops, 1),
+            "frac_bf16_peak": round(tflops / BF16_PEAK_TFLOPS, 4), "flop_count": fl.RULE,
             "masked_snvs_per_s": round(masked * world * args.train_steps / el, 1),
             "batch_per_gpu": Bt, "window_sites": S, "k": 8, "panel_haplotypes": 2 * nref,
             "n_gpus": world, "loss": round(float(loss), 3),
