@@ -82,6 +82,17 @@ __device__ __forceinline__ uint32_t tl_lds(const char* p) {
 __device__ __forceinline__ float tl_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float tl_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ float tl_bf(const u32x4& v, int j) { return (j & 1) ? tl_hi(v[j >> 1]) : tl_lo(v[j >> 1]); }
+// lane id produced afresh at each use (volatile: not CSE'd with earlier ones), so no lane-derived
+// address stays live across the FFN and gets spilled
+__device__ __forceinline__ int tl_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+// x + x of the lane 32 apart (the row reductions over the two lane halves)
+__device__ __forceinline__ float tl_xsum32(float x) {
+  return x + __int_as_float(__builtin_amdgcn_ds_bpermute((tl_lane() ^ 32) << 2, __float_as_int(x)));
+}
 
 // wait until at most `younger` (<= MAXY) slabs of this wave (4 LDS-DMA instructions each) are in flight
 template <int MAXY> __device__ __forceinline__ void tl_wait(int younger) {
@@ -278,15 +289,15 @@ void tail_kernel(TailArgs p) {
   };
 
   u32x4 a[TL_PF];
-  tl_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
-            std::make_integer_sequence<int, TL_PF>{});
 
   // consume NF fragments (whole slabs) of the part starting at ring slot rd_slot: mma(f, A) per
   // fragment, LDS reads PF ahead (into the next part), one sync per slab
   // G0: the part's first launch slab when known at compile time (PRE), else -1
-  auto run = [&](auto nf_tag, auto g0_tag, auto&& mma) {
+  // STOP: no reads past the part (the caller re-primes a[] with prime() before the next part)
+  auto run = [&](auto nf_tag, auto g0_tag, auto&& mma, auto stop_tag) {
     constexpr int NF = decltype(nf_tag)::value;
     constexpr int G0 = decltype(g0_tag)::value;
+    constexpr bool STOP = decltype(stop_tag)::value;
     static_assert(NF % 16 == 0, "parts are whole slabs");
     tl_unroll([&](auto fc) {
       constexpr int f = decltype(fc)::value;
@@ -300,7 +311,8 @@ void tail_kernel(TailArgs p) {
       mma(fc, cur);
       // (past the end of the stream this reads stale ring bytes that are never used)
       constexpr int qn = f + TL_PF;
-      a[f % TL_PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
+      if constexpr (!STOP || qn < NF)
+        a[f % TL_PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
       if constexpr (TL_SGB) {
         // pipeline shape for the scheduler: MFMA f, then the read PF fragments ahead
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -310,10 +322,15 @@ void tail_kernel(TailArgs p) {
     rd_slot += (NF / 16) * TL_SLAB;
     rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
   };
+  auto prime = [&]() {
+    tl_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
+              std::make_integer_sequence<int, TL_PF>{});
+  };
 
   // (ao: out-projection accumulators; acc: FFN accumulators, born in the first chunk with a zero
   // C operand — explicit zero vectors here get materialised in VGPRs and spilled)
   f32x16 acc[NT];
+  prime();
   if constexpr (PROJ) {
     // ---- per output chunk: acc = x W_c^T (zero C operand at k-step 0); + bias -> bf16 in yo.
     // The NT x 2 stores of chunk c go out PPS per slab during chunk c + 1's stream (bounds-
@@ -347,7 +364,7 @@ void tail_kernel(TailArgs p) {
             tl_unroll([&](auto pc) { store_pair(std::integral_constant<int, slab * PPS + decltype(pc)::value>{}); },
                       std::make_integer_sequence<int, PPS>{});
           }
-        });
+        }, std::false_type{});
       }, std::make_integer_sequence<int, KS / 4>{});
 #pragma unroll
       for (int T = 0; T < NT; ++T) {
@@ -403,7 +420,7 @@ void tail_kernel(TailArgs p) {
       run(std::integral_constant<int, 4 * NT>{}, std::integral_constant<int, g * (NT / 4)>{}, [&](auto fc, const u32x4& A) {
         constexpr int f = decltype(fc)::value;
         ao[f % NT] = mfma32(A, xa[4 * g + f / NT], ao[f % NT]);
-      });
+      }, std::bool_constant<g == KS / 4 - 1>{});
     }, std::make_integer_sequence<int, KS / 4>{});
     stamp(TS_PROJ);
     // ---- x1 = LN1(ao) -> xr (B fragments): pass 1 sums v and v^2, pass 2 normalises
@@ -424,8 +441,8 @@ void tail_kernel(TailArgs p) {
 #pragma unroll
     for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(ao[T]));
     asm volatile("" ::: "memory");
-    sum += __shfl_xor(sum, 32, 64);
-    sq += __shfl_xor(sq, 32, 64);
+    sum = tl_xsum32(sum);
+    sq = tl_xsum32(sq);
     const float mean = sum * (1.0f / D);
     const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
 #pragma unroll
@@ -441,6 +458,9 @@ void tail_kernel(TailArgs p) {
         xr[2 * T + h2] = u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
                                tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
     }
+    // the FFN's first fragments are read only now: read ahead across LN1 they were live through
+    // it and spilled, and their scratch reloads waited on vmcnt(0), i.e. drained the weight ring
+    prime();
   }
   stamp(TS_LN1);
   // x1 opaque from here on: otherwise hipcc folds the epilogue's bf16 -> f32 unpacking of x1
@@ -492,7 +512,7 @@ void tail_kernel(TailArgs p) {
       hn[f & 1] = mfma32(A, xr[f >> 1], hn[f & 1]);
       constexpr int SP = S::FW1 / 16;                // 16 epilogue pairs spread over the MFMAs
       if constexpr (EPI && f % SP == 0) epi_pair(hc, f / SP);
-    });
+    }, std::false_type{});
   };
   // phase 2 of the chunk whose hidden sits in hf: out^T += W2'_c h_c^T (fragment f: k-step
   // f / NT, output tile f % NT); the first one starts acc with a zero C operand
@@ -502,7 +522,7 @@ void tail_kernel(TailArgs p) {
       constexpr int f = decltype(fc)::value;
       if constexpr (FIRST && f < NT) acc[f] = mfma32(A, hf[0], f32x16{});
       else acc[f % NT] = mfma32(A, hf[f / NT], acc[f % NT]);
-    });
+    }, std::false_type{});
   };
   // even chunks in h0, odd in h1: no hidden copies (a loop-carried copy makes hipcc shuffle
   // the accumulator registers at every back edge)
@@ -527,14 +547,14 @@ void tail_kernel(TailArgs p) {
 
   stamp(TS_FFN);
   // ---- epilogue: out = LN2(x1 + lrelu(rstd_f acc - rstd_f mean_f c1 + b2'))
-  st1 += __shfl_xor(st1, 32, 64);
-  st2 += __shfl_xor(st2, 32, 64);
+  st1 = tl_xsum32(st1);
+  st2 = tl_xsum32(st2);
   const float hm = st1 * (1.0f / (4 * D));
   const float hr = 1.0f / sqrtf(fmaxf(st2 * (1.0f / (4 * D)) - hm * hm, 0.f) + p.eps);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stream overrun has landed
   __syncthreads();                                   // every wave is done with the ring
   float* ev = reinterpret_cast<float*>(ring);        // [b2' | c1 | g2 | be2]
-  for (int i = tid; i < 4 * D; i += 256) ev[i] = p.vec[4 * D + i];
+  for (int i = wave * 64 + tl_lane(); i < 4 * D; i += 256) ev[i] = p.vec[4 * D + i];   // fresh tid (no spill)
   __syncthreads();
   stamp(TS_EPI);
   const float* b2 = ev;
@@ -555,17 +575,22 @@ void tail_kernel(TailArgs p) {
       acc[T][i] = v;
       sum += v;
       sq = fmaf(v, v, sq);
+      // one tile's vector-table reads at a time: hoisted over all tiles they held ~30 registers
+      // while x1 is still live, and x1 was spilled during the last chunk
+      if (i == 15) asm volatile("" ::: "memory");
     }
 #pragma unroll
   for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(acc[T]));
   asm volatile("" ::: "memory");
-  sum += __shfl_xor(sum, 32, 64);
-  sq += __shfl_xor(sq, 32, 64);
+  sum = tl_xsum32(sum);
+  sq = tl_xsum32(sq);
   const float mean = sum * (1.0f / D);
   const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
   const float nmr = -mean * rstd;
   auto v2 = [&](int T, int i) { return fmaf(acc[T][i], rstd, nmr); };
-  if (row < p.M) {
+  // the row recomputed from a fresh lane id (kept live from the prologue it was spilled)
+  const long row_e = (long)blockIdx.x * TL_ROWS + wave * 32 + (tl_lane() & 31);
+  if (row_e < p.M) {
 #pragma unroll
     for (int T = 0; T < NT; ++T) {
       float y[16];
@@ -576,7 +601,7 @@ void tail_kernel(TailArgs p) {
       }
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2)
-        *reinterpret_cast<u32x4*>(p.out + row * D + 32 * T + 16 * hh + 8 * h2) =
+        *reinterpret_cast<u32x4*>(p.out + row_e * D + 32 * T + 16 * hh + 8 * h2) =
             u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
                   tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
     }
