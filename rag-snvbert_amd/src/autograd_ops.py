@@ -157,6 +157,24 @@ def _sg_stream(ws, bs, n_out: int):
     return ent[2], ent[3]
 
 
+def _cached(tag: str, ts, make):
+    """``make()`` cached per (tag, the tensors' identities, their versions, the optimizer epoch),
+    like the packed streams: the concatenated QKV weights / biases of the row-panel GEMM path are
+    built once per optimizer step instead of by a cat kernel at every call."""
+    keys, bases = [], []
+    for t in ts:
+        base, key = _base_key(t)
+        keys.append(key)
+        bases.append(base)
+    key = (tag,) + tuple(keys)
+    ver = (tuple(b._version for b in bases), _EPOCH[0])
+    ent = _SG.get(key)
+    if ent is None or any(r() is not b for r, b in zip(ent[0], bases)) or ent[1] != ver:
+        ent = [[weakref.ref(b) for b in bases], ver, make()]
+        _SG[key] = ent
+    return ent[2]
+
+
 def _sg_stream_t(w: torch.Tensor, n_out: int):
     """Packed stream of W^T (the dX = dY W GEMM of a single Linear with out_features = 384)."""
     base, key = _base_key(w)
@@ -253,8 +271,9 @@ class _HipLinear(torch.autograd.Function):
             wsp, vec = _sg_stream(ws, bs, n_out)
             y = K.sgemm(x2, wsp, n_out, vec)
         else:
-            w = bf16_of(ws[0]) if n == 1 else torch.cat([bf16_of(t) for t in ws], 0)
-            b = torch.cat([t.detach().float().reshape(-1) for t in bs]).contiguous() if has_b else None
+            w = bf16_of(ws[0]) if n == 1 else _cached("wcat", ws, lambda: torch.cat([bf16_of(t) for t in ws], 0))
+            b = _cached("bcat", bs, lambda: torch.cat([t.detach().float().reshape(-1) for t in bs]).contiguous()) \
+                if has_b else None
             y = K.linear(x2, w, b)
         ctx.save_for_backward(x2, *ws)
         ctx.n, ctx.has_bias = n, has_b
@@ -295,7 +314,7 @@ class _HipLinear(torch.autograd.Function):
                 gx = K.sgemm(g2, wsp, n_in, vec)
             else:
                 wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else \
-                    torch.cat([bf16_of(t) for t in ws], 0).t().contiguous()
+                    _cached("wcatT", ws, lambda: torch.cat([bf16_of(t) for t in ws], 0).t().contiguous())
                 gx = K.linear(g2, wt)
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
         n_all, k_in = g2.shape[1], x2.shape[1]
