@@ -560,17 +560,10 @@ template <bool PRESCALED, bool TRAIN = false>
 __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
                                                   int* __restrict__ n_fallback, long total_rows,
-                                                  float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{},
-                                                  int desync = 0) {
+                                                  float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{}) {
   using namespace a32;
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
   const int nwg = gridDim.x, orig = blockIdx.x;
-  // first round: the k-th workgroup of each CU starts k * desync cycles late, so the waves that
-  // share a SIMD are not all in their exp phase (or all in their MFMA phase) at once
-  if (desync > 0 && orig < 1024) {
-    const long wait = (long)desync * (orig >> 8), t0 = (long)__builtin_amdgcn_s_memtime();
-    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(4);
-  }
   const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
   const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
@@ -701,224 +694,6 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
   }
 }
 
-// ------------------------------ bf16, head dim 32, LDS-DMA ring, software pipelined --
-// attn32_pipe: attn32_dma's arithmetic (same fixed shift from tile 0, same MFMA order, so the
-// output is bit-identical) with the wave's loop software-pipelined by one tile: iteration t
-// issues the QK^T MFMAs of tile t + 1 beside the exps of tile t, then the PV / row-sum MFMAs of
-// tile t.  In attn32_dma a wave's exps wait on its own QK^T results and its PV MFMAs on its
-// exps, so each SIMD's matrix pipe and VALU issue take turns unless another wave happens to be
-// in the other phase; here every wave carries independent matrix work (8 MFMAs) through its
-// VALU-heavy phase (32 v_exp_f32 + 16 v_cvt_pk_bf16_f32).  The ring has 5 slots (40 KiB) so
-// that two tiles stay in flight beyond the one the next QK^T needs.  Full tiles only; the
-// ragged last tile runs attn32_dma's masked tile body.
-namespace a32 {
-constexpr int NSP = 5;
-
-__device__ __forceinline__ void qk4(const char* Kt, const bf16x8 (&qf)[2], const f32x4 (&c)[2], f32x4 (&s)[4][2],
-                                    int li, int lg) {
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kt + k_off(16 * kt + li, lg));
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt], c[qt], 0, 0, 0);
-  }
-}
-
-__device__ __forceinline__ void exp4(const f32x4 (&s)[4][2], bf16x8 (&pb)[2][2]) {
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pb[cb][qt][j] = (bf16)__builtin_amdgcn_exp2f(s[2 * cb + (j >> 2)][qt][j & 3]);
-}
-
-__device__ __forceinline__ void pv4(const char* Vt, const bf16x8 (&pb)[2][2], State& st, int li, int lg) {
-  const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
-  const int tq = li >> 2, tp = li & 3;
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int k0 = 32 * cb + 4 * lg + tq;
-      const bf16x8 vf = cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[cb][qt], st.o[e][qt], 0, 0, 0);
-    }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) st.ls[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[cb][qt], st.ls[qt], 0, 0, 0);
-  }
-}
-}  // namespace a32
-
-template <bool PRESCALED, int SCHED>
-__global__ __launch_bounds__(256) void attn32_pipe(int L, int H, const bf16* __restrict__ qkv, long ld,
-                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
-                                                   int* __restrict__ n_fallback, long total_rows) {
-  using namespace a32;
-  __shared__ __attribute__((aligned(16))) char smem[NSP * SLOT];
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 15, lg = lane >> 4;
-  const int D = H * 32;
-  const long base = (long)seq * L * ld;
-  const bf16* Qp = qkv + base + h * 32;
-  const bf16* Kp = qkv + base + D + h * 32;
-  const bf16* Vp = qkv + base + 2 * D + h * 32;
-  const int q0 = qb * QPB + wave * QPW;
-  const bool active = q0 < L;                      // wave-uniform
-
-  bf16x8 qf[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-    bf16x8 v = q < L ? *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + 8 * lg) : bf16x8{};
-    if constexpr (!PRESCALED) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * scale_log2e);
-    }
-    qf[qt] = v;
-  }
-
-  // K / V pieces as in attn32_dma
-  const long rem = (total_rows - (long)seq * L) * ld * 2;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(qkv + base), (short)0, (int)(rem < 0x7fffffffL ? rem : 0x7fffffffL), 0x00020000);
-  const int kk = 16 * wave + (lane >> 2), c4 = lane & 3;
-  const int kc = c4 ^ ((-(kk >> 2)) & 3);
-  const int vc = 2 * ((c4 >> 1) ^ ((kk >> 2) & 1)) + (c4 & 1);
-  const int vk = (int)(kk * ld * 2) + (D + h * 32) * 2 + kc * 16;
-  const int vv = (int)(kk * ld * 2) + (2 * D + h * 32) * 2 + vc * 16;
-  const int tile_bytes = (int)(KT * ld * 2);
-  auto issue = [&](int t, int slot) {
-    char* s = smem + slot * SLOT + wave * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)s, 16, vk, t * tile_bytes,
-                                             0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)(s + TB), 16, vv,
-                                             t * tile_bytes, 0, 0);
-  };
-  // retire this wave's pieces of all but the y youngest tiles in flight (y <= NSP - 2)
-  auto wait = [&](int y) {
-    if (y >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (y == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (y == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  State st;
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) st.o[0][qt] = st.o[1][qt] = st.ls[qt] = st.negm[qt] = zero;
-  const int ntile = (L + KT - 1) / KT, nfull = L / KT;   // nfull >= 1 (host)
-#pragma unroll
-  for (int j = 0; j < NSP - 1; ++j)
-    if (j < ntile) issue(j, j);
-  wait(min(NSP - 2, ntile - 1));
-  __builtin_amdgcn_s_barrier();
-  // tile 0's scores: their maximum is the fixed shift
-  f32x4 s[4][2];
-  if (active) {
-    const f32x4 z2[2] = {zero, zero};
-    qk4(smem, qf, z2, s, li, lg);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      st.negm[qt] = f32x4{-mx, -mx, -mx, -mx};
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[kt][qt] += st.negm[qt];
-    }
-  }
-  // iteration t: QK^T of tile t + 1 (when full) beside the exps of tile t, then PV of tile t
-  auto body = [&](const char* Kn, const char* Vt, bool nxt) {
-    f32x4 sn[4][2];
-    bf16x8 pb[2][2];
-    if (nxt) qk4(Kn, qf, st.negm, sn, li, lg);
-    exp4(s, pb);
-    if constexpr (SCHED == 1) {
-      // 8 QK^T MFMAs spread through the 48 softmax VALU instructions
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-      }
-    }
-    pv4(Vt, pb, st, li, lg);
-    if (nxt) {
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) s[kt][0] = sn[kt][0], s[kt][1] = sn[kt][1];
-    }
-  };
-  auto step = [&](auto s_tag, int t) {
-    constexpr int S = decltype(s_tag)::value;
-    if (t + 1 < ntile) {
-      wait(min(NSP - 3, ntile - 2 - t));
-      __builtin_amdgcn_s_barrier();                // tile t + 1 visible; every wave is done with t - 1
-      if (t + NSP - 1 < ntile) issue(t + NSP - 1, (S + NSP - 1) % NSP);
-    }
-    if (active) body(smem + ((S + 1) % NSP) * SLOT, smem + S * SLOT + TB, t + 1 < nfull);
-  };
-  int t = 0;
-  for (; t + NSP <= nfull; t += NSP) {
-    step(std::integral_constant<int, 0>{}, t);
-    step(std::integral_constant<int, 1>{}, t + 1);
-    step(std::integral_constant<int, 2>{}, t + 2);
-    step(std::integral_constant<int, 3>{}, t + 3);
-    step(std::integral_constant<int, 4>{}, t + 4);
-  }
-  for (; t < nfull; ++t) {
-    if (t + 1 < ntile) {
-      wait(min(NSP - 3, ntile - 2 - t));
-      __builtin_amdgcn_s_barrier();
-      if (t + NSP - 1 < ntile) issue(t + NSP - 1, (t + NSP - 1) % NSP);
-    }
-    if (active) body(smem + ((t + 1) % NSP) * SLOT, smem + (t % NSP) * SLOT + TB, t + 1 < nfull);
-  }
-  if (nfull < ntile && active) {                   // the ragged tile (landed and visible: waited above)
-    const char* Kt = smem + (nfull % NSP) * SLOT;
-    tile_any<false>(Kt, Kt + TB, nfull * KT, L, qf, st, li, lg);
-  }
-  if (!active) return;
-
-  bool bad = false;
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const float l = st.ls[qt][0];
-    bad |= !(l > 0.f && l < INFINITY);
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(st.o[e][qt][r]);
-  }
-  if (__ballot(bad)) {
-    if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
-    attn32_online<false>(Kp, Vp, ld, L, qf, st, li, lg);
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-    if (q >= L) continue;
-    const float inv = 1.0f / st.ls[qt][0];
-    bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * 32;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      bf16x4 w;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)(st.o[e][qt][r] * inv);
-      *reinterpret_cast<bf16x4*>(op + 16 * e + 4 * lg) = w;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- f32 path --
 template <int DH>
 __global__ __launch_bounds__(64) void attn_fwd_f32(int nseq, int L, int H, const float* __restrict__ qkv,
@@ -985,24 +760,13 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     int* cnt = attn_fallback_counter();
     const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
     const bool dma = !(reg && reg[0] == '1');
-    const char* pipe = getenv("SNVRAG_ATTN_PIPE");    // A/B: the software-pipelined kernel (1, 2 = sched hints)
-    const char* dz = getenv("SNVRAG_ATTN_DESYNC");       // A/B: first-round stagger (cycles)
-    const int desync = dz ? atoi(dz) : 0;
-    if (pipe && pipe[0] != '0' && L >= a32::KT) {
-      const bool sch = pipe[0] == '2';
-      if (pre)
-        hipLaunchKernelGGL((sch ? attn32_pipe<true, 1> : attn32_pipe<true, 0>), dim3((unsigned)nb), dim3(256), 0, s,
-                           (int)L, H, (const bf16*)qkv, ld, (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L);
-      else
-        hipLaunchKernelGGL((sch ? attn32_pipe<false, 1> : attn32_pipe<false, 0>), dim3((unsigned)nb), dim3(256), 0, s,
-                           (int)L, H, (const bf16*)qkv, ld, (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L);
-    } else if (dma) {
+    if (dma) {
       if (pre)
         hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{}, desync);
+                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
       else
         hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{}, desync);
+                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
     } else if (pre)
       hipLaunchKernelGGL(attn32_bf16<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
                          (bf16*)out, ldo, 1.0f, nqb, cnt);

@@ -1,7 +1,7 @@
 """A/B of the bf16 dh=32 attention kernels at the bench shape (512 sequences x 1030 tokens,
 12 heads, prescaled Q): each variant selected by environment (read by the library per launch),
 outputs compared bit for bit with the default kernel, times from CUDA events over REPS launches.
-usage: VARIANTS="SNVRAG_ATTN_PIPE=1 SNVRAG_ATTN_PIPE=2" python tools/attn_ab.py"""
+usage: VARIANTS="SNVRAG_ATTN_REGSTAGE=1" python tools/attn_ab.py"""
 import math
 import os
 import sys
@@ -38,7 +38,7 @@ def run(env):
 
 base, ms0 = run([])
 print(f"default: {ms0:.4f} ms  {flop / ms0 / 1e9:.1f} TFLOP/s", flush=True)
-for var in os.environ.get("VARIANTS", "SNVRAG_ATTN_PIPE=1").split(";"):
+for var in os.environ.get("VARIANTS", "SNVRAG_ATTN_REGSTAGE=1").split(";"):
     env = var.split()
     out, ms = run(env)
     same = torch.equal(out, base)
