@@ -439,6 +439,144 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
   }
 }
 
+// ln_bwd_kernel<NC, 1> with the next row's s / dy / stats loads issued before the current row's
+// reductions (a wave's rows are otherwise load -> reduce -> store in series, latency-bound)
+__device__ __forceinline__ void unpack8bf(const u32x4& a, float* v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(a[e] << 16);
+    v[2 * e + 1] = __uint_as_float(a[e] & 0xffff0000u);
+  }
+}
+template <int NC>
+__global__ __launch_bounds__(256) void ln_bwd_pf_kernel(long M, int N, int rows_per_wave, const bf16* __restrict__ dy,
+                                                        const bf16* __restrict__ s, const float2* __restrict__ stats,
+                                                        const float* __restrict__ g, bf16* __restrict__ ds,
+                                                        bf16* __restrict__ dres, float* __restrict__ part, LnDrop dr,
+                                                        const bf16* __restrict__ rp) {
+  extern __shared__ float red[];                      // [4 waves][2][N]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = N / 8;
+  float dgp[NC][8], dbp[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dgp[c][j] = dbp[c][j] = 0.f;
+  const long r0 = ((long)blockIdx.x * 4 + wave) * rows_per_wave;
+  const long r1 = min(M, r0 + rows_per_wave);
+  u32x4 ns[NC], nd[NC];
+  float2 nst = make_float2(0.f, 0.f);
+  auto fetch = [&](long m) {
+    nst = stats[m];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int cc = lane + 64 * c;
+      if (cc < nc) {
+        ns[c] = *reinterpret_cast<const u32x4*>(s + m * N + 8 * cc);
+        nd[c] = *reinterpret_cast<const u32x4*>(dy + m * N + 8 * cc);
+      }
+    }
+  };
+  if (r0 < r1) fetch(r0);
+  for (long m = r0; m < r1; ++m) {
+    u32x4 cs[NC], cd[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      cs[c] = ns[c];
+      cd[c] = nd[c];
+    }
+    const float2 st = nst;
+    if (m + 1 < r1) fetch(m + 1);
+    float xh[NC][8], gy[NC][8];
+    uint32_t neg[NC];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int cc = lane + 64 * c;
+      if (cc < nc) {
+        float dv[8];
+        unpack8bf(cs[c], xh[c]);
+        if (dr.sl_x != 0.f) {
+          neg[c] = 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            neg[c] |= (xh[c][j] > 0.f ? 0u : 1u) << j;
+            xh[c][j] = (float)(bf16)ln_lrelu(xh[c][j], dr.sl_x);
+          }
+        }
+        unpack8bf(cd[c], dv);
+        if (dr.th_o) {
+          float mk[8];
+          ln_drop8(dr.base_o, dr.th_o, dr.sc_o, m, cc, mk);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dv[j] *= mk[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xh[c][j] - st.x) * st.y;
+          gy[c][j] = dv[j] * g[8 * cc + j];
+          a1 += gy[c][j];
+          a2 += gy[c][j] * xh[c][j];
+          dgp[c][j] += dv[j] * xh[c][j];
+          dbp[c][j] += dv[j];
+        }
+      }
+    }
+    a1 = wave_sum(a1) / N;
+    a2 = wave_sum(a2) / N;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int cc = lane + 64 * c;
+      if (cc < nc) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = st.y * (gy[c][j] - a1 - xh[c][j] * a2);
+        if (dr.sl_x != 0.f) {
+          float dx[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dx[j] = ((neg[c] >> j) & 1u) ? o[j] * dr.sl_x : o[j];
+          st8bf(ds + m * N + 8 * cc, dx);
+        } else {
+          st8bf(ds + m * N + 8 * cc, o);
+        }
+        if (dres) {
+          if (dr.th_r) {
+            float mk[8];
+            ln_drop8(dr.base_r, dr.th_r, dr.sc_r, m, cc, mk);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+          }
+          if (rp) {
+            float rv[8];
+            ld8bf(rp + m * N + 8 * cc, rv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = rv[j] > 0.f ? o[j] : o[j] * dr.sl_r;
+          }
+          st8bf(dres + m * N + 8 * cc, o);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int cc = lane + 64 * c;
+    if (cc < nc)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wave * 2 + 0) * N + 8 * cc + j] = dgp[c][j];
+        red[(wave * 2 + 1) * N + 8 * cc + j] = dbp[c][j];
+      }
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < 2 * N; n += 256) {
+    const int which = n / N, col = n % N;
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc += red[(w * 2 + which) * N + col];
+    part[(long)blockIdx.x * 2 * N + n] = acc;
+  }
+}
+
 // column sums of the ln_bwd partials [R][2N] into dg (columns < N) and db: written, or added
 // to what they hold (accumulate: the parameters' .grad buffers); fixed-order (deterministic)
 __global__ __launch_bounds__(256) void ln_part_sum_kernel(long R, int N, const float* __restrict__ x,
@@ -724,8 +862,15 @@ extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s
                        (const bf16*)dy, (const bf16*)s, (const float2*)stats, g, (bf16*)ds, (bf16*)dres, part, dr, rp);
   };
   const int nch = cdiv(N / 8, 64);
-  // one row per wave step (2 rows: 174 -> 209 us at N = 1536, tools/ln_micro.py)
-  if (nch == 1) go(ln_bwd_kernel<1, 1>);
+  // one row per wave step (2 rows: 174 -> 209 us at N = 1536, tools/ln_micro.py); for N > 512 the
+  // next row's loads issued ahead (N = 1536: 147-150 vs 174 us; N = 384: 55 vs 52 us, so not there)
+  // unless SNVRAG_LN_BWD_NOPF (A/B)
+  static const bool pf = getenv("SNVRAG_LN_BWD_NOPF") == nullptr;
+  if (pf && nch > 1) {
+    if (nch == 2) go(ln_bwd_pf_kernel<2>);
+    else if (nch == 3) go(ln_bwd_pf_kernel<3>);
+    else go(ln_bwd_pf_kernel<4>);
+  } else if (nch == 1) go(ln_bwd_kernel<1, 1>);
   else if (nch == 2) go(ln_bwd_kernel<2, 1>);
   else if (nch == 3) go(ln_bwd_kernel<3, 1>);
   else go(ln_bwd_kernel<4, 1>);

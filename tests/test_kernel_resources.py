@@ -31,7 +31,8 @@ HOT = [
     ("snvrag::dw_dma_kernel", "training dW"),
     ("snvrag::scan2_kernel<16, 2, 0>", "kNN panel scan"),
     # (bf16 template arguments: c++filt leaves these names mangled)
-    ("_ZN6snvrag13ln_bwd_kernel", "training LayerNorm backward"),
+    ("_ZN6snvrag13ln_bwd_kernel", "training LayerNorm backward (N <= 512)"),
+    ("_ZN6snvrag16ln_bwd_pf_kernel", "training LayerNorm backward (N > 512)"),
     ("_ZN6snvrag19ln_fwd_train_kernel", "training LayerNorm forward"),
 ]
 
