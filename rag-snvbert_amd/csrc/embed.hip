@@ -127,49 +127,103 @@ __global__ __launch_bounds__(256) void posfeat_kernel(int L, const float* __rest
 
 // ------------------------------------------------------------------- AF gate --
 // fusion.py:82-86: gate = sigmoid(W2 gelu(W1 c + b1) + b2), enc = gelu(LN(Wj c + bj)),
-// out = af + rs * gate * enc.  One wave per row m; D <= 1024.
-// Lane-per-row layout: the 32 gate hiddens of a row sit in the lane's VGPRs and the
-// per-column weights (g2_w row, j_w, LN affine) are wave-uniform scalar loads, so the
-// [D x 32] gate GEMV costs 32 v_fma per element with no cross-lane traffic.  The
-// joint-encoder LayerNorm is two passes over the D columns of the 2-input Linear.
+// out = af + rs * gate * enc.  One lane per row (AF_R rows per lane).
+// Lane-per-row layout: the 32 gate hiddens of AF_R rows sit in the lane's VGPRs and the
+// per-column weights (g2_w row, j_w, LN affine) are wave-uniform scalar loads shared by those
+// rows, so the [D x 32] gate GEMV costs 32 v_fma per element with no cross-lane traffic.
+constexpr int AF_R = 1;                 // rows per lane (4: 555 vs 304 us, occupancy 2 vs 4 waves/SIMD)
 template <typename T>
 __global__ __launch_bounds__(256) void af_gate_kernel(long M, int D, const float* __restrict__ af,
                                                       const float* __restrict__ afp, snvrag_afgate_w_t w,
                                                       T* __restrict__ out) {
   constexpr int V = 16 / sizeof(T);
-  // 64 rows per workgroup; its 4 waves split the D output columns
-  const long m = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  // 64 AF_R rows per workgroup (lane l: rows base + l + 64 r); its 4 waves split the D columns
+  const long base = (long)blockIdx.x * 64 * AF_R + (threadIdx.x & 63);
   const int cpw = ((D / V + 3) / 4) * V;
   const int c_lo = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * cpw);
   const int c_hi = min(D, c_lo + cpw);
-  const bool ok = m < M;
-  const float a0 = ok ? af[m] : 0.f, a1 = ok ? afp[m] : 0.f;
-  float hid[32];
-#pragma unroll
-  for (int u = 0; u < 32; ++u) hid[u] = gelu_erf(w.g1_w[u * 2] * a0 + w.g1_w[u * 2 + 1] * a1 + w.g1_b[u]);
-  float s = 0.f;
-  for (int n = 0; n < D; ++n) s += w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n];
-  const float mean = s / D;
-  float q = 0.f;
-  for (int n = 0; n < D; ++n) {
-    const float d = w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n] - mean;
-    q += d * d;
+  // joint_encoder[0] is affine in (af, af_p): enc_n = j0_n a0 + j1_n a1 + jb_n, so its LayerNorm
+  // statistics are mean = mu . (a0, a1, 1) and var = (a0, a1, 1) S (a0, a1, 1)^T with the
+  // centred second moments S of the weight columns — reduced once per workgroup (two passes)
+  // instead of two D-long loops per row
+  __shared__ float red[4][6];
+  const int wv = threadIdx.x >> 6;
+  float m0 = 0.f, m1 = 0.f, mb = 0.f;
+  for (int n = threadIdx.x; n < D; n += 256) {
+    m0 += w.j_w[n * 2];
+    m1 += w.j_w[n * 2 + 1];
+    mb += w.j_b[n];
   }
-  const float rstd = 1.0f / sqrtf(q / D + 1e-5f);
+  m0 = wave_sum(m0);
+  m1 = wave_sum(m1);
+  mb = wave_sum(mb);
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = m0; red[wv][1] = m1; red[wv][2] = mb; }
+  __syncthreads();
+  m0 = (red[0][0] + red[1][0] + red[2][0] + red[3][0]) / D;
+  m1 = (red[0][1] + red[1][1] + red[2][1] + red[3][1]) / D;
+  mb = (red[0][2] + red[1][2] + red[2][2] + red[3][2]) / D;
+  __syncthreads();
+  float sm[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};                // S00 S11 S01 S0b S1b Sbb
+  for (int n = threadIdx.x; n < D; n += 256) {
+    const float c0 = w.j_w[n * 2] - m0, c1 = w.j_w[n * 2 + 1] - m1, cb = w.j_b[n] - mb;
+    sm[0] += c0 * c0;
+    sm[1] += c1 * c1;
+    sm[2] += c0 * c1;
+    sm[3] += c0 * cb;
+    sm[4] += c1 * cb;
+    sm[5] += cb * cb;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    sm[i] = wave_sum(sm[i]);
+    if ((threadIdx.x & 63) == 0) red[wv][i] = sm[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sm[i] = (red[0][i] + red[1][i] + red[2][i] + red[3][i]) / D;
+  float a0[AF_R], a1[AF_R], mean[AF_R], rstd[AF_R], hid[AF_R][32];
+#pragma unroll
+  for (int r = 0; r < AF_R; ++r) {
+    const long m = base + 64 * r;
+    const bool ok = m < M;
+    a0[r] = ok ? af[m] : 0.f;
+    a1[r] = ok ? afp[m] : 0.f;
+    mean[r] = m0 * a0[r] + m1 * a1[r] + mb;
+    const float var = a0[r] * a0[r] * sm[0] + a1[r] * a1[r] * sm[1] +
+                      2.f * (a0[r] * a1[r] * sm[2] + a0[r] * sm[3] + a1[r] * sm[4]) + sm[5];
+    rstd[r] = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      hid[r][u] = gelu_erf(w.g1_w[u * 2] * a0[r] + w.g1_w[u * 2 + 1] * a1[r] + w.g1_b[u]);
+  }
   for (int n0 = c_lo; n0 < c_hi; n0 += V) {
-    T o[V];
+    T o[AF_R][V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int n = n0 + j;
-      float g = w.g2_b[n];
+      float g[AF_R];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) g = fmaf(w.g2_w[n * 32 + u], hid[u], g);
-      g = 1.0f / (1.0f + expf(-g));
-      const float enc = w.j_w[n * 2] * a0 + w.j_w[n * 2 + 1] * a1 + w.j_b[n];
-      const float e = gelu_erf((enc - mean) * rstd * w.ln_w[n] + w.ln_b[n]);
-      o[j] = from_f32<T>(a0 + w.res_scale * (g * e));
+      for (int r = 0; r < AF_R; ++r) g[r] = w.g2_b[n];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const float wu = w.g2_w[n * 32 + u];
+#pragma unroll
+        for (int r = 0; r < AF_R; ++r) g[r] = fmaf(wu, hid[r][u], g[r]);
+      }
+      const float j0 = w.j_w[n * 2], j1 = w.j_w[n * 2 + 1], jb = w.j_b[n], lw = w.ln_w[n], lb = w.ln_b[n];
+#pragma unroll
+      for (int r = 0; r < AF_R; ++r) {
+        const float gt = 1.0f / (1.0f + expf(-g[r]));
+        const float enc = j0 * a0[r] + j1 * a1[r] + jb;
+        const float e = gelu_erf((enc - mean[r]) * rstd[r] * lw + lb);
+        o[r][j] = from_f32<T>(a0[r] + w.res_scale * (gt * e));
+      }
     }
-    if (ok) *reinterpret_cast<u32x4*>(out + m * D + n0) = *reinterpret_cast<u32x4*>(o);
+#pragma unroll
+    for (int r = 0; r < AF_R; ++r) {
+      const long m = base + 64 * r;
+      if (m < M) *reinterpret_cast<u32x4*>(out + m * D + n0) = *reinterpret_cast<u32x4*>(o[r]);
+    }
   }
 }
 
@@ -340,9 +394,11 @@ extern "C" int snvrag_af_gate(int dtype_out, int64_t M, int64_t D, const float* 
   if (M == 0) return 0;
   hipStream_t s = as_stream(stream);
   if (dtype_out == SNVRAG_BF16)
-    hipLaunchKernelGGL(af_gate_kernel<bf16>, dim3(cdiv(M, 64)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (bf16*)out);
+    hipLaunchKernelGGL(af_gate_kernel<bf16>, dim3(cdiv(M, 64 * AF_R)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w,
+                       (bf16*)out);
   else
-    hipLaunchKernelGGL(af_gate_kernel<float>, dim3(cdiv(M, 64)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w, (float*)out);
+    hipLaunchKernelGGL(af_gate_kernel<float>, dim3(cdiv(M, 64 * AF_R)), dim3(256), 0, s, (long)M, (int)D, af, af_p, *w,
+                       (float*)out);
   SNV_LAUNCH_CHECK();
   return 0;
 }
