@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 23
+#define SNVRAG_ABI_VERSION 24
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -33,6 +33,12 @@ int snvrag_abi_version(void);
 const char* snvrag_last_error(void);
 /* fills name (>= 64 bytes) with the device name of `device`; returns the CU count */
 int snvrag_device_info(int device, char* name, int name_len);
+/* Library options — tuning switches of the micro-benchmarks and test hooks, no reference
+ * counterpart: knn_no_reduce, scan_mode, scan_nt, unfused_ln, encoder_chunk, gemm_tile128,
+ * gemm_nw, tail_variant, tail_desync, sg_desync, sg_waves4, ln_bwd_nopf.  Each starts from the
+ * environment variable SNVRAG_<NAME> (read once, at first use); launches read the table. */
+int snvrag_set_option(const char* name, int64_t value);
+int snvrag_get_option(const char* name, int64_t* value);
 
 /* ------------------------------------------------------------------------
  * Dense layers  (replaces torch.nn.Linear calls of model/attention/

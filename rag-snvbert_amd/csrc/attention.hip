@@ -4,7 +4,8 @@
 // mask — padding tokens participate) with the head split/merge of
 // multi_head_attention.py:44-51.  L = 1030 for every v18 configuration.
 //
-// bf16 path (v_mfma_f32_16x16x32_bf16), one workgroup = 4 waves = 64 queries of
+// Head dim 32 (every v18 model: d384/H12, d128/H4, d64/H2): attn32_dma below.  Other head
+// dims: attn_fwd_bf16 (v_mfma_f32_16x16x32_bf16), one workgroup = 4 waves = 64 queries of
 // one (sequence, head); each wave owns 16 queries.  Scores are computed
 // TRANSPOSED, S^T = K Q^T, so each lane holds one query's column of scores and
 // the softmax row statistics need only 2 cross-lane shuffles; P^T then feeds
@@ -424,121 +425,6 @@ __device__ __forceinline__ void attn32_online(const bf16* Kp, const bf16* Vp, lo
 }
 }  // namespace a32
 
-// TRAIN (training forward, snvrag_attention_train_fwd): Q unscaled, lse [nseq, H, L] written
-// (log2 domain: lse = c m + log2 l), attention-probability dropout on the PV operand.
-template <bool PRESCALED, bool TRAIN = false>
-__global__ __launch_bounds__(256) void attn32_bf16(int L, int H, const bf16* __restrict__ qkv, long ld,
-                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
-                                                   int* __restrict__ n_fallback, float* __restrict__ lse = nullptr,
-                                                   AttnDrop drop = AttnDrop{}) {
-  using namespace a32;
-  __shared__ __attribute__((aligned(16))) char smem[2][2 * TB];
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int qq = nwg / 8, rr = nwg % 8, xcd = orig % 8;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int qb = wg % nqb, sh = wg / nqb, h = sh % H, seq = sh / H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, lg = lane >> 4;
-  const int D = H * 32;
-  const long base = (long)seq * L * ld;
-  const bf16* Qp = qkv + base + h * 32;
-  const bf16* Kp = qkv + base + D + h * 32;
-  const bf16* Vp = qkv + base + 2 * D + h * 32;
-  const int q0 = qb * QPB + wave * QPW;
-  const bool active = q0 < L;                      // wave-uniform
-
-  bf16x8 qf[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-    bf16x8 v = q < L ? *reinterpret_cast<const bf16x8*>(Qp + (long)q * ld + 8 * lg) : bf16x8{};
-    if constexpr (!PRESCALED && !TRAIN) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * scale_log2e);
-    }
-    qf[qt] = v;
-  }
-
-  // loader: thread -> (key = tid / 4, 16-B chunk = tid % 4) of K and of V
-  const int lkey = tid >> 2, lch = tid & 3;
-  u32x4 kr = {0u, 0u, 0u, 0u}, vr = {0u, 0u, 0u, 0u};
-  const bf16* kp_l = Kp + (long)lkey * ld + 8 * lch;
-  const bf16* vp_l = Vp + (long)lkey * ld + 8 * lch;
-#define A32_LOAD(t)                                                         \
-  {                                                                         \
-    const bool ok = (t) * KT + lkey < L;                                    \
-    const long off = (long)(t) * KT * ld;                                   \
-    kr = ok ? *reinterpret_cast<const u32x4*>(kp_l + off) : u32x4{0u, 0u, 0u, 0u}; \
-    vr = ok ? *reinterpret_cast<const u32x4*>(vp_l + off) : u32x4{0u, 0u, 0u, 0u}; \
-  }
-#define A32_STORE(stage)                                                                      \
-  {                                                                                           \
-    *reinterpret_cast<u32x4*>(smem[stage] + k_off(lkey, lch)) = kr;                           \
-    *reinterpret_cast<u32x4*>(smem[stage] + TB + v_off(lkey, lch >> 1) + 16 * (lch & 1)) = vr; \
-  }
-
-  State st;
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    st.o[0][qt] = st.o[1][qt] = st.ls[qt] = zero;
-    st.negm[qt] = zero;
-  }
-  Train tr{};
-  if constexpr (TRAIN) tr = Train{scale_log2e, drop, drop.thresh ? drop_base(drop.seed, (uint32_t)sh) : 0u, q0};
-  const int ntile = (L + KT - 1) / KT;
-  A32_LOAD(0);
-  A32_STORE(0);
-  __syncthreads();
-  for (int t = 0; t < ntile; ++t) {
-    const bool more = t + 1 < ntile;
-    if (more) A32_LOAD(t + 1);
-    if (active) {
-      const char* Kt = smem[t & 1];
-      if (t == 0) tile_any<true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
-      else tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
-    }
-    if (more) A32_STORE((t + 1) & 1);
-    __syncthreads();
-  }
-#undef A32_LOAD
-#undef A32_STORE
-  if (!active) return;
-  if constexpr (TRAIN) drop_scale_o(st, drop);
-
-  bool bad = false;
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const float l = st.ls[qt][0];
-    bad |= !(l > 0.f && l < INFINITY);
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(st.o[e][qt][r]);
-  }
-  if (__ballot(bad)) {
-    if (lane == 0 && n_fallback) atomicAdd(n_fallback, 1);
-    attn32_online<TRAIN>(Kp, Vp, ld, L, qf, st, li, lg, tr);
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-    if (q >= L) continue;
-    const float inv = 1.0f / st.ls[qt][0];
-    if constexpr (TRAIN) {
-      if (lg == 0) lse[((long)seq * H + h) * L + q] = -scale_log2e * st.negm[qt][0] + log2f(st.ls[qt][0]);
-    }
-    bf16* op = out + (long)seq * L * ldo + (long)q * ldo + h * 32;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      bf16x4 w;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)(st.o[e][qt][r] * inv);
-      *reinterpret_cast<bf16x4*>(op + 16 * e + 4 * lg) = w;
-    }
-  }
-}
-
 // ------------------------------------------- bf16, head dim 32, LDS-DMA ring --
 // attn32_dma: the attn32 math (same tile<> bodies, same LDS images) with K/V staged by
 // LDS-DMA (buffer_load ... lds) through a 4-slot ring instead of register staging.  In the
@@ -589,25 +475,26 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
     }
     qf[qt] = v;
   }
+  // retire the Q loads HERE: the waitcnt pass would otherwise place their wait at the first use,
+  // inside the tile loop (the loop header merges the preheader's pending loads), where it
+  // becomes an s_waitcnt vmcnt(0) per tile that also drains the LDS-DMA ring
+  asm volatile("" : "+v"(qf[0]), "+v"(qf[1]));
 
   // K / V pieces: wave w moves keys 16 w .. 16 w + 15 of a tile (1 KiB of K, 1 KiB of V); lane
   // l lands at byte 16 l of the piece, i.e. key 16 w + l / 4, image chunk l % 4, so it loads the
   // source chunk that k_off / v_off put there
   const long rem = (total_rows - (long)seq * L) * ld * 2;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(qkv + base), (short)0, (int)(rem < 0x7fffffffL ? rem : 0x7fffffffL), 0x00020000);
+  const i32x4 rs = dma_rsrc(qkv + base, rem);
   const int kk = 16 * wave + (lane >> 2), c4 = lane & 3;
   const int kc = c4 ^ ((-(kk >> 2)) & 3);
   const int vc = 2 * ((c4 >> 1) ^ ((kk >> 2) & 1)) + (c4 & 1);
   const int vk = (int)(kk * ld * 2) + (D + h * 32) * 2 + kc * 16;
   const int vv = (int)(kk * ld * 2) + (2 * D + h * 32) * 2 + vc * 16;
   const int tile_bytes = (int)(KT * ld * 2);
+  const uint32_t lds_w = lds_addr(smem) + wave * 1024;
   auto issue = [&](int t, int slot) {
-    char* s = smem + slot * SLOT + wave * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)s, 16, vk, t * tile_bytes,
-                                             0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) char*)(s + TB), 16, vv,
-                                             t * tile_bytes, 0, 0);
+    dma_x4(rs, lds_w + slot * SLOT, vk, t * tile_bytes);
+    dma_x4(rs, lds_w + slot * SLOT + TB, vv, t * tile_bytes);
   };
   // retire this wave's pieces of tile t: y = younger tiles still in flight (<= NS - 2)
   auto wait = [&](int y) {
@@ -630,16 +517,18 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
   for (int j = 0; j < NS - 1; ++j)
     if (j < ntile) issue(j, j);
   // one tile of the ring: slot S is compile-time, so the LDS reads take immediate offsets
+  // (inside the unrolled loop t + NS <= nfull: NS - 2 younger tiles are in flight and tile
+  // t + NS - 1 exists, so the wait and the issue are unconditional)
   auto step = [&](auto s_tag, int t) {
     constexpr int S = decltype(s_tag)::value;
-    wait(min(NS - 2, ntile - 1 - t));
+    wait(NS - 2);
     __builtin_amdgcn_s_barrier();                  // tile t visible; every wave is done with t - 1
-    if (t + NS - 1 < ntile) issue(t + NS - 1, (S + NS - 1) % NS);
-    if (active) {
-      const char* Kt = smem + S * SLOT;
-      if (t == 0) tile<4, false, true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
-      else tile<4, false, false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
-    }
+    issue(t + NS - 1, (S + NS - 1) % NS);
+    // (a wave past L — the last query block's — computes on zero queries and stores nothing:
+    // no per-tile branch)
+    const char* Kt = smem + S * SLOT;
+    if (t == 0) tile<4, false, true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+    else tile<4, false, false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
   };
   int t = 0;
   for (; t + NS <= nfull; t += NS) {
@@ -751,28 +640,19 @@ template <int DH>
 static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, long ld, void* out,
                        long ldo, float scale, hipStream_t s) {
   evlog_begin(s);
-  if (DH == 32 && dtype == SNVRAG_BF16 && !getenv("SNVRAG_ATTN_V1")) {
+  if (DH == 32 && dtype == SNVRAG_BF16) {
     const int nqb = cdiv(L, a32::QPB);
     const long nb = (long)nqb * H * nseq;
     SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
     const float sl2 = scale * 1.4426950408889634f;
     const bool pre = fabsf(sl2 - 1.0f) < 1e-6f;      // Q already carries log2(e)/sqrt(dh)
     int* cnt = attn_fallback_counter();
-    const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
-    const bool dma = !(reg && reg[0] == '1');
-    if (dma) {
-      if (pre)
-        hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
-      else
-        hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                           (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
-    } else if (pre)
-      hipLaunchKernelGGL(attn32_bf16<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                         (bf16*)out, ldo, 1.0f, nqb, cnt);
+    if (pre)
+      hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                         (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
     else
-      hipLaunchKernelGGL(attn32_bf16<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
-                         (bf16*)out, ldo, sl2, nqb, cnt);
+      hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                         (bf16*)out, ldo, sl2, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
   } else if (dtype == SNVRAG_BF16) {
     const int nqb = cdiv(L, AQ);
     const long nb = (long)nqb * H * nseq;
@@ -820,25 +700,16 @@ extern "C" int snvrag_attention_train_fwd(int64_t nseq, int64_t L, int heads, in
   SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
   const float sl2 = scale * 1.4426950408889634f;
   evlog_begin(s);
-  if (dh == 32 && !getenv("SNVRAG_ATTN_TRAIN_V1")) {
+  if (dh == 32) {
     // the inference kernel's structure (fixed shift, ones-MFMA row sums, 32 queries per wave) with
-    // unscaled Q, lse and dropout (attn32_bf16<false, true>)
+    // unscaled Q, lse and dropout (attn32_dma<false, true>)
     const int nqb3 = cdiv(L, a32::QPB);
     const long nb3 = (long)nqb3 * heads * nseq;
     SNV_CHECK_ARG(nb3 < (1L << 31), "grid too large");
-    const char* reg = getenv("SNVRAG_ATTN_REGSTAGE");   // A/B: the register-staged kernel
-    if (reg && reg[0] == '1')
-      hipLaunchKernelGGL((attn32_bf16<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
-                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
-                         lse, drop);
-    else
-      hipLaunchKernelGGL((attn32_dma<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
-                         (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
-                         (long)nseq * L, lse, drop);
-  } else if (dh == 32)
-    hipLaunchKernelGGL(attn_fwd_bf16<32>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
-                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);
-  else if (dh == 64)
+    hipLaunchKernelGGL((attn32_dma<false, true>), dim3((unsigned)nb3), dim3(256), 0, s, (int)L, heads,
+                       (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb3, attn_fallback_counter(),
+                       (long)nseq * L, lse, drop);
+  } else if (dh == 64)
     hipLaunchKernelGGL(attn_fwd_bf16<64>, dim3((unsigned)nb), dim3(256), 0, s, (int)nseq, (int)L, heads,
                        (const bf16*)qkv, (long)ld_qkv, (bf16*)out, (long)ld_out, sl2, nqb, lse, drop);
   else

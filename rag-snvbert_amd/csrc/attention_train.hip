@@ -392,12 +392,10 @@ __device__ __forceinline__ bf16x8 tfrag(const char* im, int e, int c, int li, in
 __device__ __forceinline__ bf16x8 rowfrag(const char* im, int row, int lg) {
   return *reinterpret_cast<const bf16x8*>(im + img(row, lg));
 }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
-                                           0x00020000);
-}
-__device__ __forceinline__ void dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) char*)lds, 16, voff, soff, 0, 0);
+__device__ __forceinline__ i32x4 rsrc(const void* base, long bytes) { return dma_rsrc(base, bytes); }
+// LDS-DMA by inline asm (common.h dma_x4): no compiler-inserted ring drains
+__device__ __forceinline__ void dma(const i32x4& r, const char* lds, int voff, int soff) {
+  dma_x4(r, lds_addr(lds), voff, soff);
 }
 }  // namespace b32
 
@@ -419,13 +417,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv32(int L, int H, const bf16* 
   const int key = kb * 64 + wave * 16 + li;
   const uint32_t dbase = drop_base(drop.seed, (uint32_t)sh);
   const bf16x8 kf = key < L ? *reinterpret_cast<const bf16x8*>(qkv + (row0 + key) * ld + D + h * 32 + 8 * lg) : bf16x8{};
-  const bf16x8 vf = key < L ? *reinterpret_cast<const bf16x8*>(qkv + (row0 + key) * ld + 2 * D + h * 32 + 8 * lg) : bf16x8{};
+  bf16x8 vf = key < L ? *reinterpret_cast<const bf16x8*>(qkv + (row0 + key) * ld + 2 * D + h * 32 + 8 * lg) : bf16x8{};
+  bf16x8 kf_ = kf;
+  asm volatile("" : "+v"(kf_), "+v"(vf));        // retire the loads before the DMA ring (dma_x4)
 
   // this wave's pieces of a tile: Q / dO rows 16 wave + lane / 4 (image position lane % 4), and
   // lanes 0..3: lse / D of queries 16 wave + 4 lane .. + 3 (rows past L: the buffer's zeros)
-  const __amdgpu_buffer_rsrc_t rq = rsrc(qkv + row0 * ld, (total_rows - row0) * ld * 2);
-  const __amdgpu_buffer_rsrc_t ro = rsrc(dO + row0 * lddo, (total_rows - row0) * lddo * 2);
-  const __amdgpu_buffer_rsrc_t rl = rsrc(lse + srow, (long)L * 4), rd = rsrc(Dq + srow, (long)L * 4);
+  const i32x4 rq = rsrc(qkv + row0 * ld, (total_rows - row0) * ld * 2);
+  const i32x4 ro = rsrc(dO + row0 * lddo, (total_rows - row0) * lddo * 2);
+  const i32x4 rl = rsrc(lse + srow, (long)L * 4), rd = rsrc(Dq + srow, (long)L * 4);
   const int prow = 16 * wave + (lane >> 2), pc = img_src(prow, lane & 3);
   const int vq = (int)(prow * ld * 2) + (h * 32 + 8 * pc) * 2;
   const int vo = (int)(prow * lddo * 2) + (h * 32 + 8 * pc) * 2;
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv32(int L, int H, const bf16* 
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
-      s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(qi, 16 * qt + li, lg), kf, z, 0, 0, 0);
+      s[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(qi, 16 * qt + li, lg), kf_, z, 0, 0, 0);
       dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(oi, 16 * qt + li, lg), vf, z, 0, 0, 0);
       l4[qt] = *reinterpret_cast<const f32x4*>(lf + qt * 32 + 4 * lg);
       d4[qt] = *reinterpret_cast<const f32x4*>(lf + qt * 32 + 16 + 4 * lg);
@@ -505,9 +505,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv32(int L, int H, const bf16* 
     if (j < ntile) issue(j, j);
   auto step = [&](auto s_tag, int t) __attribute__((always_inline)) {
     constexpr int S = decltype(s_tag)::value;
-    wait(min(NS - 2, ntile - 1 - t));
+    wait(NS - 2);                       // unrolled loop (t + NS <= ntile): NS - 2 younger tiles in flight
     __builtin_amdgcn_s_barrier();
-    if (t + NS - 1 < ntile) issue(t + NS - 1, (S + NS - 1) % NS);
+    issue(t + NS - 1, (S + NS - 1) % NS);
     if ((t + 1) * 64 <= L) body(smem + S * SLOT, t, std::false_type{});
     else body(smem + S * SLOT, t, std::true_type{});
   };
@@ -565,11 +565,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq32(int L, int H, const bf16* _
   dq_ += __shfl_xor(dq_, 16, 64);
   dq_ += __shfl_xor(dq_, 32, 64);
   const long srow = ((long)seq * H + h) * L;
-  const float lse_q = qv ? lse[srow + q] : 0.f;
+  float lse_q = qv ? lse[srow + q] : 0.f;
   const uint32_t dbase = drop_base(drop.seed, (uint32_t)sh);
   if (qv && lg == 0) Dout[srow + q] = dq_;
+  bf16x8 qf_ = qf, df_ = df;
+  asm volatile("" : "+v"(qf_), "+v"(df_), "+v"(lse_q));   // retire the loads before the DMA ring (dma_x4)
 
-  const __amdgpu_buffer_rsrc_t rk = rsrc(qkv + row0 * ld, (total_rows - row0) * ld * 2);
+  const i32x4 rk = rsrc(qkv + row0 * ld, (total_rows - row0) * ld * 2);
   const int prow = 16 * wave + (lane >> 2), pc = img_src(prow, lane & 3);
   const int vk = (int)(prow * ld * 2) + (D + h * 32 + 8 * pc) * 2;
   const int vv = (int)(prow * ld * 2) + (2 * D + h * 32 + 8 * pc) * 2;
@@ -594,8 +596,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq32(int L, int H, const bf16* _
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(ki, 16 * kt + li, lg), qf, z, 0, 0, 0);
-      dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(vi, 16 * kt + li, lg), df, z, 0, 0, 0);
+      s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(ki, 16 * kt + li, lg), qf_, z, 0, 0, 0);
+      dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag(vi, 16 * kt + li, lg), df_, z, 0, 0, 0);
     }
     const uint32_t drow = drop_row(dbase, (uint32_t)q, (uint32_t)(32 * t + 2 * lg));
     bf16x8 dsb[2];
@@ -623,9 +625,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq32(int L, int H, const bf16* _
     if (j < ntile) issue(j, j);
   auto step = [&](auto s_tag, int t) __attribute__((always_inline)) {
     constexpr int S = decltype(s_tag)::value;
-    wait(min(NS - 2, ntile - 1 - t));
+    wait(NS - 2);                       // unrolled loop (t + NS <= ntile): NS - 2 younger tiles in flight
     __builtin_amdgcn_s_barrier();
-    if (t + NS - 1 < ntile) issue(t + NS - 1, (S + NS - 1) % NS);
+    issue(t + NS - 1, (S + NS - 1) % NS);
     if ((t + 1) * 64 <= L) body(smem + S * SLOT, t, std::false_type{});
     else body(smem + S * SLOT, t, std::true_type{});
   };
@@ -664,7 +666,7 @@ static int launch_bwd(long nseq, long L, int H, const bf16* qkv, long ld, const 
   SNV_CHECK_ARG(grid < (1L << 31), "grid too large");
   const float cl = scale * 1.4426950408889634f;
   evlog_begin(s);
-  if (DH == 32 && !getenv("SNVRAG_ATTN_BWD_V1")) {
+  if constexpr (DH == 32) {
     const long rows = nseq * L;
     hipLaunchKernelGGL(attn_bwd_dq32, dim3((unsigned)grid), dim3(256), 0, s, (int)L, H, qkv, ld, O, ldo, dO, lddo,
                        lse, Dws, dqkv, ldd, cl, scale, nb, drop, rows);

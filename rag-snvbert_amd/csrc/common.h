@@ -6,6 +6,10 @@
 #include <string>
 #include <type_traits>
 
+// the inline-asm LDS-DMA (dma_x4) names m0, which the compiler reserves: it rematerialises m0
+// before each of its own uses, so the clobber is safe here
+#pragma clang diagnostic ignored "-Winline-asm"
+
 #include "../../include/snvrag.h"
 
 namespace snvrag {
@@ -48,10 +52,64 @@ int fail(const char* where, const std::string& msg);
       return ::snvrag::fail(__func__, hipGetErrorString(e_));        \
   } while (0)
 
+// Library options: tuning switches of the micro-benchmarks (tools/) and test hooks.  Each is
+// initialised ONCE from the environment variable SNVRAG_<NAME> (upper case) at first use and can
+// be changed through snvrag_set_option; launch paths read this struct, never the environment.
+struct Options {
+  int64_t knn_no_reduce;   // 1: the kNN scan always runs both int8 limbs (test: == the reduced scan)
+  int64_t scan_mode;       // scan2 pipeline variant (tools/knn_probe.py), 0 = default
+  int64_t scan_nt;         // -1 auto (non-temporal code stream when one query group reads it), 0 / 1
+  int64_t unfused_ln;      // 1: the encoder without the fused block tail (test: fused == unfused)
+  int64_t encoder_chunk;   // sequences per encoder chunk, 0 = auto
+  int64_t gemm_tile128;    // 1: the 128-tile GEMM instead of the row-panel GEMM (tools/gemm_micro.py)
+  int64_t gemm_nw;         // row-panel GEMM tile width (1, 2, 4, 6 x 64 columns), 0 = auto
+  int64_t tail_variant;    // block-tail diagnostic instantiation (tools/tail_micro.py), 0 = default
+  int64_t tail_desync;     // block-tail first-round stagger in cycles, -1 = auto
+  int64_t sg_desync;       // stream-GEMM first-round stagger in cycles, -1 = auto
+  int64_t sg_waves4;       // 1: 4-wave stream GEMM for the rank-free projections (A/B)
+  int64_t ln_bwd_nopf;     // 1: LayerNorm backward without the next-row prefetch (A/B)
+};
+Options& options();
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ------------------------------------------------------------------ device --
+// A buffer resource (V#) in four SGPRs for the inline-asm LDS-DMA below: base, stride 0,
+// num_records = ``bytes`` (clamped to 2^31 - 1; reads past it return 0), dword 3 = 0x00020000
+// (the same raw-buffer format __builtin_amdgcn_make_buffer_rsrc is given in this library).
+__device__ __forceinline__ i32x4 dma_rsrc(const void* base, long bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
+  r[3] = 0x00020000;
+  return r;
+}
+
+// LDS-DMA of one 16-B piece per lane (1 KiB per wave): buffer_load_dwordx4 ... lds into the LDS
+// bytes [lds, lds + 1024) (lane i -> lds + 16 i), source = base + voffset + soffset.  Issued by
+// inline asm so that the compiler's waitcnt pass does not see an LDS store: with the builtin it
+// treats every later ds_read of the same __shared__ array as aliasing EVERY DMA in flight and
+// inserts s_waitcnt vmcnt before it (e.g. vmcnt(0) before each tile's reads in a prefetch ring:
+// the ring collapses to synchronous loads).  The caller owns the ordering: a counted
+// s_waitcnt vmcnt (this wave's pieces) and a barrier (the other waves') before reading — and
+// must retire any compiler-visible global load whose first use is inside the ring loop before
+// the loop (asm volatile("" : "+v"(x))), or its wait lands in the loop as vmcnt(0).
+// ``lds`` is the wave-uniform LDS byte address (lds_addr()).
+__device__ __forceinline__ void dma_x4(const i32x4& rsrc, uint32_t lds, int voffset, int soffset) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds), "v"(voffset), "s"(rsrc), "s"(soffset)
+               : "memory", "m0");
+}
+// LDS byte address of a pointer into a __shared__ array: the low 32 bits of its flat address
+// (the shared aperture is the high dword), without the null check of an address-space cast
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)p);
+}
+
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f32(float x);

@@ -14,8 +14,7 @@
 // ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i
 // receives column i of the 4 rows): two such reads are one 8-k MFMA fragment, A[n][m] = dY[m][n]
 // and B[m][k] = X[m][k].  Rows are 256 B; the 32-B column blocks are XOR-swizzled by (row & 7)
-// so the four rows of a transposed read fall in different banks.  Global -> LDS is register
-// staged, double buffered (the next stage's loads in flight under this stage's MFMAs).
+// so the four rows of a transposed read fall in different banks.
 #include "common.h"
 
 #include <cstdlib>
@@ -46,119 +45,10 @@ struct DwOut {
   int seg;
 };
 
-__global__ __launch_bounds__(256) void dw_kernel(int M, int N, int K, const bf16* __restrict__ dy, long ldy,
-                                                 const bf16* __restrict__ x, long ldx, DwOut out, int chunk) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * DW_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 1, wk = wave & 1;
-  const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
-  const int part = n0 / out.seg;                     // a 128-row tile lies in one part (seg % 128 == 0)
-  const int nbase = part * out.seg;                  // first n of the part
-  float* __restrict__ dw = out.w[part];
-  float* __restrict__ db = out.b[part];
-  const int m_begin = blockIdx.z * chunk;
-  const int m_end = min(M, m_begin + chunk);
-  if (m_begin >= m_end) return;                      // whole workgroup, before any barrier
-  const int nst = (m_end - m_begin + DW_R - 1) / DW_R;
-
-  // loader: stage = 32 rows x 256 B of dY and of X = 2 x 512 16-B chunks; thread t moves chunks
-  // t and t + 256 of each
-  u32x4 ry[2], rx[2];
-  auto load = [&](int st) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, c16 = c & 15;
-      const int m = m_begin + st * DW_R + row;
-      const bool ok = m < m_end;
-      ry[i] = ok ? *reinterpret_cast<const u32x4*>(dy + (long)m * ldy + n0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
-      rx[i] = ok ? *reinterpret_cast<const u32x4*>(x + (long)m * ldx + k0 + 8 * c16) : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto store = [&](int buf) {
-    char* s = smem + buf * DW_STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 4, c16 = c & 15;
-      *reinterpret_cast<u32x4*>(s + dw_swz(row, 16 * c16)) = ry[i];
-      *reinterpret_cast<u32x4*>(s + DW_R * 256 + dw_swz(row, 16 * c16)) = rx[i];
-    }
-  };
-
-  // transposed-read addresses: 16-lane group g = lane / 16 takes columns 16 (g & 1) .. + 15 of
-  // its 32-column MFMA tile and rows 8 (g >> 1) + 4 h .. + 3 (h = first / second read)
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int rowb = 8 * (g >> 1) + q;                 // + 16 s (k-step) + 4 h
-  const int colb = 2 * (16 * (g & 1) + 4 * p);       // bytes, + 64 T within the wave's 64 columns
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
-  const bool do_db = db != nullptr && blockIdx.y == 0 && wk == 0;
-  float dbs[2] = {0.f, 0.f};
-
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const bool more = st + 1 < nst;
-    if (more) load(st + 1);
-    const char* s = smem + (st & 1) * DW_STAGE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int r0 = 16 * ks + rowb;
-        const int ca = 128 * wn + 64 * t + colb;     // bytes within the dY tile row
-        const int cb = 128 * wk + 64 * t + colb;
-        const bf16x4 a0 = dw_tr(s + dw_swz(r0, ca)), a1 = dw_tr(s + dw_swz(r0 + 4, ca));
-        const bf16x4 b0 = dw_tr(s + DW_R * 256 + dw_swz(r0, cb)), b1 = dw_tr(s + DW_R * 256 + dw_swz(r0 + 4, cb));
-        fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-        fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-      if (do_db) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dbs[a] += (float)fa[a][j];
-      }
-    }
-    if (more) store((st + 1) & 1);
-    __syncthreads();
-  }
-
-  // C layout of 32x32x16: lane holds column k = lane % 32 and rows 8 (e / 4) + 4 (lane / 32) + e % 4
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int kk = k0 + 64 * wk + 32 * b + (lane & 31);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int nn = n0 + 64 * wn + 32 * a + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
-        unsafeAtomicAdd(dw + (long)(nn - nbase) * K + kk, acc[a][b][e]);
-      }
-    }
-  if (do_db) {
-    // A-fragment lanes l and l + 32 hold the same column n (rows 0..7 / 8..15 of each k-step)
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const float v = dbs[a] + __shfl_xor(dbs[a], 32, 64);
-      if (lane < 32) unsafeAtomicAdd(db + (n0 - nbase) + 64 * wn + 32 * a + lane, v);
-    }
-  }
-}
-
-// dw_dma_kernel: the same tiles, fragments and epilogue with the 32-row stages brought in by
-// LDS-DMA (buffer_load ... lds, 1 KiB = 4 rows of one operand per wave instruction) through a
-// 4-slot ring, 3 stages in flight, one barrier per stage.  The register-staged kernel above moves
-// every operand byte through VGPRs and a ds_write_b128 (≈79 B/clk/CU of LDS store transfer) with
-// one stage of look-ahead; here the XOR swizzle of dw_swz is applied to the SOURCE column of each
+// dw_dma_kernel: the 32-row stages brought in by LDS-DMA (buffer_load ... lds, 1 KiB = 4 rows of
+// one operand per wave instruction) through a 4-slot ring, 3 stages in flight, one barrier per
+// stage (r3: replaced a register-staged kernel that moved every operand byte through VGPRs and a
+// ds_write_b128 with one stage of look-ahead).  The XOR swizzle of dw_swz is applied to the SOURCE column of each
 // lane (the LDS side of a DMA piece is contiguous) and rows past the chunk read the buffer's zeros.
 constexpr int DWD_NS = 4;
 
@@ -325,12 +215,8 @@ static int launch_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ld
   const int chunk = (int)((((M + splits - 1) / splits) + DW_R - 1) / DW_R * DW_R);
   const int S = (int)((M + chunk - 1) / chunk);
   evlog_begin(s);
-  if (getenv("SNVRAG_DW_V1"))                         // A/B: the register-staged kernel
-    hipLaunchKernelGGL(dw_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
-                       (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
-  else
-    hipLaunchKernelGGL(dw_dma_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0,
-                       s, (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
+  hipLaunchKernelGGL(dw_dma_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
+                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
   SNV_LAUNCH_CHECK();
   evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
   return 0;

@@ -20,11 +20,7 @@
 namespace snvrag {
 
 static int64_t chunk_seqs(int64_t nseq, int64_t L, int D, int esz) {
-  const char* e = getenv("SNVRAG_ENCODER_CHUNK");
-  if (e) {
-    const long v = atol(e);
-    if (v > 0) return std::min<int64_t>(v, nseq);
-  }
+  if (options().encoder_chunk > 0) return std::min<int64_t>(options().encoder_chunk, nseq);
   // The row-panel GEMMs tile M by 128 rows with whole output rows per tile, so a chunk
   // must hold >= ~4 tiles per CU (1024 tiles = 131k rows) to fill 256 CUs; cap the
   // per-chunk workspace (10 D / token) at ~16 GB of the 288 GB HBM; chunks are balanced
@@ -72,7 +68,7 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
   const int dh = D / heads;
   const float scale = 1.0f / sqrtf((float)dh);
 
-  const bool fused = (D == 64 || D == 128 || D == 256 || D == 384) && !getenv("SNVRAG_UNFUSED_LN") &&
+  const bool fused = (D == 64 || D == 128 || D == 256 || D == 384) && !options().unfused_ln &&
                      layers[0].w2g && layers[0].b2g && layers[0].c2g;
   for (int64_t s0 = 0; s0 < nseq; s0 += cs) {
     const int64_t ns = std::min<int64_t>(cs, nseq - s0);

@@ -236,7 +236,7 @@ extern "C" int snvrag_linear_ex(int dtype_in, int dtype_out, int64_t M, int64_t 
   if (M == 0) return 0;
   const int ept = dtype_in == SNVRAG_BF16 ? 64 : 32;
   const bool fused = anorm || (epi && (epi->ln_g || epi->stats_out));
-  const bool rows_ok = N % 64 == 0 && K % ept == 0 && !getenv("SNVRAG_GEMM_TILE128");
+  const bool rows_ok = N % 64 == 0 && K % ept == 0 && !options().gemm_tile128;
   if (fused || rows_ok) {               // row-panel GEMM (checks its own shape constraints)
     hipStream_t s = as_stream(stream);
     evlog_begin(s);

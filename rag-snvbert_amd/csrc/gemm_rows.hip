@@ -3,10 +3,8 @@
 // C[128 x BN] tiles, BN = 64*NW (NW = 6 -> 384 = the model width D, so one tile
 // holds whole output rows), 512 threads = 8 waves in a 2 (M) x 4 (N) grid, each
 // wave 64 x 16*NW = 4 x NW MFMA 16x16 tiles.  Operands are staged with
-// global_load_lds (16 B / lane, 1 KiB per wave instruction) into a 4-stage LDS
-// ring of 64-B K-tile rows with three K-tiles in flight across raw s_barriers
-// (counted s_waitcnt vmcnt(N); guide §5 'Pipelining across barriers'); narrow
-// tiles use a 2-stage ring of 128-B rows.  The XOR swizzle of the ds_read_b128
+// global_load_lds (16 B / lane, 1 KiB per wave instruction) into a 2-stage LDS
+// ring of 128-B K-tile rows (one tile in flight under the MFMAs of the other).  The XOR swizzle of the ds_read_b128
 // fragment reads is applied on the SOURCE address (the LDS image of a glds is
 // lane-linear) — guide §5 rule 21.
 //
@@ -86,15 +84,15 @@ __device__ __forceinline__ float maf_w(float af) {
   return fminf(log1pf(1.0f / (maf + 1e-6f)), 3.0f);
 }
 
-// DEEP: 64-B K-tile rows, 4 LDS stages, 3 tiles in flight (counted vmcnt, raw barriers)
-// else: 128-B K-tile rows, 2 stages, vmcnt(0) + barrier per tile.
-template <typename TI, typename TO, int NW, bool DEEP, bool ROWNORM>
+// 128-B K-tile rows, 2 LDS stages: the next tile's global_load_lds in flight under this tile's
+// MFMAs, vmcnt(0) + barrier per tile (a 64-B, 4-stage ring with 3 tiles in flight measured slower).
+template <typename TI, typename TO, int NW, bool ROWNORM>
 __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, const TI* __restrict__ A, long lda,
                                                         const TI* __restrict__ W, long ldw, TO* __restrict__ C,
                                                         long ldc, EpiX epi, RowNorm rn, int n_tiles_n) {
   constexpr int BN = 64 * NW;
-  constexpr int ROWB = DEEP ? 64 : 128;
-  constexpr int NST = DEEP ? 4 : 2;
+  constexpr int ROWB = 128;
+  constexpr int NST = 2;
   constexpr int CPR = ROWB / 16;                   // 16-B chunks per tile row
   constexpr int RPI = 1024 / ROWB;                 // rows per 1-KiB glds wave instruction
   constexpr int EPC = 16 / sizeof(TI);
@@ -198,32 +196,15 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
     }
   };
 
-  if constexpr (DEEP) {
-    // prologue: tiles 0..2 in flight
-#pragma unroll
-    for (int t = 0; t < NST - 1; ++t)
-      if (t < nk) issue(t, t * EPT);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int ahead = min(NST - 2, nk - 1 - kt);     // tiles allowed to stay in flight
-      if (ahead >= 2) vm_wait<2 * P>();
-      else if (ahead == 1) vm_wait<P>();
-      else vm_wait<0>();
-      __builtin_amdgcn_s_barrier();                    // tile kt landed everywhere; stage kt-1 free
-      if (kt + NST - 1 < nk) issue((kt + NST - 1) % NST, (kt + NST - 1) * EPT);
-      compute(kt % NST);
-    }
-    __syncthreads();
-  } else {
-    issue(0, 0);
+  issue(0, 0);
+  vm_wait<0>();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue(cur ^ 1, (kt + 1) * EPT);
+    compute(cur);
     vm_wait<0>();
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) issue(cur ^ 1, (kt + 1) * EPT);
-      compute(cur);
-      vm_wait<0>();
-      __syncthreads();
-    }
   }
 
   // ---------------------------------------------------------------- epilogue --
@@ -368,16 +349,16 @@ __global__ __launch_bounds__(512) void rows_gemm_kernel(int M, int N, int K, con
   }
 }
 
-template <typename TI, typename TO, int NW, bool DEEP, bool RN>
+template <typename TI, typename TO, int NW, bool RN>
 static int launch_rows_v(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
                          const EpiX& e, const RowNorm& rn, hipStream_t s) {
   constexpr int BN = 64 * NW;
-  constexpr int ROWB = DEEP ? 64 : 128, NST = DEEP ? 4 : 2;
+  constexpr int ROWB = 128, NST = 2;
   const int tn = cdiv(N, BN), tm = cdiv(M, R_BM);
   const long nb = (long)tn * tm;
   SNV_CHECK_ARG(nb < (1L << 31), "grid too large");
   const size_t lds = NST * (size_t)(R_BM + BN) * ROWB + R_BM * sizeof(float2) + 6 * BN * sizeof(float);
-  auto kern = rows_gemm_kernel<TI, TO, NW, DEEP, RN>;
+  auto kern = rows_gemm_kernel<TI, TO, NW, RN>;
   static bool attr = false;
   if (!attr) {
     SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -392,16 +373,9 @@ static int launch_rows_v(long M, long N, long K, const void* A, long lda, const 
 template <typename TI, typename TO, int NW>
 static int launch_rows(long M, long N, long K, const void* A, long lda, const void* W, long ldw, void* C, long ldc,
                        const EpiX& e, const RowNorm* rn, hipStream_t s) {
-  // deep glds ring for the wide tiles (3 or 4 glds per wave per K-tile); K must hold 64-B tiles
-  constexpr bool DEEP_OK = NW == 4 || NW == 6;
-  const bool deep = DEEP_OK && getenv("SNVRAG_GEMM_DEEP");   // measured: the 2-stage 128-B ring is faster
   RowNorm r = rn ? *rn : RowNorm{};
-  if (deep) {
-    if (rn) return launch_rows_v<TI, TO, NW, DEEP_OK, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
-    return launch_rows_v<TI, TO, NW, DEEP_OK, false>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
-  }
-  if (rn) return launch_rows_v<TI, TO, NW, false, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
-  return launch_rows_v<TI, TO, NW, false, false>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+  if (rn) return launch_rows_v<TI, TO, NW, true>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
+  return launch_rows_v<TI, TO, NW, false>(M, N, K, A, lda, W, ldw, C, ldc, e, r, s);
 }
 
 template <typename TI, typename TO>
@@ -417,7 +391,7 @@ static int dispatch_nw(int nw, long M, long N, long K, const void* A, long lda, 
 
 // tile width for an N: prefer 384 (6), then 256, 128, 64; 0 = unsupported
 int rows_pick_nw(long N, bool need_full_row) {
-  static const int force = getenv("SNVRAG_GEMM_NW") ? atoi(getenv("SNVRAG_GEMM_NW")) : 0;
+  const int force = (int)options().gemm_nw;
   if (force && !need_full_row && N % (64L * force) == 0 && (force == 1 || force == 2 || force == 4 || force == 6))
     return force;
   const int cands[4] = {6, 4, 2, 1};

@@ -861,17 +861,15 @@ static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* code
   static_assert(NST * STAGE + S2_CAND <= S2_LDS, "LDS budget");
   auto kern = scan2_kernel<KS, LB, 0>;
   if constexpr (KS == 16 && LB == 2) {
-    const char* m = getenv("SNVRAG_SCAN_MODE");
-    if (m && m[0] == '1') kern = scan2_kernel<KS, LB, 1>;
-    if (m && m[0] == '2') kern = scan2_kernel<KS, LB, 2>;
+    if (options().scan_mode == 1) kern = scan2_kernel<KS, LB, 1>;
+    if (options().scan_mode == 2) kern = scan2_kernel<KS, LB, 2>;
   }
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int G = ((nq + 15) / 16 + 7) / 8;
   const long nwg = (long)((n_parts + 7) / 8) * 8 * G;
   // one query group: every code byte is read by exactly one workgroup, so stream it with
   // the non-temporal policy; with G > 1 the other groups read the range from L2 (default)
-  const char* pol = getenv("SNVRAG_SCAN_NT");
-  const int nt = pol ? (pol[0] == '1') : (G == 1);
+  const int nt = options().scan_nt >= 0 ? (int)(options().scan_nt != 0) : (G == 1);
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), lds, s, codes, n_ref, ld, lut, nq, k, range, off, parts, th,
                      wide, n_parts, G, nt);
 }
@@ -996,12 +994,12 @@ extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_c
   hipStream_t s = as_stream(stream);
   const int8_t* L8 = (const int8_t*)lut;
   // lut_kernel's "some query needs two limbs" flag (limbs == 2 buffers only)
-  const int* wide = (limbs == 2 && !getenv("SNVRAG_KNN_NO_REDUCE"))
+  const int* wide = (limbs == 2 && !options().knn_no_reduce)
                         ? reinterpret_cast<const int*>(L8 + lut_tail_offset(nq, n_sites_pad) +
                                                        (size_t)((nq + 15) / 16) * 16 * 4)
                         : nullptr;
   evlog_begin(s);
-  const bool v2 = n_sites_pad % 256 == 0 && n_sites_pad <= 1280 && !getenv("SNVRAG_SCAN_V1");
+  const bool v2 = n_sites_pad % 256 == 0 && n_sites_pad <= 1280;
   if (v2) {
 #define SCAN2(K_)                                                                                          \
   case K_:                                                                                                 \

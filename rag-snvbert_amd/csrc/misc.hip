@@ -1,6 +1,8 @@
 // Error reporting, ABI/device queries and MFMA layout self-tests.
 #include "common.h"
 
+#include <cctype>
+#include <cstdlib>
 #include <cstring>
 
 namespace snvrag {
@@ -88,6 +90,53 @@ __global__ void mfma_selftest_kernel(int* errors) {
 }  // namespace snvrag
 
 using namespace snvrag;
+
+namespace snvrag {
+namespace {
+struct OptDesc { const char* name; int64_t Options::*field; int64_t dflt; };
+const OptDesc kOpts[] = {
+    {"knn_no_reduce", &Options::knn_no_reduce, 0}, {"scan_mode", &Options::scan_mode, 0},
+    {"scan_nt", &Options::scan_nt, -1},            {"unfused_ln", &Options::unfused_ln, 0},
+    {"encoder_chunk", &Options::encoder_chunk, 0}, {"gemm_tile128", &Options::gemm_tile128, 0},
+    {"gemm_nw", &Options::gemm_nw, 0},             {"tail_variant", &Options::tail_variant, 0},
+    {"tail_desync", &Options::tail_desync, -1},    {"sg_desync", &Options::sg_desync, -1},
+    {"sg_waves4", &Options::sg_waves4, 0},         {"ln_bwd_nopf", &Options::ln_bwd_nopf, 0},
+};
+Options make_options() {
+  Options o{};
+  for (const OptDesc& d : kOpts) {
+    std::string env = "SNVRAG_";
+    for (const char* c = d.name; *c; ++c) env += (char)toupper(*c);
+    const char* v = getenv(env.c_str());
+    o.*(d.field) = v ? atoll(v) : d.dflt;
+  }
+  return o;
+}
+const OptDesc* find_opt(const char* name) {
+  for (const OptDesc& d : kOpts)
+    if (name && strcmp(d.name, name) == 0) return &d;
+  return nullptr;
+}
+}  // namespace
+Options& options() {
+  static Options o = make_options();
+  return o;
+}
+}  // namespace snvrag
+
+extern "C" int snvrag_set_option(const char* name, int64_t value) {
+  const snvrag::OptDesc* d = snvrag::find_opt(name);
+  if (!d) return fail(__func__, std::string("unknown option ") + (name ? name : "(null)"));
+  snvrag::options().*(d->field) = value;
+  return 0;
+}
+
+extern "C" int snvrag_get_option(const char* name, int64_t* value) {
+  const snvrag::OptDesc* d = snvrag::find_opt(name);
+  if (!d || !value) return fail(__func__, std::string("unknown option ") + (name ? name : "(null)"));
+  *value = snvrag::options().*(d->field);
+  return 0;
+}
 
 extern "C" int snvrag_abi_version(void) { return SNVRAG_ABI_VERSION; }
 extern "C" const char* snvrag_last_error(void) { return g_err.c_str(); }

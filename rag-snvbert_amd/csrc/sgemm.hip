@@ -654,8 +654,8 @@ static int sg_launch(SgArgs a, hipStream_t s) {
   // first-round phase step (tail.hip's de-synchronised rounds): 10 k cycles for the 8-wave
   // projections (QKV at M = 527 360: 0.559 -> 0.540 ms; 20 k / 30 k: 0.557 / 0.584,
   // tools/proj_micro.py); SNVRAG_SG_DESYNC overrides
-  const char* dz = getenv("SNVRAG_SG_DESYNC");
-  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 ? (dz ? atoi(dz) : (WAVES == 8 ? 10000 : 0)) : 0;
+  const int64_t dz = options().sg_desync;
+  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 ? (dz >= 0 ? (int)dz : (WAVES == 8 ? 10000 : 0)) : 0;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -679,7 +679,7 @@ static int sg_dispatch(int epi, int act, bool rank, const SgArgs& a, hipStream_t
   if constexpr (D == 384) {
     // 8 waves (256 rows per workgroup) for the projections: 15-22 % faster than 4
     // (tools/proj_micro.py); SNVRAG_SG_WAVES4 forces 4 (A/B)
-    static const bool w8 = getenv("SNVRAG_SG_WAVES4") == nullptr;
+    const bool w8 = !options().sg_waves4;
     // (the rank and head variants need more than 256 registers: 4 waves)
     if (w8 && !rank && act == SNVRAG_ACT_NONE) return sg_launch<D, SG_ACT, SNVRAG_ACT_NONE, false, 8>(a, s);
     if (w8 && !rank && act == SNVRAG_ACT_GELU) return sg_launch<D, SG_ACT, SNVRAG_ACT_GELU, false, 8>(a, s);

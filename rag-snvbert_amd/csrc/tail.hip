@@ -673,8 +673,7 @@ static unsigned long long* g_tail_stamps = nullptr;   // snvrag_tail_stamps (dia
 
 template <int D, bool PRE>
 static int launch_tail(TailArgs a, hipStream_t s) {
-  const char* ev = getenv("SNVRAG_TAIL_VARIANT");
-  const int var = ev ? atoi(ev) : 0;
+  const int var = (int)options().tail_variant;
   auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
               : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false>
               : var == 5 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 3> : tail_kernel<D, PRE>;
@@ -685,9 +684,9 @@ static int launch_tail(TailArgs a, hipStream_t s) {
   // first-round phase step: only when every CU runs several rounds (the delay is paid once).
   // Default 1/8 of a block's ~200 k cycles at D = 384 (tools/tail_micro.py, M = 527 360:
   // 1.668 ms without, 1.611 / 1.593 / 1.602 ms at 12 k / 25 k / 40 k), scaled with the D^2 work
-  const char* dz = getenv("SNVRAG_TAIL_DESYNC");
   const long nwg = cdiv(a.M, TL_ROWS);
-  a.desync = nwg >= 8 * 256 ? (dz ? atoi(dz) : 25000 * D / 384 * D / 384) : 0;
+  const int64_t dz = options().tail_desync;
+  a.desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 25000 * D / 384 * D / 384) : 0;
   constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + 7 * D * 4;     // ring + b1, g1, be1, b_o
   static_assert(7 * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

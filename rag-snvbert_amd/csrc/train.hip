@@ -865,7 +865,7 @@ extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s
   // one row per wave step (2 rows: 174 -> 209 us at N = 1536, tools/ln_micro.py); for N > 512 the
   // next row's loads issued ahead (N = 1536: 147-150 vs 174 us; N = 384: 55 vs 52 us, so not there)
   // unless SNVRAG_LN_BWD_NOPF (A/B)
-  static const bool pf = getenv("SNVRAG_LN_BWD_NOPF") == nullptr;
+  const bool pf = !options().ln_bwd_nopf;
   if (pf && nch > 1) {
     if (nch == 2) go(ln_bwd_pf_kernel<2>);
     else if (nch == 3) go(ln_bwd_pf_kernel<3>);

@@ -228,9 +228,11 @@ def direct_weight_grads(enabled: bool = True):
     and db straight into the parameters' f32 ``.grad`` (the flat gradient buffer of
     ``FlatParams``) with the dW kernel, instead of returning fresh tensors that autograd then
     adds in with one kernel per parameter (and zero-fills before: ~300 small launches per
-    step).  Those parameters get no autograd accumulation, so the post-accumulate hooks are
-    replaced by ``p._snv_grad_ready(p)`` (set by ``GradBucketer``).  Outside the context (e.g.
-    ``torch.autograd.grad``), gradients are returned as usual."""
+    step).  Autograd still runs each such parameter's AccumulateGrad node once per backward,
+    after the LAST use of the parameter has run its backward (with an undefined gradient, so
+    nothing is added), and its post-accumulate hooks fire there — exactly once per parameter
+    and step, which is what ``GradBucketer`` keys its bucket launches on.  Outside the context
+    (e.g. ``torch.autograd.grad``), gradients are returned as usual."""
     global _DIRECT_GRADS
     prev = _DIRECT_GRADS
     _DIRECT_GRADS = enabled
@@ -243,12 +245,6 @@ def direct_weight_grads(enabled: bool = True):
 def _grad_buffer(p) -> Optional[torch.Tensor]:
     g = p.grad if (p is not None and p.is_leaf and p.requires_grad) else None
     return g if (g is not None and g.dtype == torch.float32 and g.is_contiguous()) else None
-
-
-def _grad_ready(p) -> None:
-    cb = getattr(p, "_snv_grad_ready", None)
-    if cb is not None:
-        cb(p)
 
 
 class _HipLinear(torch.autograd.Function):
@@ -334,8 +330,6 @@ class _HipLinear(torch.autograd.Function):
                 for w, b, sz in zip(pws, pbs, sizes):
                     K.linear_dw(g2[:, off:off + sz], x2, dw=w.grad, db=b.grad if ctx.has_bias else None)
                     off += sz
-            for t in list(pws) + (list(pbs) if ctx.has_bias else []):
-                _grad_ready(t)
             return (gx, None, *([None] * ctx.n), *([None] * ctx.n))
         if any(ctx.needs_input_grad[2:2 + ctx.n]) and dw_ok:
             # dW (and db) on the split-M MFMA kernel (csrc/dw.hip), f32 accumulation and result
@@ -522,8 +516,6 @@ class _HipAddLayerNorm(torch.autograd.Function):
                                     slope_x=slope_x, slope_r=slope_r, r_pre=rp[0] if rp else None)
         dr = (dres if dres is not None else ds) if ctx.has_r else None
         if direct:
-            _grad_ready(w)
-            _grad_ready(b)
             return ds, dr, None, None, None, None, None, None, None, None
         return ds, dr, dg, db, None, None, None, None, None, None
 

@@ -58,6 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--mask_rate", type=float, default=0.3,
                    help="synthetic: fraction of panel sites absent from the target (C5 sweep 0.1..0.9)")
     p.add_argument("--no_vcf", action="store_true")
+    p.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
+                   help="WORLD_SIZE > 1 (torch.distributed.run, one process per GPU): nccl (= RCCL) or gloo "
+                        "(host-staged: the multi-rank tests with every rank on one GPU)")
     return p.parse_args(argv)
 
 
@@ -133,14 +136,43 @@ def build_dataset(args):
     return make_infer_dataset(a, index_window_len=args.index_window_len)
 
 
-def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_len: int = INFER_WINDOW_LEN):
+def rank_rows(n_rows: int, rank: int, world: int):
+    """The contiguous slice of the window-major sampler stream rank ``rank`` imputes: whole
+    sample-windows, ranks in stream order, so each rank touches few windows (few panel-index
+    builds) and the gather is a concatenation in rank order."""
+    return n_rows * rank // world, n_rows * (rank + 1) // world
+
+
+def _gather_rows(t: torch.Tensor, sizes, group=None) -> torch.Tensor:
+    """Concatenate every rank's rows (ragged counts ``sizes``) in rank order."""
+    from .retrieval.shards import _all_gather
+    pad = max(sizes)
+    if t.shape[0] < pad:
+        t = torch.cat([t, t.new_zeros((pad - t.shape[0],) + tuple(t.shape[1:]))])
+    g = _all_gather(t.contiguous(), group)
+    return torch.cat([g[r, :n] for r, n in enumerate(sizes)])
+
+
+def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_len: int = INFER_WINDOW_LEN,
+        group=None):
     """The inference loop (infer_embedding_rag.py:132-157) and geometry (:165-203) over ``ds``
     with an eval ``model`` on ``dev``.  Returns host arrays h1/h2 [n_sites, S], gt
-    [n_sites, S, 4], mask [n_sites, S], the neighbour indices per sampler row and the time."""
+    [n_sites, S, 4], mask [n_sites, S], the neighbour indices per sampler row and the time.
+
+    Several ranks (``torch.distributed`` initialised, configs[4]): the panel is replicated,
+    rank r imputes rows ``rank_rows`` of the window-major stream (batches formed inside its
+    slice), and the per-row outputs are all-gathered in stream order before the geometry — the
+    same arrays as one process (every row's retrieval and forward depend on that row alone).
+    ``seconds`` is the slowest rank's loop time."""
     from .dataset.embedding_rag_dataset import embedding_rag_collate_fn
     from .dataset.sampler import WindowMajorSampler
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
     emb = model.bert.embedding
-    loader = torch.utils.data.DataLoader(ds, batch_size=batch_size, sampler=WindowMajorSampler(ds),
+    order = list(iter(WindowMajorSampler(ds)))
+    lo, hi = rank_rows(len(order), rank, world)
+    loader = torch.utils.data.DataLoader(ds, batch_size=batch_size, sampler=order[lo:hi],
                                          num_workers=num_workers, collate_fn=embedding_rag_collate_fn)
     outs = {"h1": [], "h2": [], "gt": [], "mask": [], "idx1": [], "idx2": []}
     t0 = time.perf_counter()
@@ -158,6 +190,17 @@ def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_le
             outs["idx2"].append(x["rag_idx_h2"])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        sizes = [rank_rows(len(order), r, world)[1] - rank_rows(len(order), r, world)[0] for r in range(world)]
+        full = {}
+        for key, v in outs.items():
+            loc = torch.cat(v) if v else _empty_rows(key, dev, k)
+            loc = loc.long() if key in ("idx1", "idx2", "mask") else loc.float()   # one dtype on every rank
+            full[key] = _gather_rows(loc, sizes, group)
+        outs = {key: [t] for key, t in full.items()}
+        from .retrieval.shards import _all_reduce
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        elapsed = float(_all_reduce(t, dist.ReduceOp.MAX, group).item())
     host = {key: torch.cat(v).cpu().numpy() for key, v in outs.items()}
     h1, h2, gt, mask = geometry(host["h1"], host["h2"], host["gt"], host["mask"], ds.window_count,
                                 len(ds.ori_pos), window_len)
@@ -166,12 +209,30 @@ def run(ds, model, dev, batch_size: int, k: int, num_workers: int = 0, window_le
                 batch_h2=host["h2"])
 
 
+def _empty_rows(key, dev, k):
+    """A rank with no rows (more ranks than sample-windows) contributes zero-row tensors."""
+    shape = {"gt": (0, MAX_SEQ_LEN, 4), "idx1": (0, k), "idx2": (0, k)}.get(key, (0, MAX_SEQ_LEN))
+    dt = torch.long if key in ("idx1", "idx2", "mask") else torch.float32
+    return torch.zeros(shape, device=dev, dtype=dt)
+
+
 def infer(argv=None):
     args = parse_args(argv)
     if not torch.cuda.is_available():
         raise SystemExit("imputation runs on the MI355X kernels only (no CPU fallback)")
-    dev = torch.device(f"cuda:{args.cuda_devices[0] if args.cuda_devices else torch.cuda.current_device()}")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dev = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}")
+    else:
+        dev = torch.device(f"cuda:{args.cuda_devices[0] if args.cuda_devices else torch.cuda.current_device()}")
     torch.cuda.set_device(dev)
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from .engine import engine_for
     from .model import build_model
     ds, vocab = build_dataset(args)
@@ -187,6 +248,8 @@ def infer(argv=None):
     engine_for(model).set_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     res = run(ds, model, dev, args.infer_batch_size, args.k_retrieve, args.num_workers, args.window_len)
     h1, h2, gt, mask = res["h1"], res["h2"], res["gt"], res["mask"]
+    if rank != 0:                      # the gathered arrays are written once
+        return res
     os.makedirs(args.output_path, exist_ok=True)
     np.savez_compressed(os.path.join(args.output_path, "imputed.npz"), hap1=h1, hap2=h2, gp=gt, mask=mask,
                         pos=np.asarray(ds.ori_pos))

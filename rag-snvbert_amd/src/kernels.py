@@ -6,6 +6,8 @@ passed in.  Every call runs on the current HIP stream.  No CPU fallback.
 
 from __future__ import annotations
 
+import contextlib
+
 import ctypes as C
 from typing import Optional, Sequence, Tuple
 
@@ -460,6 +462,26 @@ def encoder_ws_bytes(dtype: torch.dtype, nseq: int, L: int, D: int, heads: int) 
 
 def selftest_mfma() -> int:
     return int(N.lib().snvrag_selftest_mfma(stream_ptr()))
+
+
+def set_option(name: str, value: int) -> int:
+    """Set a library option (snvrag_set_option: test hooks / micro-benchmark switches, see
+    include/snvrag.h); returns the previous value."""
+    import ctypes
+    prev = ctypes.c_int64()
+    check(N.lib().snvrag_get_option(name.encode(), ctypes.byref(prev)), "get_option")
+    check(N.lib().snvrag_set_option(name.encode(), int(value)), "set_option")
+    return int(prev.value)
+
+
+@contextlib.contextmanager
+def option(name: str, value: int):
+    """``with option("knn_no_reduce", 1): ...`` — the previous value restored afterwards."""
+    prev = set_option(name, value)
+    try:
+        yield
+    finally:
+        set_option(name, prev)
 
 
 # ---------------------------------------------------------------- training --

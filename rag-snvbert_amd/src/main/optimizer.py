@@ -11,11 +11,11 @@ the data-parallel wrapper (``nn.DataParallel`` there; one process per GPU here):
   FusedAdam     snvrag_sqnorm + snvrag_adam_step: clip coefficient computed on the
                 device, Adam update and the bf16 mirror in one pass over the buffer —
                 no host synchronisation in the step.
-  GradBucketer  DDP gradient averaging: contiguous buckets of the flat gradient buffer
+  GradBucketer  DDP gradient exchange: contiguous buckets of the flat gradient buffer
                 (parameters laid out in reverse registration order, so buckets fill in
-                backward order) are all-reduced asynchronously (RCCL over xGMI on the
-                GPU, gloo in the CPU tests) as soon as their last gradient is
-                accumulated, overlapping the rest of the backward pass.
+                backward order) are all-reduced (SUM) asynchronously (RCCL over xGMI on the
+                GPU, gloo in the CPU tests) once every parameter in them is final, in one
+                bucket order on every rank, overlapping the rest of the backward pass.
 """
 
 from __future__ import annotations
@@ -118,15 +118,37 @@ class FusedAdam:
 
 
 class GradBucketer:
-    """Bucketed asynchronous all-reduce (SUM) of FlatParams.grad; averaging is folded into
-    FusedAdam's grad_scale (1 / world)."""
+    """Bucketed asynchronous all-reduce of FlatParams.grad (DDP gradient exchange).
 
-    def __init__(self, flat: FlatParams, bucket_bytes: int = 32 << 20, group=None, always: bool = False):
+    Readiness: a parameter reports ONCE per backward, from its post-accumulate hook.  Autograd
+    runs a leaf's AccumulateGrad node once per backward, after every use of the parameter has
+    run its backward — also for the parameters whose HIP backward adds dW / db straight into
+    the flat buffer (``autograd_ops.direct_weight_grads``: the node then sees an undefined
+    gradient and adds nothing, and the hook still fires).  A parameter used several times in a
+    step (the AF MLP runs for the queries and once per neighbour window group) therefore reports
+    after its LAST contribution has been enqueued, never earlier.  A second report in one step
+    is an error.
+
+    Launch order: bucket b is all-reduced once all of its parameters reported AND buckets
+    0..b-1 were launched — the same order (0, 1, 2, ...) on every rank whatever order the
+    rank's graph finished its parameters in (a rank with more neighbour window groups finishes
+    the embedding bucket later; RCCL needs the collectives in one order everywhere).  Buckets
+    with parameters that got no gradient this step are launched by ``finish`` (in order).
+
+    Reduction: SUM.  The reference trains with nn.DataParallel (pretrain_with_val_optimized.py:
+    59-65): one summed focal loss over the whole global batch (:215-233) and ONE gradient, which
+    is clipped and stepped (:235-245).  With the global batch split over ranks, the sum of the
+    ranks' gradients of their summed losses IS that gradient; ``finish`` returns grad scale 1.
+    ``average=True`` gives torch-DDP averaging (scale 1 / world) instead."""
+
+    def __init__(self, flat: FlatParams, bucket_bytes: int = 32 << 20, group=None, always: bool = False,
+                 average: bool = False):
         """``always``: run the collectives even in a world of one (the RCCL smoke test)."""
         self.fp = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.active = self.world > 1 or (always and dist.is_initialized())
+        self.average = average
         self.buckets: List[List[int]] = []        # param indices (flat order)
         self.bounds: List[tuple] = []
         cur, start, size = [], 0, 0
@@ -142,15 +164,17 @@ class GradBucketer:
         for b, idxs in enumerate(self.buckets):
             for i in idxs:
                 self.owner[i] = b
-        self.pending = [0] * len(self.buckets)
+        self.ready: List[set] = [set() for _ in self.buckets]
+        self.next_launch = 0
         self.handles: Dict[int, object] = {}
+        self.staged: Dict[int, torch.Tensor] = {}
         self.enabled = True
+        self.trace: Optional[list] = None          # tests: [(bucket, frozenset(ready params))] per launch
         self._hooks = []
         if self.active:
+            self._stage = dist.get_backend(group) == "gloo" and flat.grad.is_cuda
             for i, p in enumerate(flat.params):
-                hook = self._make_hook(i)
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                p._snv_grad_ready = hook           # gradients accumulated in place by the HIP ops
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
 
     def _close(self, idxs, start, end):
         if idxs:
@@ -162,24 +186,41 @@ class GradBucketer:
             if not self.enabled:
                 return
             b = self.owner[i]
-            self.pending[b] += 1
-            if self.pending[b] == len(self.buckets[b]) and b not in self.handles:
-                self._launch(b)
+            if i in self.ready[b]:
+                raise RuntimeError(f"GradBucketer: parameter {i} reported ready twice in one backward")
+            self.ready[b].add(i)
+            while self.next_launch < len(self.buckets) and \
+                    len(self.ready[self.next_launch]) == len(self.buckets[self.next_launch]):
+                self._launch(self.next_launch)
         return hook
 
     def _launch(self, b):
+        assert b == self.next_launch and b not in self.handles
+        if self.trace is not None:
+            self.trace.append((b, frozenset(self.ready[b])))
         s, e = self.bounds[b]
-        self.handles[b] = dist.all_reduce(self.fp.grad[s:e], group=self.group, async_op=True)
+        if self._stage:
+            # gloo (the CPU-collective tests with the ranks' tensors on a GPU): through the host
+            host = self.fp.grad[s:e].cpu()
+            self.handles[b] = dist.all_reduce(host, group=self.group, async_op=True)
+            self.staged[b] = host
+        else:
+            self.handles[b] = dist.all_reduce(self.fp.grad[s:e], group=self.group, async_op=True)
+        self.next_launch += 1
 
     def finish(self) -> float:
-        """Wait for every bucket (launching those whose parameters got no gradient this step);
-        returns the grad scale that averages over ranks."""
+        """Launch the buckets not launched yet (parameters without a gradient this step), in
+        order, wait for all; returns the grad scale FusedAdam applies (1: SUM, see class doc)."""
         if self.active:
-            for b in range(len(self.buckets)):
-                if b not in self.handles:
-                    self._launch(b)
+            while self.next_launch < len(self.buckets):
+                self._launch(self.next_launch)
             for b in sorted(self.handles):
                 self.handles[b].wait()
+                if b in self.staged:
+                    s, e = self.bounds[b]
+                    self.fp.grad[s:e].copy_(self.staged[b])
         self.handles.clear()
-        self.pending = [0] * len(self.buckets)
-        return 1.0 / self.world
+        self.staged.clear()
+        self.ready = [set() for _ in self.buckets]
+        self.next_launch = 0
+        return 1.0 / self.world if self.average else 1.0

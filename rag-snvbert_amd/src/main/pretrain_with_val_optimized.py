@@ -12,6 +12,21 @@ Per batch (pretrain_with_val_optimized.py:160-245):
 Metrics (losses, TP/FP/FN per class, rare/common split by MAF) accumulate on the device
 and are read once per ``log_freq`` batches / per epoch — no per-batch host sync.
 
+Several ranks (one process per GPU) are one data-parallel trainer over a global batch of
+world x per-rank batch, the reference's nn.DataParallel (:59-65) without the replica
+scatter/gather:
+  * gradients: SUM all-reduce (GradBucketer) — the gradient of the reference's one summed loss
+    over the global batch;
+  * epoch metrics: the loss sums and every TP/FP/FN count are summed over ranks before the CSV
+    row, ``is_best`` and early stopping, so they describe the WHOLE epoch (:362-372, :490-500);
+    the batch count is the number of global steps (equal on every rank);
+  * early stopping: decided on those global counts and broadcast from rank 0, so every rank
+    leaves the epoch loop together;
+  * BatchNorm running statistics (PositionFeatModule, fusion.py:317-332): each rank advances its
+    own from its batches (batch statistics of its chunk, as a DataParallel replica does); at
+    the end of every training epoch rank 0's buffers are broadcast — DataParallel keeps only
+    device 0's updates too — so validation and checkpoints use the same statistics everywhere.
+
 The compute dtype is bf16 with f32 master weights and f32 accumulation (the reference
 uses fp16 autocast + GradScaler; bf16's exponent range needs no loss scaling).
 """
@@ -32,6 +47,28 @@ from .optim_schedule import DeviceConfusion, FocalLoss, ScheduledOptim
 from .optimizer import FlatParams, FusedAdam, GradBucketer
 
 
+MIN_RECON_LOSS = 0.01        # pretrain_with_val_optimized.py:18
+
+
+def recon_mse(a: torch.Tensor, b: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """nn.MSELoss()(a[mask], b[mask]) in f32: the mean of the squared differences over the
+    masked sites' features.  An empty mask gives 0 (the reference's NaN fails both threshold
+    comparisons the same way, and 0 keeps NaN out of the unselected branch's gradient)."""
+    d = (a.float() - b.float()) * mask.unsqueeze(-1)
+    n = (mask.sum() * a.shape[-1]).clamp(min=1)
+    return d.pow(2).sum() / n
+
+
+def _sum_over_ranks(x: torch.Tensor) -> torch.Tensor:
+    """all_reduce(SUM) of a small metric tensor (through the host for gloo)."""
+    if dist.get_backend() == "gloo" and x.is_cuda:
+        h = x.cpu()
+        dist.all_reduce(h)
+        return h.to(x.device)
+    dist.all_reduce(x)
+    return x
+
+
 class BERTTrainerWithValidationOptimized:
     def __init__(self, model, train_dataloader=None, val_dataloader=None, vocab=None, lr: float = 1e-4,
                  betas=(0.9, 0.999), weight_decay: float = 0.01, warmup_steps: int = 10000,
@@ -39,8 +76,7 @@ class BERTTrainerWithValidationOptimized:
                  focal_gamma: float = 2.0, use_recon_loss: bool = False, patience: int = 5,
                  val_metric: str = "f1", min_delta: float = 0.001, rare_threshold: float = 0.05,
                  output_csv: Optional[str] = None, max_grad_norm: float = 1.0, bucket_bytes: int = 32 << 20):
-        if use_recon_loss:
-            raise NotImplementedError("use_recon_loss=True (MSE between embedding stages) is not supported")
+        self.use_recon_loss = bool(use_recon_loss)
         self.device = next(model.parameters()).device
         self.model = model
         self.train_data, self.val_data, self.vocab = train_dataloader, val_dataloader, vocab
@@ -56,13 +92,16 @@ class BERTTrainerWithValidationOptimized:
         self.gt_criterion = FocalLoss(gamma=focal_gamma, reduction="sum")
         self.log_freq = log_freq
         self.patience, self.val_metric, self.min_delta = patience, val_metric, min_delta
-        self.best_val_metric = -np.inf if val_metric in ("f1", "accuracy") else np.inf
+        # early stopping always monitors the validation hap F1 (should_stop_early), higher is better;
+        # the reference starts at +inf for val_metric='loss', after which nothing ever improves
+        self.best_val_metric = -np.inf
         self.epochs_no_improve = 0
         self.best_model_path = None
         self.rare_threshold = rare_threshold
         self.output_csv = output_csv
         self.epoch_metrics = []
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rag_train_dataset = getattr(train_dataloader, "dataset", None) if train_dataloader else None
         self.rag_val_dataset = getattr(val_dataloader, "dataset", None) if val_dataloader else None
         self.embedding_layer = model.bert.embedding
@@ -79,13 +118,25 @@ class BERTTrainerWithValidationOptimized:
     def loss(self, output, data) -> torch.Tensor:
         """(3 FL(h1) + 3 FL(h2) + 4 FL(gt)) / grad_accum_steps over the masked sites
         (pretrain_with_val_optimized.py:215-233) and the three unweighted focal losses the
-        reference's metrics accumulate (:312-313)."""
+        reference's metrics accumulate (:312-313).
+
+        ``use_recon_loss`` (:219-228): the MSE between the raw embeddings (outputs 3, 4) and the
+        encoder outputs (5, 6) at the masked sites, nn.MSELoss (mean over sites x features);
+        when both exceed MIN_RECON_LOSS = 0.01 the total becomes 0.2 FL(h1) + 0.2 FL(h2) +
+        0.3 FL(gt) + 0.15 MSE1 + 0.15 MSE2, else the plain weighting.  The branch is decided on
+        the device (torch.where), without the reference's host sync on the comparison."""
         masks = data["mask"].bool()
         w = 1.0 / self.grad_accum_steps
         l1 = self.hap_criterion(output[0], data["hap_1_label"], masks)
         l2 = self.hap_criterion(output[1], data["hap_2_label"], masks)
         lg = self.gt_criterion(output[2], data["gt_label"], masks)
-        return (3.0 * l1 + 3.0 * l2 + 4.0 * lg) * w, (l1, l2, lg)
+        total = 3.0 * l1 + 3.0 * l2 + 4.0 * lg
+        if self.use_recon_loss:
+            r1 = recon_mse(output[3], output[5], masks)
+            r2 = recon_mse(output[4], output[6], masks)
+            alt = 0.2 * l1 + 0.2 * l2 + 0.3 * lg + 0.15 * r1 + 0.15 * r2
+            total = torch.where((r1 > MIN_RECON_LOSS) & (r2 > MIN_RECON_LOSS), alt, total)
+        return total * w, (l1, l2, lg)
 
     def train_step(self, data: Dict) -> torch.Tensor:
         """One micro-batch: retrieval, forward, loss, backward (+ optimizer step on the last
@@ -159,11 +210,25 @@ class BERTTrainerWithValidationOptimized:
                 print(f"EP_Train:{epoch} it {i} Precision {p_[1].item():.4f} Recall {r_[1].item():.4f} "
                       f"F1 {f_[1].item():.4f} avg_hap_loss {ls[0] + ls[1]:.4f} avg_gt_loss {ls[2]:.4f} "
                       f"{(time.perf_counter() - t0) / (i + 1) * 1e3:.1f} ms/it", flush=True)
+        confs = (("hap", hap), ("gt", gt), ("rare", rare), ("common", common))
+        if self.world > 1:
+            # the whole epoch's metrics (:362-372): sum the loss sums and counts over ranks (f64
+            # holds the integer counts exactly); batches = global steps, equal on every rank
+            packed = torch.cat([loss_sum.double()] + [c.counts.double().reshape(-1) for _, c in confs] +
+                               [torch.tensor([float(n_batches)], device=dev, dtype=torch.float64)])
+            packed = _sum_over_ranks(packed)
+            loss_sum = packed[:3].float()
+            off = 3
+            for _, c in confs:
+                c.counts = packed[off:off + c.counts.numel()].round().long().view_as(c.counts)
+                off += c.counts.numel()
+            n_batches = int(round(packed[off].item() / self.world))
+            if train:
+                self.sync_buffers()
         torch.cuda.synchronize(dev) if dev.type == "cuda" else None
         elapsed = time.perf_counter() - t0
         ls = loss_sum.tolist()
-        counts = {name: conf.counts.cpu() for name, conf in
-                  (("hap", hap), ("gt", gt), ("rare", rare), ("common", common))}
+        counts = {name: conf.counts.cpu() for name, conf in confs}
         row = self.metric_row(epoch, train, counts, ls[0] + ls[1], max(n_batches, 1))
         self.epoch_metrics.append(row)
         res = dict(row)
@@ -178,6 +243,19 @@ class BERTTrainerWithValidationOptimized:
             if self.output_csv:
                 self._save_epoch_metrics(row)
         return res
+
+    def sync_buffers(self) -> None:
+        """Broadcast rank 0's buffers (the BatchNorm running statistics) to every rank — the
+        statistics DataParallel keeps (device 0's replica is the module)."""
+        if self.world <= 1:
+            return
+        for b in self.model.buffers():
+            if dist.get_backend() == "gloo" and b.is_cuda:
+                h = b.detach().cpu()
+                dist.broadcast(h, 0)
+                b.data.copy_(h)
+            else:
+                dist.broadcast(b.data, 0)
 
     # ------------------------------------------------------------ metrics --
     @staticmethod
@@ -271,6 +349,14 @@ class BERTTrainerWithValidationOptimized:
             current = f1[1].item()
         else:
             current = float(val_metrics["overall_f1"])
+        if getattr(self, "world", 1) > 1:
+            # one decision for all ranks (the metrics are already global; rank 0's value is
+            # broadcast so no rank can leave the epoch loop alone on a rounding difference)
+            t = torch.tensor([current], dtype=torch.float64)
+            if dist.get_backend() != "gloo":
+                t = t.to(self.device)
+            dist.broadcast(t, 0)
+            current = float(t.item())
         if current > self.best_val_metric + self.min_delta:
             self.best_val_metric, self.epochs_no_improve = current, 0
             if self.rank == 0:

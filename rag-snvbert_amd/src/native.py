@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -77,6 +77,8 @@ _SIGS = {
     "snvrag_abi_version": ([], C.c_int),
     "snvrag_last_error": ([], C.c_char_p),
     "snvrag_device_info": ([C.c_int, C.c_char_p, C.c_int], C.c_int),
+    "snvrag_set_option": ([C.c_char_p, i64], C.c_int),
+    "snvrag_get_option": ([C.c_char_p, C.POINTER(i64)], C.c_int),
     "snvrag_linear": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), vp], C.c_int),
     "snvrag_linear_ex": ([C.c_int, C.c_int, i64, i64, i64, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue),
                           C.POINTER(RowNormS), vp], C.c_int),

@@ -6,8 +6,9 @@ model and optimiser hyper-parameters, rag_k, resume, output) plus:
                           has no 1000-Genomes files and no h5py/allel to read them;
   --max_steps N           stop an epoch after N batches (smoke runs).
 Multi-GPU: launch one process per GPU with torch.distributed.run; ranks walk the windows
-in lock-step (DistributedWindowSampler) and average gradients with bucketed RCCL
-all-reduces (src/main/optimizer.py).
+in lock-step (DistributedWindowSampler), sum gradients with bucketed RCCL all-reduces
+(src/main/optimizer.py: the reference's DataParallel gradient over the global batch), sum
+the epoch metrics over ranks and stop early together (main/pretrain_with_val_optimized.py).
 """
 
 from __future__ import annotations
@@ -57,6 +58,10 @@ def parse_args(argv=None):
                    help="DDP: each rank holds 1/world of every window's panel and serves every rank's "
                         "queries (SURVEY §8e), or every rank holds the whole panel")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--dropout", type=float, default=0.1, help="model dropout (the reference's BERT default)")
+    p.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend for WORLD_SIZE > 1: nccl (= RCCL, one GPU per rank) or "
+                        "gloo (host-staged collectives: the multi-rank tests with all ranks on one GPU)")
     return p.parse_args(argv)
 
 
@@ -99,16 +104,24 @@ def main(argv=None):
     dev = torch.device(f"cuda:{local}")
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     torch.manual_seed(args.seed + rank)
     train_loader, val_loader, vocab = build_data(args, rank, world)
     from .main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from .model import build_model
-    model = build_model(len(vocab), args.dims, args.layers, args.attn_heads).to(dev)
+    model = build_model(len(vocab), args.dims, args.layers, args.attn_heads, dropout=args.dropout).to(dev)
     if world > 1:   # identical initial weights on every rank
         import torch.distributed as dist
         for t in list(model.parameters()) + list(model.buffers()):
-            dist.broadcast(t.data, 0)
+            if args.dist_backend == "gloo":
+                h = t.data.cpu()
+                dist.broadcast(h, 0)
+                t.data.copy_(h)
+            else:
+                dist.broadcast(t.data, 0)
     trainer = BERTTrainerWithValidationOptimized(
         model, train_loader, val_loader, vocab, lr=args.lr, weight_decay=args.weight_decay,
         warmup_steps=args.warmup_steps, log_freq=args.log_freq, grad_accum_steps=args.grad_accum_steps,

@@ -142,3 +142,96 @@ def test_infer_tied_rows_vs_oracle(case):
         p1, p2, _ = data_np.infer_probs(o["probs_h1"], o["probs_h2"])
         np.testing.assert_allclose(res["batch_h1"][r], p1[0], atol=1e-4, rtol=0, err_msg=f"row {r}")
         np.testing.assert_allclose(res["batch_h2"][r], p2[0], atol=1e-4, rtol=0, err_msg=f"row {r}")
+
+
+# ---------------------------------------------------------------- several ranks (configs[4]) --
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _infer_rank_worker(rank, world, port, mode, arg, q):
+    """One rank of a gloo group, every rank on cuda:0: ``mode`` "fixture" runs ``run`` on a golden
+    case, "cli" runs the ``infer`` entry point (WORLD_SIZE / RANK from the environment)."""
+    import os
+    import sys
+    import traceback
+    import faulthandler
+    faulthandler.dump_traceback_later(200, exit=True)
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.join(here, "..")
+    sys.path[:0] = [root, os.path.join(root, "rag-snvbert_amd"), here]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    try:
+        torch.cuda.set_device(0)
+        if mode == "fixture":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            case, dt = arg
+            _, _, _, res = _fixture_run(case, getattr(torch, dt))
+        else:
+            from src.infer_embedding_rag import infer
+            res = infer(arg + ["--dist_backend", "gloo"])
+        q.put((rank, {k: v for k, v in res.items() if isinstance(v, np.ndarray)} | {"seconds": res["seconds"]}))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run_ranks(world, mode, arg):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_infer_rank_worker, args=(r, world, port, mode, arg, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        got = dict(q.get(timeout=250) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+                p.join(10)
+    for r, v in got.items():
+        assert not isinstance(v, str), f"rank {r}:\n{v}"
+    assert all(p.exitcode == 0 for p in ps)
+    return got
+
+
+_KEYS = ("h1", "h2", "gt", "mask", "idx1", "idx2", "batch_h1", "batch_h2", "batch_mask")
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("case,dtype,world", [("infer_c5_b256", "bfloat16", 3), ("infer_c5_m90", "float32", 2)])
+def test_infer_ranks_match_single_process(case, dtype, world):
+    """configs[4] across ranks: the panel replicated, each rank imputing a contiguous slice of the
+    window-major stream (3 ranks split the 256 sample-windows 85/85/86, across the window
+    boundary), the outputs gathered in stream order — every rank's arrays equal the single-process
+    run on the same fixture bit for bit (reference loop: infer_embedding_rag.py:129-203)."""
+    got = _run_ranks(world, "fixture", (case, dtype))
+    _, _, _, one = _fixture_run(case, getattr(torch, dtype))
+    for r in range(world):
+        for k in _KEYS:
+            np.testing.assert_array_equal(got[r][k], one[k], err_msg=f"rank {r} {k}")
+
+
+@pytest.mark.timeout(400)
+def test_infer_cli_two_ranks_writes_single_process_output(tmp_path):
+    """The entry point under WORLD_SIZE = 2: rank 0 writes imputed.npz / imputed.vcf identical to
+    a single-process run's; rank 1 writes nothing."""
+    args = ["--synthetic", "6", "--synthetic_sites", "2040", "--synthetic_ref", "24", "-d", "64", "-l", "2", "-a", "2",
+            "-b", "4", "--k_retrieve", "3", "--mask_rate", "0.5", "--index_window_len", "1020"]
+    _run_ranks(2, "cli", args + ["-o", str(tmp_path / "ddp")])
+    from src.infer_embedding_rag import infer
+    infer(args + ["-o", str(tmp_path / "one")])
+    a, b = np.load(tmp_path / "ddp" / "imputed.npz"), np.load(tmp_path / "one" / "imputed.npz")
+    for k in b.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert (tmp_path / "ddp" / "imputed.vcf").read_text() == (tmp_path / "one" / "imputed.vcf").read_text()

@@ -154,11 +154,9 @@ def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
         # binary Delta (aligned masks) reduces to the one-limb scan; either way the keys
         # equal the forced two-limb scan's
         assert lut_wide_flag(lut, nq, idx_t.n_sites_pad) == (0 if tie else 1)
-        os.environ["SNVRAG_KNN_NO_REDUCE"] = "1"
-        try:
+        from src import kernels as K_
+        with K_.option("knn_no_reduce", 1):
             keys2 = idx_t.scan_keys(lut, nq, 2, k)
-        finally:
-            del os.environ["SNVRAG_KNN_NO_REDUCE"]
         torch.testing.assert_close(keys2, keys, rtol=0, atol=0)
 
 
@@ -341,9 +339,9 @@ def test_encoder_fused_equals_unfused(dt, monkeypatch):
     ws = torch.empty(K().encoder_ws_bytes(dt, 3, 1030, 384, 12), device=DEV, dtype=torch.uint8)
     a = x0.clone()
     K().encoder_forward(a, P.layers, 12, ws)
-    monkeypatch.setenv("SNVRAG_UNFUSED_LN", "1")
     b = x0.clone()
-    K().encoder_forward(b, P.layers, 12, ws)
+    with K().option("unfused_ln", 1):
+        K().encoder_forward(b, P.layers, 12, ws)
     tol = 2e-4 if dt == torch.float32 else 6e-2
     torch.testing.assert_close(a.float(), b.float(), rtol=tol, atol=tol)
 

@@ -143,3 +143,62 @@ def test_knn_aq_ne_ar_exact_lut():
     assert lut_wide_flag(lut, nq, index.n_sites_pad) == 1           # real-valued Delta: two limbs
     sample = np.arange(nq)
     _check_sampled(index, lut, nq, 2, keys, idx, sample, k)
+
+
+def test_knn_quantised_lut_vs_exact_fp64_l2_reorder_bound():
+    """What the 14-bit LUT quantisation costs against the reference's real-valued distances,
+    with real-valued Delta (A_q != A_r, as for train-mode dropped-out queries or a stale panel
+    snapshot) at N = 200 000: for every query the exact float64 distance
+    dist(q, r) = C_q + sum_s Delta_q[s] a_r[s] (the reference's cdist^2 up to C_q,
+    embedding_rag_dataset.py:390-402) is recomputed over the WHOLE panel and its true top-k
+    taken.  Guarantee (rigorous): the device's picks are the exact top-k of the quantised
+    distances, which differ from the exact ones by at most eps_q = sum_s |Delta_q[s] -
+    dq[s] 2^-e| — so every device pick lies within eps_q of the true k-th distance and every
+    true neighbour closer than the k-th by more than 2 eps_q is picked.  Reported: how many
+    picks differ from the exact fp64 order (near-ties inside the bound); bounded at 1 %."""
+    from src.retrieval import PanelIndex
+    n_ref, n_sites, nq, k, D, L = 200_000, 512, 96, 16, 64, 1030
+    rng = np.random.default_rng(40)
+    af = torch.from_numpy(rng.beta(0.3, 3.0, n_sites).astype(np.float32)).to(DEV)
+    index = PanelIndex.synthetic(n_ref, n_sites, af, torch.zeros(L, device=DEV), seed=19)
+    codes = index.codes[:, :n_sites]
+    codes_h = codes.cpu().numpy()
+    W = rng.standard_normal((12, D)).astype(np.float32)
+    Aq = (0.3 * rng.standard_normal((nq, L, D))).astype(np.float32)
+    Ar = (0.3 * rng.standard_normal((L, D))).astype(np.float32)
+    site_mask = (rng.random(n_sites) < 0.3).astype(np.uint8)
+    q_alle = codes_h[rng.integers(0, n_ref, nq)] ^ (rng.random((nq, n_sites)) < 0.05)
+    tok = np.zeros((nq, L), np.int64)
+    tok[:, 0], tok[:, 1 + n_sites] = 2, 3
+    tok[:, 1:1 + n_sites] = np.where(site_mask[None] == 1, 4, 5 + q_alle)
+    T = lambda a: torch.from_numpy(a).to(DEV)
+    idx, _, keys, lut, exps = index.search(T(tok), T(W), T(site_mask), k, Aq=T(Aq), aq_period=nq, Ar=T(Ar),
+                                           return_keys=True)
+    delta = knn_np.lut_delta(W, tok, Aq - Ar[None], site_mask)                    # float64 [nq, S]
+    dq = decode_lut(lut, nq, index.n_sites_pad, 2)[:, :n_sites].astype(np.float64)
+    scale = np.exp2(-exps.cpu().numpy().astype(np.float64))
+    eps = np.abs(delta - dq * scale[:, None]).sum(1)                              # per-query bound
+    # exact float64 distances over the whole panel (the C_q constant cancels in every order)
+    exact = torch.from_numpy(delta).to(DEV) @ codes.to(torch.float64).t()          # [nq, N]
+    ex_sorted = torch.sort(exact, 1).values
+    kth = ex_sorted[:, k - 1].cpu().numpy()
+    picks = torch.gather(exact, 1, idx).cpu().numpy()
+    assert (picks <= kth[:, None] + eps[:, None] + 1e-9).all()
+    # every neighbour closer than the k-th by more than 2 eps is picked
+    true_sets = torch.topk(exact, k, 1, largest=False).indices.cpu().numpy()
+    ex_np = exact.cpu().numpy()
+    idx_np = idx.cpu().numpy()
+    missed_clear = 0
+    for q in range(nq):
+        must = true_sets[q][ex_np[q, true_sets[q]] < kth[q] - 2 * eps[q]]
+        missed_clear += len(set(must.tolist()) - set(idx_np[q].tolist()))
+    assert missed_clear == 0
+    # how often the quantised order differs from the exact one (near-ties inside the bound)
+    diff = sum(len(set(true_sets[q].tolist()) ^ set(idx_np[q].tolist())) // 2 for q in range(nq))
+    dist_diff = np.abs(np.sort(picks, 1) - ex_sorted[:, :k].cpu().numpy())
+    print(f"quantised vs exact fp64 top-{k}: {diff} of {nq * k} picks differ "
+          f"({100.0 * diff / (nq * k):.3f} %), max |distance gap| {dist_diff.max():.3e}, "
+          f"median bound eps {np.median(eps):.3e}, median k-th distance gap to k+1 "
+          f"{np.median((ex_sorted[:, k] - ex_sorted[:, k - 1]).cpu().numpy()):.3e}")
+    assert diff <= 0.01 * nq * k
+    assert (dist_diff <= 2 * eps[:, None] + 1e-9).all()

@@ -81,3 +81,50 @@ def test_a14_oracle_pinned_to_reference_outputs():
     from src.infer_embedding_rag import geometry
     for a, b in zip(geometry(p1, p2, gt, g["item_mask"][g["order"]], 2, n_var, 1020), (h1, h2, gtg, mask)):
         np.testing.assert_array_equal(a, b)
+
+
+def _split_worker(rank, world, port, n_rows, q):
+    import os
+    import traceback
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.infer_embedding_rag import _gather_rows, rank_rows
+        lo, hi = rank_rows(n_rows, rank, world)
+        rows = torch.arange(lo, hi, dtype=torch.long)
+        sizes = [rank_rows(n_rows, r, world)[1] - rank_rows(n_rows, r, world)[0] for r in range(world)]
+        full = _gather_rows(torch.stack([rows, -rows], 1), sizes)
+        q.put((rank, full.numpy()))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_rows,world", [(256, 3), (2, 3), (7, 2)])
+def test_infer_rank_split_and_ordered_gather_gloo(n_rows, world):
+    """The multi-rank inference plumbing (src/infer_embedding_rag.py run): contiguous slices of the
+    window-major stream cover every row once in order (a rank may get none), and the ragged
+    gather returns the rows in stream order on every rank."""
+    import socket
+    import torch.multiprocessing as mp
+    from src.infer_embedding_rag import rank_rows
+    cover = [i for r in range(world) for i in range(*rank_rows(n_rows, r, world))]
+    assert cover == list(range(n_rows))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_split_worker, args=(r, world, port, n_rows, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(30)
+    want = np.stack([np.arange(n_rows), -np.arange(n_rows)], 1)
+    for r in range(world):
+        assert not isinstance(got[r], str), got[r]
+        np.testing.assert_array_equal(got[r], want)

@@ -71,8 +71,10 @@ def _bucket_worker(rank, world, port, q):
             bk.enabled = micro == 1
             net(x * (micro + 1)).pow(2).sum().backward()
         scale = bk.finish()
+        assert scale == 1.0
         avg = (fp.grad * scale).clone()
-        # expected: mean over ranks of the locally accumulated gradients
+        # expected: SUM over ranks of the locally accumulated gradients (the reference's
+        # DataParallel gradient of one summed loss over the global batch)
         local = []
         for r in range(world):
             n2 = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 8),
@@ -86,7 +88,7 @@ def _bucket_worker(rank, world, port, q):
             local.append([p.grad.clone() for p in n2.parameters()])
         ok = True
         for i, p in enumerate(net.parameters()):
-            exp = sum(l[i] for l in local) / world
+            exp = sum(l[i] for l in local)
             got = fp.view(avg, _index(fp, p))
             ok &= torch.allclose(got, exp, rtol=1e-5, atol=1e-6)
         for p in unused.parameters():
@@ -109,6 +111,103 @@ def test_grad_bucketer_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+class _DirectLinear(torch.autograd.Function):
+    """A Linear whose backward adds dW / db straight into ``w.grad`` / ``b.grad`` and returns None
+    for them — the shape of autograd_ops' HIP Linear under direct_weight_grads."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b = ctx.saved_tensors
+        w.grad.add_(gy.t() @ x)
+        b.grad.add_(gy.sum(0))
+        return gy @ w, None, None
+
+
+def _shared_use_worker(rank, world, port, q):
+    """A graph where the first-registered parameters (the LAST bucket, as the AF MLP is) are used
+    a rank-dependent number of times through the direct-accumulation path plus once through
+    autograd: every bucket must launch only after all of its parameters are final, in the same
+    order on both ranks, and the reduced gradient must equal the sum of the ranks' full
+    gradients."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.main.optimizer import FlatParams, GradBucketer
+        torch.manual_seed(0)
+        shared = torch.nn.Linear(8, 8)                 # registered first -> last bucket
+        body = torch.nn.Linear(8, 8)
+        head = torch.nn.Linear(8, 2)
+        params = list(shared.parameters()) + list(body.parameters()) + list(head.parameters())
+        init = [p.detach().clone() for p in params]
+        fp = FlatParams(params, mirror=False)
+        trace = []
+        final_at = {}               # param index -> launches issued when it became final
+        for i, p in enumerate(fp.params):           # registered before the bucketer's hooks: run first
+            p.register_post_accumulate_grad_hook(lambda _p, i=i: final_at.update({i: len(trace)}) and None)
+        bk = GradBucketer(fp, bucket_bytes=300)
+        assert len(bk.buckets) >= 3
+        bk.trace = trace
+
+        def fwd(x, n_uses, direct):
+            lin = (lambda t, m: _DirectLinear.apply(t, m.weight, m.bias)) if direct else (lambda t, m: m(t))
+            h = sum(lin(x * (u + 1), shared) for u in range(n_uses))   # rank-dependent use count
+            h = torch.tanh(lin(h, body))
+            return shared(torch.tanh(head(h)).repeat(1, 4)).pow(2).sum()   # one autograd use too
+
+        n_uses = 3 if rank == 0 else 1
+        x = torch.randn(5, 8, generator=torch.Generator().manual_seed(rank))
+        fwd(x, n_uses, True).backward()
+        assert bk.finish() == 1.0
+        order = [b for b, _ in bk.trace]
+        ok = order == list(range(len(bk.buckets)))
+        ok &= all(ready == frozenset(bk.buckets[b]) for b, ready in bk.trace)
+        # no bucket launched before one of its members was final
+        ok &= all(final_at[i] <= b for b, _ in bk.trace for i in bk.buckets[b])
+        # expected: sum over ranks of plain-autograd gradients
+        exp = torch.zeros_like(fp.grad)
+        for r in range(world):
+            ps = [torch.nn.Parameter(t.clone()) for t in init]
+            s2, b2, h2 = torch.nn.Linear(8, 8), torch.nn.Linear(8, 8), torch.nn.Linear(8, 2)
+            for m, (w, b) in zip((s2, b2, h2), zip(ps[0::2], ps[1::2])):
+                m.weight, m.bias = w, b
+            xr = torch.randn(5, 8, generator=torch.Generator().manual_seed(r))
+            shared_, body_, head_ = s2, b2, h2
+            h = sum(shared_(xr * (u + 1)) for u in range(3 if r == 0 else 1))
+            h = torch.tanh(body_(h))
+            shared_(torch.tanh(head_(h)).repeat(1, 4)).pow(2).sum().backward()
+            for j, p in enumerate(ps):
+                fp.view(exp, _index_of(fp, params[j])).add_(p.grad)
+        ok &= torch.allclose(fp.grad, exp, rtol=1e-5, atol=1e-6)
+        q.put((rank, (bool(ok), order)))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _index_of(fp, p):
+    return next(i for i, t in enumerate(fp.params) if t is p)
+
+
+def test_grad_bucketer_launches_after_last_use_in_rank_order():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shared_use_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1] and res[0][0] is True, res
 
 
 def test_trainer_metric_rows_and_early_stopping_match_reference(tmp_path):
@@ -174,3 +273,74 @@ def test_pos_feat_batchnorm_matches_module_with_repeated_updates():
     bn.eval()
     ref.eval()
     torch.testing.assert_close(_batchnorm(bn, x.detach()), ref(x.detach()), rtol=1e-12, atol=1e-12)
+
+
+def test_grad_sketch_estimator_on_reference_gradients():
+    """tests/grad_sketch.py (the v18 fixture's gradient storage): on the train_tiny reference
+    gradients a sketch compares exactly to its own gradient, and a perturbation of relative size
+    1e-2 is estimated within a factor 2; the committed train_v18 sketch is consistent (norms
+    positive, 16 projections per parameter)."""
+    import grad_sketch as GS
+    g = load_golden("train_tiny")
+    rng = np.random.default_rng(0)
+    ratios = []
+    for key in (k for k in g if k.startswith("g:")):
+        name, r = key[2:], g[key]
+        if np.linalg.norm(r) == 0:
+            continue
+        sk = GS.sketch(name, r)
+        est, rel_s, cos = GS.compare(name, r, sk)
+        assert est == 0 and rel_s == 0 and abs(cos - 1) < 1e-6
+        e = rng.standard_normal(r.shape).astype(np.float32)
+        e *= 1e-2 * np.linalg.norm(r) / np.linalg.norm(e)
+        ratios.append(GS.compare(name, r + e, sk)[0] / 1e-2)
+    assert 0.6 < np.median(ratios) < 1.4 and min(ratios) > 0.3 and max(ratios) < 2.2, ratios
+    v = load_golden("train_v18")
+    names = GS.names(v)
+    assert len(names) > 250 and all(v[f"gp:{n}"].shape == (GS.NPROJ,) for n in names)
+
+
+def _torch_focal(p, y, m, gamma=2.0):
+    """FocalLoss(gamma, 'sum') on probability rows (optim_schedule.py:49-96), torch f64."""
+    p, y, m = p.reshape(-1, p.shape[-1]).double(), y.reshape(-1), m.reshape(-1)
+    pt = p.gather(1, y[:, None])[:, 0].clamp(min=1e-12)
+    return (-(1 - pt) ** gamma * pt.log())[m].sum()
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-3])
+def test_recon_loss_branch_matches_reference_formula(scale):
+    """use_recon_loss=True (pretrain_with_val_optimized.py:219-228): nn.MSELoss between outputs 3/5
+    and 4/6 at the masked sites; both above MIN_RECON_LOSS -> 0.2 FL1 + 0.2 FL2 + 0.3 FLgt + 0.15
+    MSE1 + 0.15 MSE2, else 3 FL1 + 3 FL2 + 4 FLgt; / grad_accum_steps.  ``scale`` 1e-3 puts the MSEs
+    below the threshold; the gradient flows into the raw and encoded embeddings."""
+    from types import SimpleNamespace
+    from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized as T, MIN_RECON_LOSS
+    g = torch.Generator().manual_seed(1)
+    B, L, D = 2, 30, 8
+    sm = lambda *s: torch.softmax(torch.randn(*s, generator=g), -1)
+    out = [sm(B, L, 2), sm(B, L, 2), sm(B, L, 4)] + \
+          [(scale * torch.randn(B, L, D, generator=g)).requires_grad_(True) for _ in range(4)]
+    data = {"mask": (torch.rand(B, L, generator=g) < 0.4).long(),
+            "hap_1_label": torch.randint(0, 2, (B, L), generator=g), "hap_2_label": torch.randint(0, 2, (B, L), generator=g),
+            "gt_label": torch.randint(0, 4, (B, L), generator=g)}
+    crit = lambda p, y, m: _torch_focal(p, y, m).float()
+    st = SimpleNamespace(grad_accum_steps=2, use_recon_loss=True, hap_criterion=crit, gt_criterion=crit)
+    total, (l1, l2, lg) = T.loss(st, out, data)
+    m = data["mask"].bool()
+    mse = torch.nn.MSELoss()
+    r1, r2 = mse(out[3][m], out[5][m]), mse(out[4][m], out[6][m])
+    if r1 > MIN_RECON_LOSS and r2 > MIN_RECON_LOSS:
+        want = 0.2 * l1 + 0.2 * l2 + 0.3 * lg + 0.15 * r1 + 0.15 * r2
+    else:
+        want = 3 * l1 + 3 * l2 + 4 * lg
+    assert (scale == 1.0) == bool(r1 > MIN_RECON_LOSS)
+    torch.testing.assert_close(total, want / 2, rtol=1e-5, atol=1e-6)
+    total.backward()
+    gr = out[3].grad
+    if scale == 1.0:
+        assert gr is not None and gr.abs().sum() > 0
+    else:
+        assert gr is None or float(gr.abs().sum()) == 0.0
+    st.use_recon_loss = False
+    total2, _ = T.loss(st, out, data)
+    torch.testing.assert_close(total2, (3 * l1 + 3 * l2 + 4 * lg) / 2)

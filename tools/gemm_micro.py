@@ -61,7 +61,7 @@ def main():
                                               M, D, 4 * D, 1),
         "ffn2 N384 K1536 plain": (lambda: K.linear(h, w[(D, 4 * D)], bias[D]), M, D, 4 * D, 0),
     }
-    variants = [("rows", {})] + ([("deep", {"SNVRAG_GEMM_DEEP": "1"})] if os.environ.get("GM_ALL") else [])
+    variants = [("rows", 0)] + ([("tile128", 1)] if os.environ.get("GM_ALL") else [])
     only = os.environ.get("GM_CASE")
     for name, (fn, m, n, k, extra) in cases.items():
         if only and not any(o in name for o in only.split(",")):
@@ -69,17 +69,14 @@ def main():
         flop = 2.0 * m * n * k
         byts = 2.0 * (m * k + n * k + m * n * (1 + extra)) if extra >= 0 else 2.0 * 2 * m * k
         for vn, env in variants:
-            for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
-                os.environ.pop(kk, None)
-            os.environ.update(env)
+            K.set_option("gemm_tile128", env)
             try:
                 ms = timeit(fn)
             except Exception as e:  # the 128x128 tile has no fused-LN path
                 print(f"{name:36s} {vn:8s} n/a ({str(e)[:60]})", flush=True)
                 continue
             print(f"{name:36s} {vn:8s} {ms:8.3f} ms {flop / ms / 1e9:8.1f} TF/s {byts / ms / 1e6:8.1f} GB/s", flush=True)
-        for kk in ("SNVRAG_GEMM_DEEP", "SNVRAG_GEMM_TILE128"):
-            os.environ.pop(kk, None)
+        K.set_option("gemm_tile128", 0)
         if not os.environ.get("GM_TORCH"):
             continue
         if (n, k) not in w:

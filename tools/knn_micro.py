@@ -45,27 +45,22 @@ def main():
     byts = n_ref * index.n_sites_pad
     if os.environ.get("KM_QUICK"):   # full scan vs its loads-only / compute-only halves
         for mode, name in (("0", "full"), ("1", "loads only"), ("2", "compute only")):
-            os.environ["SNVRAG_SCAN_MODE"] = mode
+            K.set_option("scan_mode", int(mode))
             ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 32, 0))
             ms2 = timeit(lambda: index.scan_keys(lut, nq, 2, 32, presample=True))
             print(f"nq={nq} scan v2 k=32 {name}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s; "
                   f"with threshold pre-pass (bench path): {ms2:7.3f} ms", flush=True)
-        os.environ.pop("SNVRAG_SCAN_MODE", None)
+        K.set_option("scan_mode", 0)
         return
-    for ver in ("v2", "v1"):
-        if ver == "v1":
-            os.environ["SNVRAG_SCAN_V1"] = "1"
-        else:
-            os.environ.pop("SNVRAG_SCAN_V1", None)
+    for ver in ("v2",):
         for k in (1, 8, 32):
             ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, k, 0))
             print(f"scan {ver} k={k:2d}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
-    os.environ.pop("SNVRAG_SCAN_V1", None)
     for mode, name in (("1", "loads only"), ("2", "compute only")):
-        os.environ["SNVRAG_SCAN_MODE"] = mode
+        K.set_option("scan_mode", int(mode))
         ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut, nq, 2, 1, 0))
         print(f"scan v2 k=1 {name}: {ms:7.3f} ms  {byts / ms / 1e6:8.1f} GB/s", flush=True)
-    os.environ.pop("SNVRAG_SCAN_MODE", None)
+    K.set_option("scan_mode", 0)
     lut1, _, _ = index.lut(tok, W, smask, 1)
     for k in (1, 32):
         ms = timeit(lambda: K.knn_scan(index.codes, index.n_sites_pad, lut1, nq, 1, k, 0))

@@ -45,12 +45,12 @@ for nq in [int(v) for v in os.environ.get("KP_NQ", "48,96,128").split(",")]:
     th128 = K.knn_threshold(K.topk_merge(K.knn_scan(ix.codes[:m], ix.n_sites_pad, lut, nq, 2, 32, 0,
                                                     n_parts=max(1, min(256, m // 64))), 32), 32)
     for mode, name in (("0", "full"), ("1", "loads only"), ("2", "compute only")):
-        os.environ["SNVRAG_SCAN_MODE"] = mode
+        K.set_option("scan_mode", int(mode))
         for tname, t in (("th1/128", th128), ("th exact", th)):
             ms = timeit(lambda: K.knn_scan(ix.codes, ix.n_sites_pad, lut, nq, 2, 32, 0, th_init=t))
             print(f"nq={nq:3d} scan {name:12s} {tname:8s}: {ms:7.4f} ms {byts / ms / 1e6:8.1f} GB/s "
                   f"({byts / ms / 1e6 / 8000:.3f} of 8 TB/s)", flush=True)
-    os.environ.pop("SNVRAG_SCAN_MODE", None)
+    K.set_option("scan_mode", 0)
     for div in os.environ.get("KP_DIVS", "128,64,32").split(","):
         os.environ["SNVRAG_SAMPLE_DIV"] = div
         ms = timeit(lambda: ix.scan_keys(lut, nq, 2, 32))

@@ -48,10 +48,9 @@ out4 = torch.empty(M, 4 * D, device=dev, dtype=bf)
 
 
 def env(k, v):
-    if v is None:
-        os.environ.pop(k, None)
-    else:
-        os.environ[k] = v
+    """SNVRAG_<NAME> -> the library option <name> (None: its default)."""
+    name = k[len("SNVRAG_"):].lower()
+    K.set_option(name, -1 if v is None and name.endswith("desync") else int(v or 0))
 
 
 for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out), None, fl),
@@ -67,5 +66,5 @@ for dz in ("0", "5000", "10000", "15000"):
     ms = timeit(lambda: K.sgemm(x, sg4, 4 * D, sv4, act=1, out=out4))
     print(f"gelu 4D desync {dz:6s} {ms:.4f} ms  {fl * 4 / 3 / ms / 1e9:.1f} TFLOP/s", flush=True)
 env("SNVRAG_SG_DESYNC", None)
-# the wave-count switch is read once per process: run again with SNVRAG_SG_WAVES4=1 for 4 waves
+# the wave-count switch: env("SNVRAG_SG_WAVES4", "1") for 4 waves
 print("(4-wave variant)" if os.environ.get("SNVRAG_SG_WAVES4") else "(8-wave variant)", flush=True)

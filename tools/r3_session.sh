@@ -22,7 +22,6 @@ for s in ${STEPS:-new ab gpu smoke bench}; do
   case $s in
     new)   step pytest_new 300 $PT tests/test_gpu_kernels.py tests/test_gpu_train.py -k "attention or linear_dw or hip_linear" ;;
     ab)    step attn_dma 120 env REPS=6 python tools/attn_only.py
-           step attn_reg 120 env REPS=6 SNVRAG_ATTN_REGSTAGE=1 python tools/attn_only.py
            step attn_dma_unscaled 120 env REPS=6 PRESCALED=0 python tools/attn_only.py ;;
     gpu)   step pytest_gpu 900 $PT tests -m gpu ${PYTEST_ARGS:-} ;;
     sel)   step pytest_sel 600 $PT tests -m gpu -k "${PYTEST_K}" ;;

@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 GPU session (STEPS selects): new tests, attention / train-attention timing, full GPU
+# suite, smoke, bench, rocprofv3 stats of the bench.  Each GPU step has its own time limit; a
+# crash / abort / timeout (rc not in {0,1}) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OUT=gpurun_out
+TAG=${TAG:-r4}
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n ${TAILN:-12} "$OUT/${TAG}_$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PT="python -u -m pytest -v -rf --timeout 300 --timeout-method thread -s"
+for s in ${STEPS:-new attn bench}; do
+  case $s in
+    new)   step pytest_new 900 $PT ${NEW_TESTS:-tests/test_gpu_ddp.py tests/test_gpu_infer.py tests/test_gpu_rccl.py} ;;
+    attnt) step pytest_attn 400 $PT tests/test_gpu_kernels.py tests/test_gpu_train.py -k "attention or attn" ;;
+    attn)  step attn_only 120 env REPS=8 python tools/attn_only.py
+           step train_attn 200 python tools/train_attn_micro.py ;;
+    gpu)   step pytest_gpu 1100 $PT tests -m gpu ${PYTEST_ARGS:-} ;;
+    sel)   step pytest_sel 800 $PT tests -m gpu -k "${PYTEST_K}" ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
+    prof)  step prof 700 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench \
+             -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0
+           rm -f $OUT/prof_$TAG/*/*.db $OUT/prof_$TAG/*.db
+           python3 tools/prof_top.py $OUT/prof_$TAG 30 > $OUT/${TAG}_prof_top.txt 2>&1; head -30 $OUT/${TAG}_prof_top.txt ;;
+  esac
+done

@@ -73,11 +73,11 @@ out = torch.empty_like(c["x"])
 fl9, fl8 = 18.0 * M * D * D, 16.0 * M * D * D
 def tail_var(v, desync=-1):
     def fn():
-        os.environ["SNVRAG_TAIL_VARIANT"] = str(v)
+        K.set_option("tail_variant", int(v))
         if desync < 0:
-            os.environ.pop("SNVRAG_TAIL_DESYNC", None)         # the library default
+            K.set_option("tail_desync", -1)         # the library default
         else:
-            os.environ["SNVRAG_TAIL_DESYNC"] = str(desync)
+            K.set_option("tail_desync", int(desync))
         K.tail_forward(c["att"], xs, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
     return fn
 
@@ -95,7 +95,7 @@ for name, fn, fl in (
         ("tail.hip PRE desync 12k", tail_var(0, 12000), fl9),
         ("tail.hip PRE desync 25k", tail_var(0, 25000), fl9),
         ("tail.hip PRE desync 40k", tail_var(0, 40000), fl9),
-        ("tail.hip FFN only", lambda: (os.environ.__setitem__("SNVRAG_TAIL_VARIANT", "0"),
+        ("tail.hip FFN only", lambda: (K.set_option("tail_variant", 0),
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
     ms = timeit(fn)
     print(f"{name:22s} {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
@@ -112,7 +112,7 @@ for _ in range(20):                                  # warm the clock up on the 
 tail_var(4, int(os.environ.get("TM_DESYNC", "-1")))()
 torch.cuda.synchronize()
 N.lib().snvrag_tail_stamps(None)
-os.environ["SNVRAG_TAIL_VARIANT"] = "0"
+K.set_option("tail_variant", 0)
 s = st.view(nwg * 4, 10).cpu().numpy().astype(np.float64)
 names = ["prologue (act loads + 8 slabs)", "out-projection (864 MFMA)", "LN1", "FFN (1728 MFMA)",
          "FFN end -> ring free (vmcnt 0 + barrier + vec tables)", "LN2 + stores (+ vmcnt 0)"]
