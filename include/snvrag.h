@@ -35,8 +35,9 @@ const char* snvrag_last_error(void);
 int snvrag_device_info(int device, char* name, int name_len);
 /* Library options — tuning switches of the micro-benchmarks and test hooks, no reference
  * counterpart: knn_no_reduce, scan_mode, scan_nt, unfused_ln, encoder_chunk, gemm_tile128,
- * gemm_nw, tail_variant, tail_desync, sg_desync, sg_waves4, ln_bwd_nopf.  Each starts from the
- * environment variable SNVRAG_<NAME> (read once, at first use); launches read the table. */
+ * gemm_nw, tail_variant, tail_desync, sg_desync, sg_waves4, ln_bwd_nopf, attn_variant.  Each
+ * starts from the environment variable SNVRAG_<NAME> (read once, at first use); launches read
+ * the table. */
 int snvrag_set_option(const char* name, int64_t value);
 int snvrag_get_option(const char* name, int64_t* value);
 

@@ -244,18 +244,32 @@ struct Train {
   int q0;             // the wave's first query
 };
 
-template <int NKT, bool MASK, bool FIRST, bool TRAIN = false>
+struct NoMid {
+  __device__ void operator()() const {}
+};
+
+// One 64-key tile for a wave's 32 queries.  VAR (inference A/B, snvrag option attn_variant):
+//   0  as described above;
+//   1  the PV + row-sum MFMA block at s_setprio 2 (a wave with MFMAs to issue wins the SIMD's
+//      issue arbitration over the co-resident waves' exp streams);
+//   2  like 1, and the S MFMAs at the head of the tile as well;
+//   3  K fragments passed in ``kin`` (read one tile ahead by the caller) and ``mid`` run between
+//      the exps and the PV block (the caller's ring barrier + next-tile K prefetch).
+template <int NKT, bool MASK, bool FIRST, bool TRAIN = false, int VAR = 0, typename Mid = NoMid>
 __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
-                                     State& st, int li, int lg, const Train& tr = Train{}) {
+                                     State& st, int li, int lg, const Train& tr = Train{},
+                                     const bf16x8* kin = nullptr, Mid mid = Mid{}) {
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4 s[NKT][2];
+  if constexpr (VAR == 2) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
-    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kt + k_off(16 * kt + li, lg));
+    const bf16x8 kf = VAR == 3 ? kin[kt] : *reinterpret_cast<const bf16x8*>(Kt + k_off(16 * kt + li, lg));
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
       s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt], FIRST ? zero : st.negm[qt], 0, 0, 0);
   }
+  if constexpr (VAR == 2) __builtin_amdgcn_s_setprio(0);
   if constexpr (MASK) {
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
@@ -317,8 +331,10 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
       }
     }
   }
+  mid();
   const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
   const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
+  if constexpr (VAR == 1 || VAR == 2) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
 #pragma unroll
@@ -333,6 +349,7 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) st.ls[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[cb][qt], st.ls[qt], 0, 0, 0);
   }
+  if constexpr (VAR == 1 || VAR == 2) __builtin_amdgcn_s_setprio(0);
 }
 
 // TRAIN with dropout: the kept probabilities entered PV unscaled; O *= 1 / (1 - p) once
@@ -442,7 +459,7 @@ constexpr int NS = 4;                           // ring slots
 constexpr int SLOT = 2 * TB;                    // K tile + V tile
 }  // namespace a32
 
-template <bool PRESCALED, bool TRAIN = false>
+template <bool PRESCALED, bool TRAIN = false, int VAR = 0>
 __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
                                                   int* __restrict__ n_fallback, long total_rows,
@@ -527,15 +544,61 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
     // (a wave past L — the last query block's — computes on zero queries and stores nothing:
     // no per-tile branch)
     const char* Kt = smem + S * SLOT;
-    if (t == 0) tile<4, false, true, TRAIN>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
-    else tile<4, false, false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+    if (t == 0) tile<4, false, true, TRAIN, VAR>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+    else tile<4, false, false, TRAIN, VAR>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
   };
   int t = 0;
+  bool ring3 = false;
+  if constexpr (VAR == 3) ring3 = nfull >= NS + 1;
+  if (ring3) {
+    // K of tile t + 1 read during tile t: the ring barrier moves between the exps and the PV
+    // block of tile t (every wave then is done with V of t - 1 and has landed tile t + 1), the
+    // look-ahead drops to 2 tiles (tile t + 3 issued into the slot of t - 1 at that barrier)
+    bf16x8 kcur[4];
+    wait(1);
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) kcur[kt] = *reinterpret_cast<const bf16x8*>(smem + k_off(16 * kt + li, lg));
+    auto step3 = [&](auto s_tag, int t) {
+      constexpr int S = decltype(s_tag)::value;
+      bf16x8 knext[4];
+      auto mid = [&]() {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");      // this wave's pieces of tile t + 1
+        __builtin_amdgcn_s_barrier();
+        issue(t + NS - 1, (S + NS - 1) % NS);
+        const char* Kn = smem + ((S + 1) % NS) * SLOT;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) knext[kt] = *reinterpret_cast<const bf16x8*>(Kn + k_off(16 * kt + li, lg));
+      };
+      const char* Kt = smem + S * SLOT;
+      if (t == 0) tile<4, false, true, TRAIN, 3>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr, kcur, mid);
+      else tile<4, false, false, TRAIN, 3>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr, kcur, mid);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) kcur[kt] = knext[kt];
+    };
+    // full tiles whose successor is a full tile that exists and whose t + NS - 1 issue is in range
+    for (; t + NS <= nfull - 1; t += NS) {
+      step3(std::integral_constant<int, 0>{}, t);
+      step3(std::integral_constant<int, 1>{}, t + 1);
+      step3(std::integral_constant<int, 2>{}, t + 2);
+      step3(std::integral_constant<int, 3>{}, t + 3);
+    }
+    // hand back to the plain loop: tile t's K is in LDS and visible; its barrier already passed,
+    // so the plain step's barrier and issue must not repeat — run tile t here, then continue
+    {
+      const char* Kt = smem + (t % NS) * SLOT;
+      __builtin_amdgcn_s_barrier();                  // every wave done with tile t - 1 (its V)
+      if (t + NS - 1 < ntile) issue(t + NS - 1, (t + NS - 1) % NS);
+      tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);   // t >= NS: not the first
+      ++t;
+    }
+  } else {
   for (; t + NS <= nfull; t += NS) {
     step(std::integral_constant<int, 0>{}, t);
     step(std::integral_constant<int, 1>{}, t + 1);
     step(std::integral_constant<int, 2>{}, t + 2);
     step(std::integral_constant<int, 3>{}, t + 3);
+  }
   }
   for (; t < ntile; ++t) {                         // the last < NS full tiles and the ragged tail
     wait(min(NS - 2, ntile - 1 - t));
@@ -647,8 +710,11 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const float sl2 = scale * 1.4426950408889634f;
     const bool pre = fabsf(sl2 - 1.0f) < 1e-6f;      // Q already carries log2(e)/sqrt(dh)
     int* cnt = attn_fallback_counter();
+    const int var = (int)options().attn_variant;
+    auto kp = var == 1 ? attn32_dma<true, false, 1> : var == 2 ? attn32_dma<true, false, 2>
+              : var == 3 ? attn32_dma<true, false, 3> : attn32_dma<true, false, 0>;
     if (pre)
-      hipLaunchKernelGGL(attn32_dma<true>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
+      hipLaunchKernelGGL(kp, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
                          (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
     else
       hipLaunchKernelGGL(attn32_dma<false>, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,

@@ -344,3 +344,110 @@ def test_recon_loss_branch_matches_reference_formula(scale):
     st.use_recon_loss = False
     total2, _ = T.loss(st, out, data)
     torch.testing.assert_close(total2, (3 * l1 + 3 * l2 + 4 * lg) / 2)
+
+
+class _StubModel(torch.nn.Module):
+    """Outputs a fixed function of the batch (probabilities from the tokens), so two ranks and one
+    process see the same per-sample outputs."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.zeros(1))
+        self.bert = torch.nn.Module()
+        self.bert.embedding = torch.nn.Module()          # the trainer's retrieval handle (unused here)
+
+    def forward(self, x):
+        h = x["hap_1"].double()
+        p1 = torch.sigmoid(torch.sin(h * 1.7 + x["af"].double()))
+        p2 = torch.sigmoid(torch.cos(h * 0.9))
+        pg = torch.softmax(torch.stack([h.sin(), h.cos(), (2 * h).sin(), x["af"].double()], -1), -1)
+        two = lambda p: torch.stack([1 - p, p], -1).float()
+        return [two(p1), two(p2), pg.float()]
+
+
+def _stub_batches(items):
+    g = torch.Generator().manual_seed(7)
+    L = 40
+    tok = torch.randint(4, 7, (16, L), generator=g)
+    af = torch.rand(16, L, generator=g)
+    mask = (torch.rand(16, L, generator=g) < 0.5).long()
+    lab = torch.randint(0, 2, (16, L), generator=g)
+    gl = torch.randint(0, 4, (16, L), generator=g)
+    out = []
+    for b in items:
+        i = torch.tensor(b)
+        out.append({"hap_1": tok[i], "af": af[i], "mask": mask[i], "hap_1_label": lab[i], "hap_2_label": 1 - lab[i],
+                    "gt_label": gl[i]})
+    return out
+
+
+def _patch_trainer_cpu(T, tr):
+    """CPU stand-ins for the two HIP kernels the epoch loop calls (focal loss, confusion counts)."""
+    from src.main import optim_schedule as OS
+    crit = lambda p, y, m: _torch_focal(p, y, m).float()
+    tr.hap_criterion = tr.gt_criterion = crit
+
+    def upd(self, probs, labels, mask, mask2=None):
+        m = mask.bool() if mask2 is None else (mask.bool() & mask2.bool())
+        c = train_np.confusion(probs.detach().numpy(), labels.numpy(), m.numpy(), self.C)
+        self.counts += torch.from_numpy(c)
+    OS.DeviceConfusion.update = upd
+
+
+def _metric_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized as T
+        m = _StubModel()
+        tr = T(m, None, _stub_batches([[0, 1, 2], [3, 4]] if rank == 0 else [[5, 6, 7], [8, 9]]), None,
+               log_freq=0, patience=1)
+        _patch_trainer_cpu(T, tr)
+        res = tr.validate(0)
+        stop1 = tr.should_stop_early(res, 0)
+        stop2 = tr.should_stop_early(res, 1)
+        q.put((rank, ({k: v for k, v in res.items() if not torch.is_tensor(v) and k != "sec"},
+                      {k: v.tolist() for k, v in res.items() if torch.is_tensor(v)}, stop1, stop2)))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_epoch_metrics_summed_over_ranks_gloo_world2():
+    """The trainer's epoch metrics under two gloo ranks (pretrain_with_val_optimized.py:362-372,
+    :490-522): losses and TP/FP/FN summed over ranks, the batch count = global steps, the CSV row
+    and the early-stopping decision identical on both ranks and equal to one process that ran the
+    union of the samples with the global batch (rank batches 3 + 3 and 2 + 2)."""
+    from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized as T
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_metric_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert not isinstance(got[0], str), got[0]
+    assert not isinstance(got[1], str), got[1]
+    assert got[0] == got[1]
+    from src.main import optim_schedule as OS
+    orig = OS.DeviceConfusion.update
+    try:
+        tr = T(_StubModel(), None, _stub_batches([[0, 1, 2, 5, 6, 7], [3, 4, 8, 9]]), None, log_freq=0, patience=1)
+        _patch_trainer_cpu(T, tr)
+        res = tr.validate(0)
+    finally:
+        OS.DeviceConfusion.update = orig
+    row, counts, s1, s2 = got[0]
+    assert row["batches"] == res["batches"] == 2
+    for k, v in row.items():
+        if isinstance(v, float):
+            np.testing.assert_allclose(v, res[k], rtol=1e-5, err_msg=k)
+        else:
+            assert v == res[k], k
+    for k, v in counts.items():
+        assert v == res[k].tolist(), k
+    assert (s1, s2) == (False, True)

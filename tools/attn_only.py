@@ -17,15 +17,32 @@ pre = os.environ.get("PRESCALED", "1") == "1"
 scale = 1.0 / math.log2(math.e) if pre else 1.0 / math.sqrt(dh)
 if pre:
     qkv[:, :H * dh] = (qkv[:, :H * dh].float() * (math.log2(math.e) / math.sqrt(dh))).to(torch.bfloat16)
-out = None
-a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for i in range(int(os.environ.get("REPS", 3))):
-    if i == 1:
-        a.record()
-    out = K.attention(qkv, nseq, L, H, dh, scale=scale)
-b.record()
-torch.cuda.synchronize()
-n = int(os.environ.get("REPS", 3)) - 1
-if n > 0:
-    ms = a.elapsed_time(b) / n
-    print(f"attention {ms:.4f} ms  {4.0 * L * L * dh * H * nseq / ms / 1e9:.1f} TFLOP/s", flush=True)
+base = None
+# ATTN_VARIANTS="0,1,2,3": the inference kernel's A/B variants (snvrag option attn_variant), each
+# timed and checked bit for bit against variant 0; rounds alternate to spread DVFS drift
+variants = [int(v) for v in os.environ.get("ATTN_VARIANTS", "0").split(",")]
+reps = int(os.environ.get("REPS", 3))
+res = {v: [] for v in variants}
+for rnd in range(int(os.environ.get("ROUNDS", 1))):
+    for v in variants:
+        K.set_option("attn_variant", v)
+        out = None
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(reps):
+            if i == 1:
+                a.record()
+            out = K.attention(qkv, nseq, L, H, dh, scale=scale)
+        b.record()
+        torch.cuda.synchronize()
+        if base is None:
+            base = out.clone()
+        same = torch.equal(out, base)
+        if reps > 1:
+            ms = a.elapsed_time(b) / (reps - 1)
+            res[v].append(ms)
+            print(f"attention variant {v}: {ms:.4f} ms  {4.0 * L * L * dh * H * nseq / ms / 1e9:.1f} TFLOP/s  "
+                  f"bit-identical to variant {variants[0]}: {same}", flush=True)
+K.set_option("attn_variant", 0)
+for v, t in res.items():
+    if t:
+        print(f"variant {v}: best {min(t):.4f} ms  median {sorted(t)[len(t) // 2]:.4f} ms", flush=True)

@@ -23,7 +23,7 @@ for s in ${STEPS:-new attn bench}; do
   case $s in
     new)   step pytest_new 900 $PT ${NEW_TESTS:-tests/test_gpu_ddp.py tests/test_gpu_infer.py tests/test_gpu_rccl.py} ;;
     attnt) step pytest_attn 400 $PT tests/test_gpu_kernels.py tests/test_gpu_train.py -k "attention or attn" ;;
-    attn)  step attn_only 120 env REPS=8 python tools/attn_only.py
+    attn)  step attn_only 240 env REPS=8 ROUNDS=3 ATTN_VARIANTS=${ATTN_VARIANTS:-0} python tools/attn_only.py
            step train_attn 200 python tools/train_attn_micro.py ;;
     gpu)   step pytest_gpu 1100 $PT tests -m gpu ${PYTEST_ARGS:-} ;;
     sel)   step pytest_sel 800 $PT tests -m gpu -k "${PYTEST_K}" ;;
