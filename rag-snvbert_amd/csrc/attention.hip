@@ -541,11 +541,13 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
     wait(NS - 2);
     __builtin_amdgcn_s_barrier();                  // tile t visible; every wave is done with t - 1
     issue(t + NS - 1, (S + NS - 1) % NS);
-    // (a wave past L — the last query block's — computes on zero queries and stores nothing:
-    // no per-tile branch)
-    const char* Kt = smem + S * SLOT;
-    if (t == 0) tile<4, false, true, TRAIN, VAR>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
-    else tile<4, false, false, TRAIN, VAR>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+    // a wave past L (3 of the 4 waves of the last query block at L = 1030: 8 % of all waves) only
+    // moves its DMA pieces and meets the barriers — a wave-uniform branch, not 20 idle MFMAs
+    if (active) {
+      const char* Kt = smem + S * SLOT;
+      if (t == 0) tile<4, false, true, TRAIN, VAR>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+      else tile<4, false, false, TRAIN, VAR>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+    }
   };
   int t = 0;
   bool ring3 = false;
@@ -571,7 +573,8 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
         for (int kt = 0; kt < 4; ++kt) knext[kt] = *reinterpret_cast<const bf16x8*>(Kn + k_off(16 * kt + li, lg));
       };
       const char* Kt = smem + S * SLOT;
-      if (t == 0) tile<4, false, true, TRAIN, 3>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr, kcur, mid);
+      if (!active) mid();                           // barrier + issue only
+      else if (t == 0) tile<4, false, true, TRAIN, 3>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr, kcur, mid);
       else tile<4, false, false, TRAIN, 3>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr, kcur, mid);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) kcur[kt] = knext[kt];
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
       const char* Kt = smem + (t % NS) * SLOT;
       __builtin_amdgcn_s_barrier();                  // every wave done with tile t - 1 (its V)
       if (t + NS - 1 < ntile) issue(t + NS - 1, (t + NS - 1) % NS);
-      tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);   // t >= NS: not the first
+      if (active) tile_any<false, TRAIN>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);   // t >= NS: not the first
       ++t;
     }
   } else {
