@@ -292,7 +292,7 @@ def main():
     # roofline object = the MFMA kernel class with the most time per step
     mf = [("rows_gemm_kernel (encoder QKV/out-proj + fusion/head GEMMs)", gemm, "2*M*N*K averaged over launches"),
           ("tail_kernel (block tail on 32x32 MFMAs: out-projection + LN1 + FFN + LN2, 12 launches)", ffn, "2*M*D*9D = 18*M*D^2 per launch"),
-          ("attn32_bf16 (attention)", attn, "4*L^2*dh*H*nseq per launch")]
+          ("attn32_dma (attention)", attn, "4*L^2*dh*H*nseq per launch")]
     name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
     roofline = dict(bound="mfma", kernel=name,
                     achieved=round(dom["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",

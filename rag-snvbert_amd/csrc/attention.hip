@@ -459,8 +459,11 @@ constexpr int NS = 4;                           // ring slots
 constexpr int SLOT = 2 * TB;                    // K tile + V tile
 }  // namespace a32
 
+// VAR 4: the VAR 0 tile body in 8-wave workgroups (2 waves per SIMD, 256 queries): every K/V
+// tile's 8 KiB of LDS-DMA is shared by twice the queries, one DMA instruction per wave per tile
+// (waves 0-3 move K, 4-7 move V) instead of two.
 template <bool PRESCALED, bool TRAIN = false, int VAR = 0>
-__global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
+__global__ __launch_bounds__(VAR == 4 ? 512 : 256, VAR == 4 ? 4 : 1) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
                                                   int* __restrict__ n_fallback, long total_rows,
                                                   float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{}) {
@@ -478,7 +481,9 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
   const bf16* Qp = qkv + base + h * 32;
   const bf16* Kp = qkv + base + D + h * 32;
   const bf16* Vp = qkv + base + 2 * D + h * 32;
-  const int q0 = qb * QPB + wave * QPW;
+  constexpr int NW = VAR == 4 ? 8 : WAVES;          // waves per workgroup
+  constexpr int TV = VAR == 4 ? 0 : VAR;            // tile-body variant
+  const int q0 = qb * (QPW * NW) + wave * QPW;
   const bool active = q0 < L;                      // wave-uniform
 
   bf16x8 qf[2];
@@ -502,21 +507,31 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
   // source chunk that k_off / v_off put there
   const long rem = (total_rows - (long)seq * L) * ld * 2;
   const i32x4 rs = dma_rsrc(qkv + base, rem);
-  const int kk = 16 * wave + (lane >> 2), c4 = lane & 3;
+  const int pw = NW == 8 ? wave & 3 : wave;         // the 16-key piece this wave moves
+  const int kk = 16 * pw + (lane >> 2), c4 = lane & 3;
   const int kc = c4 ^ ((-(kk >> 2)) & 3);
   const int vc = 2 * ((c4 >> 1) ^ ((kk >> 2) & 1)) + (c4 & 1);
   const int vk = (int)(kk * ld * 2) + (D + h * 32) * 2 + kc * 16;
   const int vv = (int)(kk * ld * 2) + (2 * D + h * 32) * 2 + vc * 16;
   const int tile_bytes = (int)(KT * ld * 2);
-  const uint32_t lds_w = lds_addr(smem) + wave * 1024;
+  const uint32_t lds_w = lds_addr(smem) + pw * 1024;
+  // 8 waves: waves 4-7 move the V pieces (one offset and one LDS base per wave, chosen once)
+  const bool vwave = NW == 8 && wave >= 4;
+  const int v_mine = vwave ? vv : vk;
+  const uint32_t lds_mine = lds_w + (vwave ? TB : 0);
   auto issue = [&](int t, int slot) {
-    dma_x4(rs, lds_w + slot * SLOT, vk, t * tile_bytes);
-    dma_x4(rs, lds_w + slot * SLOT + TB, vv, t * tile_bytes);
+    if constexpr (NW == 8) {
+      dma_x4(rs, lds_mine + slot * SLOT, v_mine, t * tile_bytes);
+    } else {
+      dma_x4(rs, lds_w + slot * SLOT, vk, t * tile_bytes);
+      dma_x4(rs, lds_w + slot * SLOT + TB, vv, t * tile_bytes);
+    }
   };
   // retire this wave's pieces of tile t: y = younger tiles still in flight (<= NS - 2)
+  constexpr int PPT = NW == 8 ? 1 : 2;              // DMA instructions per wave per tile
   auto wait = [&](int y) {
-    if (y >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (y == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (y >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPT) : "memory");
+    else if (y == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPT) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
@@ -545,8 +560,8 @@ __global__ __launch_bounds__(256) void attn32_dma(int L, int H, const bf16* __re
     // moves its DMA pieces and meets the barriers — a wave-uniform branch, not 20 idle MFMAs
     if (active) {
       const char* Kt = smem + S * SLOT;
-      if (t == 0) tile<4, false, true, TRAIN, VAR>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
-      else tile<4, false, false, TRAIN, VAR>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
+      if (t == 0) tile<4, false, true, TRAIN, TV>(Kt, Kt + TB, 0, L, qf, st, li, lg, tr);
+      else tile<4, false, false, TRAIN, TV>(Kt, Kt + TB, t * KT, L, qf, st, li, lg, tr);
     }
   };
   int t = 0;
@@ -715,8 +730,13 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     int* cnt = attn_fallback_counter();
     const int var = (int)options().attn_variant;
     auto kp = var == 1 ? attn32_dma<true, false, 1> : var == 2 ? attn32_dma<true, false, 2>
-              : var == 3 ? attn32_dma<true, false, 3> : attn32_dma<true, false, 0>;
-    if (pre)
+              : var == 3 ? attn32_dma<true, false, 3> : var == 4 ? attn32_dma<true, false, 4>
+              : attn32_dma<true, false, 0>;
+    const int nqb8 = cdiv(L, 2 * a32::QPB);
+    if (pre && var == 4)
+      hipLaunchKernelGGL(kp, dim3((unsigned)(nqb8 * H * nseq)), dim3(512), 0, s, (int)L, H, (const bf16*)qkv, ld,
+                         (bf16*)out, ldo, 1.0f, nqb8, cnt, (long)nseq * L, nullptr, AttnDrop{});
+    else if (pre)
       hipLaunchKernelGGL(kp, dim3((unsigned)nb), dim3(256), 0, s, (int)L, H, (const bf16*)qkv, ld,
                          (bf16*)out, ldo, 1.0f, nqb, cnt, (long)nseq * L, nullptr, AttnDrop{});
     else

@@ -58,6 +58,7 @@ def parse_args(argv=None):
     p.add_argument("--mask_rate", type=float, default=0.3,
                    help="synthetic: fraction of panel sites absent from the target (C5 sweep 0.1..0.9)")
     p.add_argument("--no_vcf", action="store_true")
+    p.add_argument("--seed", type=int, default=0, help="weight init without --check_point (synthetic runs)")
     p.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
                    help="WORLD_SIZE > 1 (torch.distributed.run, one process per GPU): nccl (= RCCL) or gloo "
                         "(host-staged: the multi-rank tests with every rank on one GPU)")
@@ -236,6 +237,7 @@ def infer(argv=None):
     from .engine import engine_for
     from .model import build_model
     ds, vocab = build_dataset(args)
+    torch.manual_seed(args.seed)          # every rank (and every run) builds the same random-init weights
     model = build_model(len(vocab), args.dims, args.layers, args.attn_heads)
     if args.check_point:
         ck = torch.load(args.check_point, map_location="cpu", weights_only=True)

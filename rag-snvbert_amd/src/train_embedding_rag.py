@@ -109,6 +109,11 @@ def main(argv=None):
         else:
             dist.init_process_group("gloo")
     torch.manual_seed(args.seed + rank)
+    # the datasets' construction-time window masks draw from numpy's global RNG (unseeded in the
+    # reference, embedding_rag_dataset.py:160-170): seeded here so a run is reproducible (ranks
+    # take rank 0's masks anyway, set_panel_shard)
+    import numpy as np
+    np.random.seed(args.seed)
     train_loader, val_loader, vocab = build_data(args, rank, world)
     from .main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from .model import build_model

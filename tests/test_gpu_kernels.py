@@ -525,3 +525,28 @@ def test_proj_kernel_vs_fp64(D, M, NC):
     ref = x.double() @ w.double().T + b.double()
     torch.testing.assert_close(out[:M].double(), ref, rtol=2e-2, atol=2e-2)
     assert (out[M] == 7.0).all()                       # nothing written past the last row
+
+
+@pytest.mark.parametrize("L", [1030, 520, 77])
+def test_attention_dh32_variants_bit_identical(L):
+    """The inference attention kernel's A/B variants (option attn_variant: 1/2 s_setprio around the
+    MFMA blocks, 3 the next tile's K read ahead, 4 eight-wave workgroups sharing each K/V tile) run
+    the same arithmetic in the same order: bit-identical to variant 0 (prescaled Q, the engine's
+    form), and variant 0 matches the fp32 softmax."""
+    import math
+    torch.manual_seed(L + 5)
+    nseq, H, dh = 3, 12, 32
+    qkv = (torch.randn(nseq * L, 3 * H * dh, device=DEV) * 0.8)
+    qkv[:, :H * dh] *= math.log2(math.e) / math.sqrt(dh)
+    qkv = qkv.to(torch.bfloat16)
+    scale = 1.0 / math.log2(math.e)                     # Q carries log2(e)/sqrt(dh)
+    outs = {}
+    for v in (0, 1, 2, 3, 4):
+        with K().option("attn_variant", v):
+            outs[v] = K().attention(qkv, nseq, L, H, dh, scale=scale)
+    q = qkv.float().clone()
+    q[:, :H * dh] *= math.sqrt(dh) / math.log2(math.e)
+    ref = _attn_ref(q, nseq, L, H, dh)
+    torch.testing.assert_close(outs[0].float(), ref, rtol=2e-2, atol=2e-2)
+    for v in (1, 2, 3, 4):
+        assert torch.equal(outs[v], outs[0]), v
