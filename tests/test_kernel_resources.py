@@ -21,8 +21,8 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 # (demangled-name prefix, what runs it)
 HOT = [
     ("snvrag::tail_kernel<384, true, 4, 0, true, 0>", "block tail (bench roofline kernel)"),
-    ("snvrag::attn32_dma<true, false>", "inference attention"),
-    ("snvrag::attn32_dma<false, true>", "training attention forward"),
+    ("snvrag::attn32_dma<true, false, 0>", "inference attention"),
+    ("snvrag::attn32_dma<false, true, 0>", "training attention forward"),
     ("snvrag::attn_bwd_dkv32", "training attention backward dK/dV"),
     ("snvrag::attn_bwd_dq32", "training attention backward dQ"),
     ("snvrag::sg_kernel<384, 0, 0, false, 8, false>", "QKV stream GEMM"),
