@@ -58,7 +58,8 @@ def parse_args(argv=None):
                    help="DDP: each rank holds 1/world of every window's panel and serves every rank's "
                         "queries (SURVEY §8e), or every rank holds the whole panel")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--dropout", type=float, default=0.1, help="model dropout (the reference's BERT default)")
+    p.add_argument("--dropout", type=float, default=0.1,
+                   help="model dropout (the reference's BERT default 0.1); another value sets every dropout layer")
     p.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for WORLD_SIZE > 1: nccl (= RCCL, one GPU per rank) or "
                         "gloo (host-staged collectives: the multi-rank tests with all ranks on one GPU)")
@@ -118,6 +119,12 @@ def main(argv=None):
     from .main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from .model import build_model
     model = build_model(len(vocab), args.dims, args.layers, args.attn_heads, dropout=args.dropout).to(dev)
+    if args.dropout != 0.1:
+        # every dropout layer, including the ones the reference fixes at 0.1 (fusion.py af_adapter /
+        # fusion, foundation_model.py GenotypeClassifier FeedForward)
+        for mod in model.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = args.dropout
     if world > 1:   # identical initial weights on every rank
         import torch.distributed as dist
         for t in list(model.parameters()) + list(model.buffers()):

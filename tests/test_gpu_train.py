@@ -677,6 +677,13 @@ def test_train_v18_gradients_bf16_drift_bar():
         p = named[name]
         rn = float(g[f"gn:{name}"])
         got = p.grad.detach().float().cpu().numpy() if p.grad is not None else np.zeros(p.shape, np.float32)
+        if name.endswith("attention.linear_layers.1.bias"):
+            # the key bias adds q . b_k to every score of a query: softmax cancels it, the true
+            # gradient is 0 and both sides hold rounding noise (bf16 here: no direction to compare)
+            wk = float(g[f"gn:{name[:-len('bias')]}weight"])
+            print(f"{name}: |grad| {np.linalg.norm(got):.3e} (reference {rn:.3e}, key weight {wk:.3e})")
+            assert np.linalg.norm(got) <= 0.05 * wk + 10 * rn, name
+            continue
         est, rel_s, cos = GS.compare(name, got, g)
         c = _v18_layer_class(name)
         num[c] = num.get(c, 0.0) + (est * rn) ** 2
