@@ -254,7 +254,8 @@ struct NoMid {
 //      issue arbitration over the co-resident waves' exp streams);
 //   2  like 1, and the S MFMAs at the head of the tile as well;
 //   3  K fragments passed in ``kin`` (read one tile ahead by the caller) and ``mid`` run between
-//      the exps and the PV block (the caller's ring barrier + next-tile K prefetch).
+//      the exps and the PV block (the caller's ring barrier + next-tile K prefetch);
+//   5  the V^T fragments read right after the S MFMAs (LDS latency under the exps).
 template <int NKT, bool MASK, bool FIRST, bool TRAIN = false, int VAR = 0, typename Mid = NoMid>
 __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, int L, const bf16x8 (&qf)[2],
                                      State& st, int li, int lg, const Train& tr = Train{},
@@ -296,6 +297,18 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
     }
   }
   constexpr int NCB = (NKT + 1) / 2;
+  const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
+  // VAR 5: the V^T fragments read right after the S MFMAs, their LDS latency under the exps
+  bf16x8 vpre[VAR == 5 ? NCB : 1][2];
+  if constexpr (VAR == 5) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int k0 = 32 * cb + 4 * lg + tq;
+        vpre[cb][e] = cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
+      }
+  }
   bf16x8 pb[NCB][2];
   bf16x8 pd[TRAIN ? NCB : 1][2];                 // TRAIN: the dropped-out PV operand
 #pragma unroll
@@ -333,14 +346,14 @@ __device__ __forceinline__ void tile(const char* Kt, const char* Vt, int kbase, 
   }
   mid();
   const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
-  const int tq = li >> 2, tp = li & 3;          // ds_read_b64_tr_b16: lane 4q+p -> row q, columns 4p..4p+3
   if constexpr (VAR == 1 || VAR == 2) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int k0 = 32 * cb + 4 * lg + tq;
-      const bf16x8 vf = cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
+      const bf16x8 vf = VAR == 5 ? vpre[VAR == 5 ? cb : 0][e]
+                                 : cat(tr_read(Vt + v_off(k0, e) + 8 * tp), tr_read(Vt + v_off(k0 + 16, e) + 8 * tp));
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
         st.o[e][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, TRAIN ? pd[TRAIN ? cb : 0][qt] : pb[cb][qt],
@@ -463,7 +476,7 @@ constexpr int SLOT = 2 * TB;                    // K tile + V tile
 // tile's 8 KiB of LDS-DMA is shared by twice the queries, one DMA instruction per wave per tile
 // (waves 0-3 move K, 4-7 move V) instead of two.
 template <bool PRESCALED, bool TRAIN = false, int VAR = 0>
-__global__ __launch_bounds__(VAR == 4 ? 512 : 256, VAR == 4 ? 4 : 1) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
+__global__ __launch_bounds__(VAR == 4 ? 512 : 256, VAR == 4 || VAR == 5 ? 4 : 1) void attn32_dma(int L, int H, const bf16* __restrict__ qkv, long ld,
                                                   bf16* __restrict__ out, long ldo, float scale_log2e, int nqb,
                                                   int* __restrict__ n_fallback, long total_rows,
                                                   float* __restrict__ lse = nullptr, AttnDrop drop = AttnDrop{}) {
@@ -731,7 +744,7 @@ static int launch_attn(int dtype, long nseq, long L, int H, const void* qkv, lon
     const int var = (int)options().attn_variant;
     auto kp = var == 1 ? attn32_dma<true, false, 1> : var == 2 ? attn32_dma<true, false, 2>
               : var == 3 ? attn32_dma<true, false, 3> : var == 4 ? attn32_dma<true, false, 4>
-              : attn32_dma<true, false, 0>;
+              : var == 5 ? attn32_dma<true, false, 5> : attn32_dma<true, false, 0>;
     const int nqb8 = cdiv(L, 2 * a32::QPB);
     if (pre && var == 4)
       hipLaunchKernelGGL(kp, dim3((unsigned)(nqb8 * H * nseq)), dim3(512), 0, s, (int)L, H, (const bf16*)qkv, ld,

@@ -530,7 +530,8 @@ def test_proj_kernel_vs_fp64(D, M, NC):
 @pytest.mark.parametrize("L", [1030, 520, 77])
 def test_attention_dh32_variants_bit_identical(L):
     """The inference attention kernel's A/B variants (option attn_variant: 1/2 s_setprio around the
-    MFMA blocks, 3 the next tile's K read ahead, 4 eight-wave workgroups sharing each K/V tile) run
+    MFMA blocks, 3 the next tile's K read ahead, 4 eight-wave workgroups sharing each K/V tile, 5 the
+    V fragments read before the exps) run
     the same arithmetic in the same order: bit-identical to variant 0 (prescaled Q, the engine's
     form), and variant 0 matches the fp32 softmax."""
     import math
@@ -541,12 +542,12 @@ def test_attention_dh32_variants_bit_identical(L):
     qkv = qkv.to(torch.bfloat16)
     scale = 1.0 / math.log2(math.e)                     # Q carries log2(e)/sqrt(dh)
     outs = {}
-    for v in (0, 1, 2, 3, 4):
+    for v in (0, 1, 2, 3, 4, 5):
         with K().option("attn_variant", v):
             outs[v] = K().attention(qkv, nseq, L, H, dh, scale=scale)
     q = qkv.float().clone()
     q[:, :H * dh] *= math.sqrt(dh) / math.log2(math.e)
     ref = _attn_ref(q, nseq, L, H, dh)
     torch.testing.assert_close(outs[0].float(), ref, rtol=2e-2, atol=2e-2)
-    for v in (1, 2, 3, 4):
+    for v in (1, 2, 3, 4, 5):
         assert torch.equal(outs[v], outs[0]), v

@@ -26,6 +26,8 @@ for s in ${STEPS:-new attn bench}; do
     attn)  step attn_only 240 env REPS=8 ROUNDS=3 ATTN_VARIANTS=${ATTN_VARIANTS:-0} python tools/attn_only.py
            step train_attn 200 python tools/train_attn_micro.py ;;
     pmc)   step attn_pmc 300 env TAG=${TAG}_attn bash tools/pmc_attn.sh ;;
+    tprof) step train_torchprof 400 python tools/train_torchprof.py
+           step train_only 300 python tools/train_only.py ;;
     gpu)   step pytest_gpu 1100 $PT tests -m gpu ${PYTEST_ARGS:-} ;;
     sel)   step pytest_sel 800 $PT tests -m gpu -k "${PYTEST_K}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
