@@ -55,7 +55,13 @@ __global__ __launch_bounds__(256) void focal_kernel(long M, int C, const float* 
   if (threadIdx.x == 0) atomicAdd(loss_sum, red[0] + red[1] + red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __restrict__ x, float* __restrict__ acc) {
+// Two passes with a fixed summation order (no float atomics): every rank of a data-parallel
+// job holds the same reduced gradient and must derive the same clip coefficient bit for bit,
+// or the replicas drift apart after the first optimizer step.
+constexpr int kSqBlocks = 2048;
+__device__ float g_sq_partials[kSqBlocks];   // one launch pair in flight per process (stream-ordered)
+
+__global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __restrict__ x) {
   __shared__ float red[4];
   float s = 0.f;
   const long n4 = n / 4;
@@ -68,7 +74,17 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __rest
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(acc, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) g_sq_partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void sqnorm_final_kernel(int nblocks, float* __restrict__ acc) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nblocks; i += 256) s += g_sq_partials[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *acc = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
@@ -145,10 +161,14 @@ extern "C" int snvrag_focal_loss(int64_t M, int C, const float* probs, const int
 extern "C" int snvrag_sqnorm(int64_t n, const float* x, float* acc, void* stream) {
   SNV_CHECK_ARG(x && acc && ((uintptr_t)x % 16) == 0, "null or misaligned pointer");
   hipStream_t s = as_stream(stream);
-  SNV_HIP(hipMemsetAsync(acc, 0, sizeof(float), s));
-  if (n == 0) return 0;
-  const int grid = (int)std::min<long>(cdiv(n / 4 + 1, 256), 2048);
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, (long)n, x, acc);
+  if (n == 0) {
+    SNV_HIP(hipMemsetAsync(acc, 0, sizeof(float), s));
+    return 0;
+  }
+  const int grid = (int)std::min<long>(cdiv(n / 4 + 1, 256), kSqBlocks);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, (long)n, x);
+  SNV_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, grid, acc);
   SNV_LAUNCH_CHECK();
   return 0;
 }

@@ -73,7 +73,12 @@ def _trainer(m, ds, vocab, bucket_bytes=256 << 10):
     def step(grad_scale=1.0):           # the reduced gradient and the weights the step starts from
         captured.append((tr.flat.grad.detach().cpu().clone(), tr.flat.flat.detach().cpu().clone(), grad_scale))
         orig(grad_scale)
+        torch.cuda.synchronize()
+        post.append(dict(flat=tr.flat.flat.detach().cpu().clone(), sq=float(tr.optim.sq.item()),
+                         lr=float(tr.optim.param_groups[0]["lr"]), step=tr.optim.step_count))
+    post = []
     tr.optim.step = step
+    tr._post = post
     return tr, captured
 
 
@@ -119,6 +124,7 @@ def _ddp_worker(rank, world, port, panel, q):
                                unused=unused))
         names = {id(p): n for n, p in m.named_parameters()}
         q.put((rank, dict(checks=checks, steps=[(g.numpy(), f.numpy(), s) for g, f, s in captured],
+                          post=[dict(d, flat=d["flat"].numpy()) for d in tr._post],
                           final=tr.flat.flat.detach().cpu().numpy(), n_buckets=len(bk.buckets),
                           names=[names[id(p)] for p in tr.flat.params], offsets=list(tr.flat.offsets))))
     except Exception:
@@ -159,6 +165,15 @@ def _replay_grad(flat_before, items):
     return captured[0][0].numpy()
 
 
+def _adam_host(p, g, sq, lr, step, scale, b1=0.9, b2=0.999, eps=1e-8, wd=0.01, max_norm=1.0):
+    """FusedAdam's first step (m = v = 0) in float64 from the captured inputs."""
+    p, g = p.astype(np.float64), g.astype(np.float64)
+    coef = scale * min(max_norm / (np.sqrt(sq) * scale + 1e-6), 1.0)
+    gi = g * coef + wd * p
+    m, v = (1 - b1) * gi, (1 - b2) * gi * gi
+    return p - lr / (1 - b1 ** step) * m / (np.sqrt(v) / np.sqrt(1 - b2 ** step) + eps)
+
+
 def _rel(a, b):
     return float(np.linalg.norm(a.astype(np.float64) - b) / max(np.linalg.norm(b.astype(np.float64)), 1e-30))
 
@@ -179,6 +194,10 @@ def test_ddp_train_step_buckets_final_and_ranks_equal(panel):
         assert sc0 == sc1 == 1.0
         # identical weights going into the step and identical reduced gradients on both ranks
         df, dg = np.nonzero(f0 != f1)[0], np.nonzero(g0 != g1)[0]
+        for r in (0, 1) if s == 0 else ():   # the first Adam step consumed the reduced gradient
+            pr, (gr, fr, sc) = got[r]["post"][s], got[r]["steps"][s]
+            d = np.abs(pr["flat"] - _adam_host(fr, gr, pr["sq"], pr["lr"], pr["step"], sc))
+            assert d.max() <= 1e-5, (panel, r, float(d.max()))
         where = lambda ix: sorted({got[0]["names"][int(np.searchsorted(got[0]["offsets"], i, "right")) - 1]
                                    for i in ix[:2000]})[:12]
         assert df.size == 0 and dg.size == 0, (panel, s, df.size, dg.size, where(df), where(dg),

@@ -448,6 +448,22 @@ def test_fused_adam_with_clip_vs_oracle():
     np.testing.assert_allclose(fp.bf16.float().cpu().numpy(), p0, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("n", [1, 7, 4096 + 3, 26_000_001])
+def test_sqnorm_deterministic_and_exact(n):
+    """The clip norm every data-parallel rank derives from the same reduced gradient must agree
+    bit for bit (fixed-order two-pass sum), and match float64 to f32 summation accuracy."""
+    from src import kernels as K
+    x = torch.randn(n, generator=torch.Generator(device="cpu").manual_seed(n)).to(DEV)
+    acc = torch.empty(1, device=DEV)
+    vals = set()
+    for _ in range(5):
+        K.sqnorm(x, acc)
+        vals.add(acc.item())
+    assert len(vals) == 1
+    want = float(np.sum(x.cpu().numpy().astype(np.float64) ** 2))
+    assert abs(vals.pop() - want) <= 1e-5 * want
+
+
 def test_rag_mean_train_gradients():
     from src.autograd_ops import rag_mean_train
     from src.retrieval import PanelIndex
