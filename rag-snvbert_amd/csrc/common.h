@@ -69,6 +69,7 @@ struct Options {
   int64_t sg_waves4;       // 1: 4-wave stream GEMM for the rank-free projections (A/B)
   int64_t ln_bwd_nopf;     // 1: LayerNorm backward without the next-row prefetch (A/B)
   int64_t attn_variant;    // inference attention (dh 32) A/B variant, 0 = default (attention.hip tile)
+  int64_t dw_xcd;          // 1: dW workgroups of one M chunk dealt to one XCD (0: plain grid order, A/B)
 };
 Options& options();
 

@@ -35,7 +35,8 @@ __device__ __forceinline__ bf16x4 dw_tr(const char* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-// grid: (N / 128, K / 128, S); 256 threads = 4 waves, wave (wn, wk) owns the 64 x 64 sub-tile
+// grid: (N / 128) (K / 128) S blocks (tile, chunk: see the kernel); 256 threads = 4 waves,
+// wave (wn, wk) owns the 64 x 64 sub-tile
 // n0 + 64 wn, k0 + 64 wk (2 x 2 MFMA tiles of 32 x 32).
 // Output of the launch: dW rows (and db entries) n live in part n / seg of up to 4 separately
 // allocated buffers (the q/k/v weights of one fused N = 3D output), each [seg, K] / [seg].
@@ -53,22 +54,36 @@ struct DwOut {
 constexpr int DWD_NS = 4;
 
 __global__ __launch_bounds__(256) void dw_dma_kernel(int M, int N, int K, const bf16* __restrict__ dy, long ldy,
-                                                     const bf16* __restrict__ x, long ldx, DwOut out, int chunk) {
-  // one __shared__ object per ring slot: the compiler's LDS-DMA wait tracking then knows that a
-  // stage's ds_reads do not alias the DMA just issued into another slot (with one array it puts a
-  // vmcnt(0) before every read, draining the whole ring each stage)
+                                                     const bf16* __restrict__ x, long ldx, DwOut out, int chunk,
+                                                     int xcd_map) {
+  // one __shared__ object per ring slot, filled by the inline-asm DMA (dma_x4): the compiler's
+  // waitcnt pass does not track LDS-DMA across the loop back-edge (with the builtin it still put a
+  // vmcnt(0) before the first slot's reads of every ring cycle, draining the ring once per cycle);
+  // the counted vmcnt waits below are the only ones
   __shared__ __attribute__((aligned(16))) char sl0[DW_STAGE], sl1[DW_STAGE], sl2[DW_STAGE], sl3[DW_STAGE];
   static_assert(DWD_NS == 4, "four slot objects");
   auto slot_ptr = [&](int i) -> char* { return i == 0 ? sl0 : i == 1 ? sl1 : i == 2 ? sl2 : sl3; };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 1, wk = wave & 1;
-  const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
+  // 1-D grid of tiles x chunks.  Blocks b and b + 8 share an XCD (round-robin dealing,
+  // MI355X_MICROARCH.md "Workgroup dispatch"): with xcd_map the work items (chunk-major, tiles
+  // inner) are cut into 8 contiguous ranges, one per XCD, so all tiles of an M chunk run on one
+  // XCD and read its rows from HBM once (L2 serves the other tiles); in plain order the tiles of
+  // a chunk are spread over all 8 XCDs and each XCD fetches the chunk's rows again.
+  const int nx = N / DW_T, ntile = nx * (K / DW_T);
+  int w = blockIdx.x;
+  if (xcd_map) {
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3, rem = gridDim.x & 7;
+    w = xcd * per + min(xcd, rem) + (blockIdx.x >> 3);
+  }
+  const int tile = w % ntile, zc = w / ntile;
+  const int n0 = (tile % nx) * DW_T, k0 = (tile / nx) * DW_T;
   const int part = n0 / out.seg;
   const int nbase = part * out.seg;
   float* __restrict__ dw = out.w[part];
   float* __restrict__ db = out.b[part];
-  const int m_begin = blockIdx.z * chunk;
+  const int m_begin = zc * chunk;
   const int m_end = min(M, m_begin + chunk);
   if (m_begin >= m_end) return;                      // whole workgroup, before any barrier
   const int nst = (m_end - m_begin + DW_R - 1) / DW_R;
@@ -76,10 +91,8 @@ __global__ __launch_bounds__(256) void dw_dma_kernel(int M, int N, int K, const 
   // sources: this chunk's rows only (the resource ends at m_end: later rows read zeros)
   const long rows = m_end - m_begin;
   const long by = (rows - 1) * ldy * 2 + (long)DW_T * 2, bx = (rows - 1) * ldx * 2 + (long)DW_T * 2;
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(dy + (long)m_begin * ldy + n0), (short)0, (int)(by < 0x7fffffffL ? by : 0x7fffffffL), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(x + (long)m_begin * ldx + k0), (short)0, (int)(bx < 0x7fffffffL ? bx : 0x7fffffffL), 0x00020000);
+  const i32x4 ry = dma_rsrc(dy + (long)m_begin * ldy + n0, by);
+  const i32x4 rx = dma_rsrc(x + (long)m_begin * ldx + k0, bx);
   // piece j (0..7) of an operand = rows 4 j .. 4 j + 3; wave w issues pieces 2 w, 2 w + 1 of dY and
   // of X.  Lane l lands at byte 16 l of the piece: row 4 j + l / 16, 16-B unit u = l % 16 of the
   // 256-B row, i.e. 32-B block u / 2 which dw_swz fills from column block (u / 2) ^ (row & 7)
@@ -93,14 +106,12 @@ __global__ __launch_bounds__(256) void dw_dma_kernel(int M, int N, int K, const 
   }
   const int sty = (int)(DW_R * ldy * 2), stx = (int)(DW_R * ldx * 2);
   auto issue = [&](int st, int slot) __attribute__((always_inline)) {
-    char* s = slot_ptr(slot);
+    const uint32_t s = lds_addr(slot_ptr(slot));
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * wave + i;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) char*)(s + j * 1024), 16,
-                                               voy[i], st * sty, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) char*)(s + DW_R * 256 + j * 1024),
-                                               16, vox[i], st * stx, 0, 0);
+      dma_x4(ry, s + j * 1024, voy[i], st * sty);
+      dma_x4(rx, s + DW_R * 256 + j * 1024, vox[i], st * stx);
     }
   };
   auto wait = [&](int y) {                           // 4 DMA per stage per wave
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(256) void dw_dma_kernel(int M, int N, int K, const 
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
-  const bool do_db = db != nullptr && blockIdx.y == 0 && wk == 0;
+  const bool do_db = db != nullptr && k0 == 0 && wk == 0;
   float dbs[2] = {0.f, 0.f};
   auto compute = [&](const char* s) __attribute__((always_inline)) {
 #pragma unroll
@@ -215,8 +226,9 @@ static int launch_dw(int64_t M, int64_t N, int64_t K, const void* dy, int64_t ld
   const int chunk = (int)((((M + splits - 1) / splits) + DW_R - 1) / DW_R * DW_R);
   const int S = (int)((M + chunk - 1) / chunk);
   evlog_begin(s);
-  hipLaunchKernelGGL(dw_dma_kernel, dim3((unsigned)(N / DW_T), (unsigned)(K / DW_T), (unsigned)S), dim3(256), 0, s,
-                     (int)M, (int)N, (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk);
+  hipLaunchKernelGGL(dw_dma_kernel, dim3((unsigned)((N / DW_T) * (K / DW_T) * S)), dim3(256), 0, s, (int)M, (int)N,
+                     (int)K, (const bf16*)dy, (long)ldy, (const bf16*)x, (long)ldx, out, chunk,
+                     (int)options().dw_xcd);
   SNV_LAUNCH_CHECK();
   evlog_end(s, EV_TRAIN, 2.0 * M * (double)N * K);
   return 0;

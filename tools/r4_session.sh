@@ -28,6 +28,9 @@ for s in ${STEPS:-new attn bench}; do
     pmc)   step attn_pmc 300 env TAG=${TAG}_attn bash tools/pmc_attn.sh ;;
     tprof) step train_torchprof 400 python tools/train_torchprof.py
            step train_only 300 python tools/train_only.py ;;
+    dw)    step dw_micro 300 env DW_XCD=0,1 python tools/dw_micro.py ;;
+    tonly) step train_only_a 300 env SNVRAG_DW_XCD=0 python tools/train_only.py
+           step train_only_b 300 env SNVRAG_DW_XCD=1 python tools/train_only.py ;;
     gpu)   step pytest_gpu 1100 $PT tests -m gpu ${PYTEST_ARGS:-} ;;
     sel)   step pytest_sel 800 $PT tests -m gpu -k "${PYTEST_K}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
