@@ -473,7 +473,7 @@ def train_bench(args, world, rank, dev):
 def knn_c2(args, wl, eng, k):
     """SURVEY §8d C2 embedding-space mode (cross-check of the token index): the reference's
     literal retrieval — bf16 window embeddings of the first ``args.c2_n`` panel haplotypes,
-    [N, 1030 * D], exact L2 + top-k (csrc/knn_emb.hip distance GEMM, HBM-bound) — timed at
+    [N, 1030 * D] (stored in the scan's tiled layout), exact L2 + top-k (csrc/knn_emb.hip distance GEMM, HBM-bound) — timed at
     Bq in {48, 96}; its neighbours checked against the token index's exact distances; and the
     reference-equivalent CPU cost (torch.cdist + topk over a panel sample, the v18 training
     path's own call) on the host cores."""
@@ -491,15 +491,15 @@ def knn_c2(args, wl, eng, k):
     eidx = EmbeddingIndex.build(tr, P.W, P.pe, Ar)
     lib, cap = N.lib(), 256
     out = dict(mode="embedding-space exact L2 (reference-literal cdist / IndexFlatL2 over bf16 [N, L*D])",
-               panel_haplotypes=n, dims=L * D, index_bytes=int(eidx.E.numel() * 2), bound="hbm", peak=HBM_PEAK_GBS,
+               panel_haplotypes=n, dims=L * D, index_bytes=int(eidx.n * L * D * 2), bound="hbm", peak=HBM_PEAK_GBS,
                per_queries=[])
     for bq in (48, 96):
         Q = eidx.embed_queries(wl.tok[:bq], P.W, P.pe, Ar)
         qn = K.knn_emb_norms(Q)
-        K.knn_emb_dist(eidx.E, Q, eidx.norms, qn)
+        K.knn_emb_dist(eidx.Et, Q, eidx.norms, qn)
         lib.snvrag_evlog_enable(cap)
         for _ in range(5):
-            K.knn_emb_dist(eidx.E, Q, eidx.norms, qn)
+            K.knn_emb_dist(eidx.Et, Q, eidx.norms, qn)
         torch.cuda.synchronize()
         kk, mm, ww = np.zeros(cap, np.int32), np.zeros(cap, np.float32), np.zeros(cap, np.float64)
         n2 = lib.snvrag_evlog_read(kk.ctypes.data, mm.ctypes.data, ww.ctypes.data, cap)
@@ -535,7 +535,7 @@ def knn_c2(args, wl, eng, k):
     # reference-equivalent CPU: torch.cdist + topk (embedding_rag_dataset.py:390-402) on a sample
     threads = torch.get_num_threads()
     m = min(n, 512)
-    Ec = eidx.E[:m].float().cpu()
+    Ec = eidx.rows(0, m).float().cpu()
     Qc = Q[:48].float().cpu()
     t0 = time.perf_counter()
     reps = 0

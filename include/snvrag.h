@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 24
+#define SNVRAG_ABI_VERSION 25
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -228,12 +228,17 @@ int snvrag_knn_decode(const uint64_t* keys, int32_t nq, int k, const int32_t* ex
  * retrieval over flattened window embeddings (embedding_rag_dataset.py:390-402 torch.cdist +
  * topk; embedding_rag_infer_dataset.py:176-177 IndexFlatL2 over [N, L*D]).
  * E bf16 [N, K] panel embeddings, Q bf16 [Bq, K] queries, K % 64 == 0, Bq <= 128.
- * scan: ws (f32, knn_emb_ws_bytes) <- per-split partial dots Q E^T;
+ * pack: E row-major -> Et (knn_emb_packed_bytes), the scan's index layout: 4 KiB tiles of
+ *   32 rows x 64 k, tile-major over k then rows, each ordered [k-step 4][half 2][row 32][8 k],
+ *   rows past N zero (done once when the index is built);
+ * scan: ws (f32, knn_emb_ws_bytes) <- per-split partial dots Q Et^T;
  * finish: dist [Bq, N] f32 = qn[q] + rn[r] - 2 sum_split ws (qn, rn: squared norms).
  * splits: 1..256 (snvrag_knn_emb_splits picks one that fills the chip). */
 int snvrag_knn_emb_splits(int64_t N, int64_t K, int Bq);
 size_t snvrag_knn_emb_ws_bytes(int64_t N, int Bq, int splits);
-int snvrag_knn_emb_scan(const void* E, int64_t N, int64_t K, const void* Q, int Bq, int splits, float* ws,
+size_t snvrag_knn_emb_packed_bytes(int64_t N, int64_t K);
+int snvrag_knn_emb_pack(const void* E, int64_t N, int64_t K, void* Et, void* stream);
+int snvrag_knn_emb_scan(const void* Et, int64_t N, int64_t K, const void* Q, int Bq, int splits, float* ws,
                         void* stream);
 int snvrag_knn_emb_finish(const float* ws, int splits, int Bq, int64_t N, const float* qn, const float* rn,
                           float* dist, void* stream);

@@ -6,10 +6,17 @@
 // dot[q][r] = Q[q] . E[r] over K = L * D — HBM-bound: every panel byte read once per launch
 // (N * K * 2 B), the queries (Bq * K * 2 B) re-read from L2.
 //
+// Index layout in HBM (snvrag_knn_emb_pack, once at index build): 32-row x 64-k TILES, each 4 KiB
+// contiguous, tile-major over k then rows: tile (T, b) holds rows 32 T .. + 31, k = 64 b .. + 63,
+// ordered [k-step s 4][half kh 2][row m 32][8 k] — so the 16 B a lane (m, kh) needs for k-step s
+// of an MFMA A operand sit at byte 1024 s + 16 (m + 32 kh) and every wave load instruction reads
+// one contiguous KiB.  (Row-major [N, K] rows put each instruction's 64 lanes on 32 rows 791 KB
+// apart, 32 B each: 39-46 % of HBM peak against 55-64 % tiled at the C2 shape, tools/knn_emb_micro.py.)
+// Rows past N are zero-padded to a whole tile.
+//
 // A workgroup owns 4 x 32 RT panel rows (each wave RT 32-row MFMA tiles) and one of `splits`
-// slices of K.  Each wave streams its rows' bf16 values straight into VGPRs as the A operand of
-// v_mfma_f32_32x32x16_bf16 (lane (m, kh): E[row + m][k + 8 kh .. + 7]; four k-steps per batch =
-// 128 contiguous bytes per row; PF batches in flight in a register ring).  The queries are the
+// slices of K.  Each wave streams its tiles' bf16 values straight into VGPRs as the A operand of
+// v_mfma_f32_32x32x16_bf16 (PF batches of 64 k in flight in a register ring).  The queries are the
 // B operand, shared by the 4 waves: each batch's query fragments are DMA'd global -> LDS
 // (buffer_load ... lds, 1 KiB per wave instruction, already in B-fragment order) into a ring of
 // PF + 1 slots with one barrier per batch, so a workgroup fetches QT KiB of queries per k-step
@@ -18,7 +25,15 @@
 // squared distances.
 #include "common.h"
 
+#include <utility>
+
 namespace snvrag {
+
+// f(integral_constant<int, J>) for each J of the sequence, in order
+template <int... J, class F>
+__device__ __forceinline__ void for_slots(std::integer_sequence<int, J...>, F&& f) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
 
 template <int RT, int QT, int PF>
 __global__ __launch_bounds__(256) void knn_emb_dot_kernel(const bf16* __restrict__ E, long N, long K,
@@ -35,18 +50,20 @@ __global__ __launch_bounds__(256) void knn_emb_dot_kernel(const bf16* __restrict
   const int m = lane & 31, kh = lane >> 5;
   const long rb = ((long)blockIdx.x * 4 + wave) * 32 * RT;
   const int split = blockIdx.y;
-  const long nb = K / KB;
-  const long b0 = nb * split / splits, b1 = nb * (split + 1) / splits;   // may be empty: zeros
+  // 32-bit batch counters: 64-bit compares run on the VALU, and the compiler's temporaries for
+  // them landed on a register of an in-flight row load (a write-after-write vmcnt(0) draining the
+  // whole load ring every PF + 1 batches)
+  const int nb = (int)(K / KB);
+  const int b0 = (int)((long)nb * split / splits), b1 = (int)((long)nb * (split + 1) / splits);   // may be empty
   const bf16* er[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     long r = rb + 32 * t + m;
     r = r < N ? r : N - 1;
-    er[t] = E + r * K + 8 * kh;
+    er[t] = E + (r >> 5) * 32 * K + 8 * lane;        // this lane's 16 B in k-step 0 of tile (r / 32, 0)
   }
   // fragment f = u S + s of a batch: lane (n, kh) <- Q[32 u + n][k0 + 16 s + 8 kh .. + 7]
-  const __amdgpu_buffer_rsrc_t qrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)((long)Bq * K * 2), 0x00020000);
+  const i32x4 qrs = dma_rsrc(Q, (long)Bq * K * 2);
   int qoff[FPW];
 #pragma unroll
   for (int i = 0; i < FPW; ++i) {
@@ -61,20 +78,16 @@ __global__ __launch_bounds__(256) void knn_emb_dot_kernel(const bf16* __restrict
 #pragma unroll
     for (int u = 0; u < QT; ++u) acc[t][u] = f32x16{};
   u32x4 ev[PF + 1][RT][S];
-  auto issue = [&](long b, int slot) {
-    const long bb = b < b1 ? b : b1 - 1;            // past the range: re-read the last batch
-    const int kbyte = (int)(bb * KB * 2);
-    auto* dst = (__attribute__((address_space(3))) char*)(qring + slot * SLOT + wave * FPW * 1024);
+  auto issue = [&](int b, int slot) {
+    const int bb = b < b1 ? b : b1 - 1;             // past the range: re-read the last batch
+    const int kbyte = bb * KB * 2;
+    const uint32_t dst = lds_addr(qring + slot * SLOT + wave * FPW * 1024);
 #pragma unroll
-    for (int i = 0; i < FPW; ++i) {
-      // (offsets through locals: an array-element argument makes the host pass drop the kernel stub)
-      const int vo = qoff[i], so = kbyte;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qrs, dst + i * 1024, 16, vo, so, 0, 0);
-    }
+    for (int i = 0; i < FPW; ++i) dma_x4(qrs, dst + i * 1024, qoff[i], kbyte);
 #pragma unroll
     for (int s2 = 0; s2 < S; ++s2)
 #pragma unroll
-      for (int t = 0; t < RT; ++t) ev[slot][t][s2] = *reinterpret_cast<const u32x4*>(er[t] + bb * KB + 16 * s2);
+      for (int t = 0; t < RT; ++t) ev[slot][t][s2] = *reinterpret_cast<const u32x4*>(er[t] + (long)bb * 32 * KB + 512 * s2);
   };
   if (b0 < b1) {
 #pragma unroll
@@ -82,29 +95,33 @@ __global__ __launch_bounds__(256) void knn_emb_dot_kernel(const bf16* __restrict
   }
   constexpr int AFTER = RT * S + (PF - 1) * (RT * S + FPW);   // loads issued after a batch's DMA
   static_assert(AFTER <= 63, "vmcnt range");
-  for (long b = b0; b < b1; b += PF + 1) {
+  auto batch = [&](int b, auto j_tag) __attribute__((always_inline)) {
+    constexpr int j = decltype(j_tag)::value;     // ring slot: a compile-time register / LDS index
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER) : "memory");   // my DMA of batch b landed
+    __builtin_amdgcn_s_barrier();                                    // everyone's; slot j-1 free
+    issue(b + PF, (j + PF) % (PF + 1));
+    const char* qs = qring + j * SLOT + lane * 16;
 #pragma unroll
-    for (int j = 0; j <= PF; ++j) {
-      if (b + j < b1) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AFTER) : "memory");   // my DMA of batch b + j landed
-        __builtin_amdgcn_s_barrier();                                    // everyone's; slot j-1 free
-        issue(b + j + PF, (j + PF) % (PF + 1));
-        const char* qs = qring + j * SLOT + lane * 16;
+    for (int s2 = 0; s2 < S; ++s2) {
+      u32x4 qf[QT];
 #pragma unroll
-        for (int s2 = 0; s2 < S; ++s2) {
-          u32x4 qf[QT];
+      for (int u = 0; u < QT; ++u) qf[u] = *reinterpret_cast<const u32x4*>(qs + (u * S + s2) * 1024);
 #pragma unroll
-          for (int u = 0; u < QT; ++u) qf[u] = *reinterpret_cast<const u32x4*>(qs + (u * S + s2) * 1024);
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-          for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int u = 0; u < QT; ++u)
-              acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ev[j][t][s2]),
-                                                                  __builtin_bit_cast(bf16x8, qf[u]), acc[t][u], 0, 0, 0);
-        }
-      }
+        for (int u = 0; u < QT; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ev[j][t][s2]),
+                                                              __builtin_bit_cast(bf16x8, qf[u]), acc[t][u], 0, 0, 0);
     }
-  }
+  };
+  // whole ring cycles without conditions (a conditional body made the compiler shuffle the ring
+  // registers at the back-edge and drain the loads), then the < PF + 1 remaining batches
+  int b = b0;
+  for (; b + PF + 1 <= b1; b += PF + 1)
+    for_slots(std::make_integer_sequence<int, PF + 1>{}, [&](auto j) { batch(b + j, j); });
+  for_slots(std::make_integer_sequence<int, PF + 1>{}, [&](auto j) {
+    if (b + j < b1) batch(b + j, j);
+  });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the overrun DMAs have landed before exit
 #pragma unroll
   for (int t = 0; t < RT; ++t)
@@ -119,6 +136,20 @@ __global__ __launch_bounds__(256) void knn_emb_dot_kernel(const bf16* __restrict
         if (r < N) dst[r] = acc[t][u][i];
       }
     }
+}
+
+// row-major [N, K] -> the tiled layout above; one 16-B unit per thread, coalesced stores
+__global__ void knn_emb_pack_kernel(const bf16* __restrict__ E, long N, long K, bf16* __restrict__ Et, long units) {
+  const long u = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= units) return;
+  const int lane = (int)(u & 63), s = (int)((u >> 6) & 3);
+  const long tb = u >> 8;                          // (tile, batch) = 4 KiB blocks
+  const long nbk = K / 64, tile = tb / nbk, b = tb % nbk;
+  const long row = tile * 32 + (lane & 31);
+  const long k = b * 64 + 16 * s + 8 * (lane >> 5);
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (row < N) v = *reinterpret_cast<const u32x4*>(E + row * K + k);
+  *reinterpret_cast<u32x4*>(Et + u * 8) = v;
 }
 
 __global__ void knn_emb_finish_kernel(const float* __restrict__ part, int splits, int Bq, long N,
@@ -137,11 +168,27 @@ __global__ void knn_emb_finish_kernel(const float* __restrict__ part, int splits
 
 using namespace snvrag;
 
+constexpr int KE_RT = 2, KE_PF = 2, KE_KB = 64;   // rows tiles per wave, batches in flight, k per batch
+
+extern "C" size_t snvrag_knn_emb_packed_bytes(int64_t N, int64_t K) {
+  return (size_t)((N + 31) / 32) * 32 * (size_t)K * 2;
+}
+
+extern "C" int snvrag_knn_emb_pack(const void* E, int64_t N, int64_t K, void* Et, void* stream) {
+  SNV_CHECK_ARG(E && Et, "null pointer");
+  SNV_CHECK_ARG(N > 0 && K > 0 && K % KE_KB == 0, "K must be a positive multiple of 64");
+  SNV_CHECK_ARG(((uintptr_t)E % 16) == 0 && ((uintptr_t)Et % 16) == 0, "pointers must be 16-byte aligned");
+  const long units = (long)snvrag_knn_emb_packed_bytes(N, K) / 16;
+  hipLaunchKernelGGL(knn_emb_pack_kernel, dim3((unsigned)cdiv(units, 256)), dim3(256), 0, as_stream(stream),
+                     (const bf16*)E, (long)N, (long)K, (bf16*)Et, units);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" size_t snvrag_knn_emb_ws_bytes(int64_t N, int Bq, int splits) {
   return (size_t)splits * Bq * N * 4;
 }
 
-constexpr int KE_RT = 2, KE_PF = 2, KE_KB = 64;   // rows tiles per wave, batches in flight, k per batch
 
 extern "C" int snvrag_knn_emb_splits(int64_t N, int64_t K, int Bq) {
   // ~1280 workgroups (measured best at the C2 shape: 59 % of HBM peak at Bq 48 vs 51-56 % at

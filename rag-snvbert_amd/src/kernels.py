@@ -357,32 +357,50 @@ def knn_emb_norms(E: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
     return out
 
 
-def knn_emb_dist(E: torch.Tensor, Q: torch.Tensor, rn: torch.Tensor, qn: Optional[torch.Tensor] = None,
+def knn_emb_pack(E: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The scan's index layout (csrc/knn_emb.hip header): bf16 E [N, K] row-major -> bf16
+    [ceil(N / 32) * 32, K] viewed storage of 4 KiB 32-row x 64-k tiles, padding rows zero.
+    ``out`` (e.g. a slice of a larger packed index starting at a row multiple of 32) is filled in
+    place."""
+    assert E.dtype == torch.bfloat16 and E.dim() == 2
+    n, kk = E.shape
+    assert kk % 64 == 0
+    rows = int(N.lib().snvrag_knn_emb_packed_bytes(n, kk)) // (2 * kk)
+    if out is None:
+        out = torch.empty(rows, kk, device=E.device, dtype=torch.bfloat16)
+    assert out.dtype == torch.bfloat16 and out.is_contiguous() and out.numel() >= rows * kk
+    check(N.lib().snvrag_knn_emb_pack(ptr(_c(E)), n, kk, ptr(out), stream_ptr()), "knn_emb_pack")
+    return out
+
+
+def knn_emb_dist(Et: torch.Tensor, Q: torch.Tensor, rn: torch.Tensor, qn: Optional[torch.Tensor] = None,
                  splits: Optional[int] = None) -> torch.Tensor:
     """Exact squared-L2 distances [Bq, N] between bf16 query rows Q [Bq, K] and the panel's
-    flattened window embeddings E [N, K] (csrc/knn_emb.hip; the reference's cdist over
-    [N, L * D], embedding_rag_dataset.py:390-402)."""
-    assert E.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16 and E.shape[1] == Q.shape[1]
-    n, kk = E.shape
+    flattened window embeddings, packed by ``knn_emb_pack`` (Et; N = len(rn), the rows' squared
+    norms) (csrc/knn_emb.hip; the reference's cdist over [N, L * D], embedding_rag_dataset.py:390-402)."""
+    assert Et.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16 and Et.shape[1] == Q.shape[1]
+    n, kk = rn.shape[0], Et.shape[1]
+    assert Et.shape[0] == (n + 31) // 32 * 32, "Et must be knn_emb_pack's output for len(rn) rows"
     bq = Q.shape[0]
     assert 0 < bq <= 128 and kk % 64 == 0
     if splits is None:
         splits = int(N.lib().snvrag_knn_emb_splits(n, kk, bq))
     if qn is None:
         qn = knn_emb_norms(Q)
-    ws = torch.empty(int(N.lib().snvrag_knn_emb_ws_bytes(n, bq, splits)) // 4, device=E.device, dtype=torch.float32)
-    check(N.lib().snvrag_knn_emb_scan(ptr(_c(E)), n, kk, ptr(_c(Q)), bq, splits, ptr(ws), stream_ptr()),
+    ws = torch.empty(int(N.lib().snvrag_knn_emb_ws_bytes(n, bq, splits)) // 4, device=Et.device, dtype=torch.float32)
+    check(N.lib().snvrag_knn_emb_scan(ptr(_c(Et)), n, kk, ptr(_c(Q)), bq, splits, ptr(ws), stream_ptr()),
           "knn_emb_scan")
-    dist = torch.empty(bq, n, device=E.device, dtype=torch.float32)
+    dist = torch.empty(bq, n, device=Et.device, dtype=torch.float32)
     check(N.lib().snvrag_knn_emb_finish(ptr(ws), splits, bq, n, ptr(_c(qn.float())), ptr(_c(rn.float())), ptr(dist),
                                         stream_ptr()), "knn_emb_finish")
     return dist
 
 
-def knn_emb_search(E: torch.Tensor, Q: torch.Tensor, k: int, rn: torch.Tensor, qn: Optional[torch.Tensor] = None):
+def knn_emb_search(Et: torch.Tensor, Q: torch.Tensor, k: int, rn: torch.Tensor, qn: Optional[torch.Tensor] = None):
     """(dist [Bq, k], idx [Bq, k]) — the k nearest panel rows in embedding space, ascending
-    (torch.topk(largest=False) of embedding_rag_dataset.py:401 over the distance row)."""
-    d = knn_emb_dist(E, Q, rn, qn)
+    (torch.topk(largest=False) of embedding_rag_dataset.py:401 over the distance row); Et packed
+    by knn_emb_pack."""
+    d = knn_emb_dist(Et, Q, rn, qn)
     return torch.topk(d, k, dim=1, largest=False, sorted=True)
 
 

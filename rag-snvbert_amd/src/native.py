@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -106,6 +106,8 @@ _SIGS = {
     "snvrag_knn_decode": ([vp, i32, C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_knn_emb_splits": ([i64, i64, C.c_int], C.c_int),
     "snvrag_knn_emb_ws_bytes": ([i64, C.c_int, C.c_int], sz),
+    "snvrag_knn_emb_packed_bytes": ([i64, i64], sz),
+    "snvrag_knn_emb_pack": ([vp, i64, i64, vp, vp], C.c_int),
     "snvrag_knn_emb_scan": ([vp, i64, i64, vp, C.c_int, C.c_int, vp, vp], C.c_int),
     "snvrag_knn_emb_finish": ([vp, C.c_int, C.c_int, i64, vp, vp, vp, vp], C.c_int),
     "snvrag_rag_mean": ([C.c_int, i64, i64, i64, C.c_int, vp, vp, i64, i32, vp, vp, vp, C.c_int, C.c_int,

@@ -6,9 +6,10 @@ Reference behaviour restated (src/dataset/embedding_rag_dataset.py):
     masked window tokens -> BERTEmbedding in eval -> cache [N, L, D];
   * search (:390-402; FAISS IndexFlatL2 in embedding_rag_infer_dataset.py:176-177, 279-285):
     exact L2 over the flattened [L * D] rows, topk(k, largest=False).
-Here the cache is bf16 [N, L * D] in HBM with its squared norms stored at build time, and the
-search is the HBM-bound distance GEMM of csrc/knn_emb.hip (every panel byte read once per
-query batch) followed by top-k over the distance rows.  The production path (PanelIndex)
+Here the cache is bf16 [N, L * D] in HBM — stored in the scan's tiled layout (4 KiB tiles of
+32 rows x 64 dims, K.knn_emb_pack: every wave load one contiguous KiB) — with its squared norms
+stored at build time, and the search is the HBM-bound distance GEMM of csrc/knn_emb.hip (every
+panel byte read once per query batch) followed by top-k over the distance rows.  The production path (PanelIndex)
 computes the same distances from the allele codes without ever materialising E.
 """
 
@@ -41,26 +42,48 @@ def panel_tokens(codes: torch.Tensor, n_sites: int, mask: Optional[np.ndarray], 
 
 
 class EmbeddingIndex:
-    """bf16 [N, L * D] window embeddings of the panel + f32 squared norms."""
+    """bf16 [N, L * D] window embeddings of the panel (packed: ``Et``, K.knn_emb_pack's layout)
+    + f32 squared norms."""
 
-    def __init__(self, E: torch.Tensor, norms: torch.Tensor, L: int, D: int):
+    def __init__(self, Et: torch.Tensor, norms: torch.Tensor, L: int, D: int):
+        n = norms.shape[0]
+        if Et.dtype != torch.bfloat16 or Et.dim() != 2 or Et.shape[1] != L * D or Et.shape[0] != (n + 31) // 32 * 32:
+            raise ValueError("Et must be the packed bf16 [ceil(N / 32) * 32, L * D] index of len(norms) rows")
+        self.Et, self.norms, self.L, self.D = Et, norms, L, D
+        self.n = n
+
+    @classmethod
+    def from_rows(cls, E: torch.Tensor, L: int, D: int) -> "EmbeddingIndex":
+        """From row-major bf16 E [N, L * D] (packed into a new buffer)."""
         if E.dtype != torch.bfloat16 or E.dim() != 2 or E.shape[1] != L * D:
             raise ValueError("E must be bf16 [N, L * D]")
-        self.E, self.norms, self.L, self.D = E, norms, L, D
+        return cls(K.knn_emb_pack(E), K.knn_emb_norms(E), L, D)
 
     @classmethod
     def build(cls, tok: torch.Tensor, W: torch.Tensor, pe: torch.Tensor, Ar: Optional[torch.Tensor] = None,
               chunk: int = 2048) -> "EmbeddingIndex":
         """E[r] = W[tok[r]] + pe + Ar (BERTEmbedding eval; Ar = the window's AF embedding rows,
-        shared by every haplotype of the window), chunked to bound the transient."""
+        shared by every haplotype of the window), embedded chunk by chunk (chunk a multiple of
+        32) into a row-major transient and packed into the tiled index."""
+        assert chunk % 32 == 0
         n, L = tok.shape
         D = W.shape[1]
-        E = torch.empty(n, L * D, device=tok.device, dtype=torch.bfloat16)
+        Et = torch.empty((n + 31) // 32 * 32, L * D, device=tok.device, dtype=torch.bfloat16)
+        norms = torch.empty(n, device=tok.device, dtype=torch.float32)
+        E = torch.empty(min(n, chunk), L * D, device=tok.device, dtype=torch.bfloat16)
         for i in range(0, n, chunk):
             j = min(n, i + chunk)
             K.embed_tokens(tok[i:j].contiguous(), W, pe, Ar, 1 if Ar is not None else 0, torch.bfloat16,
-                           out=E[i:j].view(j - i, L, D))
-        return cls(E, K.knn_emb_norms(E), L, D)
+                           out=E[:j - i].view(j - i, L, D))
+            norms[i:j] = K.knn_emb_norms(E[:j - i])
+            K.knn_emb_pack(E[:j - i], out=Et[i:])
+        return cls(Et, norms, L, D)
+
+    def rows(self, i: int, j: int) -> torch.Tensor:
+        """Row-major bf16 [j - i, L * D] copy of rows i..j-1 (i a multiple of 32)."""
+        assert i % 32 == 0 and 0 <= i < j <= self.n
+        t = self.Et[i:(j + 31) // 32 * 32].view(-1, self.L * self.D // 64, 4, 2, 32, 8)
+        return t.permute(0, 4, 1, 2, 3, 5).reshape(-1, self.L * self.D)[:j - i]
 
     def embed_queries(self, tok_q: torch.Tensor, W: torch.Tensor, pe: torch.Tensor,
                       Aq: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -73,7 +96,7 @@ class EmbeddingIndex:
         batches of up to 128 queries per pass over the panel."""
         ds, ix = [], []
         for i in range(0, Q.shape[0], 128):
-            d, j = K.knn_emb_search(self.E, Q[i:i + 128].contiguous(), k, self.norms)
+            d, j = K.knn_emb_search(self.Et, Q[i:i + 128].contiguous(), k, self.norms)
             ds.append(d)
             ix.append(j)
         return torch.cat(ds), torch.cat(ix)

@@ -47,7 +47,12 @@ def test_knn_emb_distance_kernel_vs_f64(N, Kd, Bq, splits):
     Q = torch.randn(Bq, Kd, device="cuda", generator=g).bfloat16()
     rn = K.knn_emb_norms(E)
     torch.testing.assert_close(rn.double(), (E.double() ** 2).sum(1), rtol=1e-5, atol=1e-3)
-    d = K.knn_emb_dist(E, Q, rn, splits=splits)
+    Et = K.knn_emb_pack(E)
+    # the packed layout: 4 KiB tiles [k-step 4][half 2][row 32][8 k], padding rows zero
+    assert Et.shape[0] == (N + 31) // 32 * 32
+    t = Et.view(-1, Kd // 64, 4, 2, 32, 8).permute(0, 4, 1, 2, 3, 5).reshape(-1, Kd)
+    assert torch.equal(t[:N], E) and not t[N:].any()
+    d = K.knn_emb_dist(Et, Q, rn, splits=splits)
     ref = _f64_dist(Q, E)
     # f32 accumulation over K terms of |q e| ~ 1: error ~ sqrt(K) * 2^-24 * scale; the norms
     # are ~K, so bound relative to them
