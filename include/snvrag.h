@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 25
+#define SNVRAG_ABI_VERSION 26
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -375,6 +375,25 @@ int snvrag_mlp_forward(int64_t M, int D, int epi2, const void* x, const void* ws
                        const float* r1, const float* r2, int64_t period, float eps, void* out, void* stream);
 size_t snvrag_sgemm_pack_bytes(int D, int N);
 int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
+
+/* Derived weight tensors of the training graph, all refreshed from the f32 master parameters
+ * in ONE launch after each optimizer step (the bf16 GEMM operands the kernels read: stream-GEMM
+ * packs, transposed / concatenated bf16 copies, f32 bias tables).  A job reads a source matrix
+ * of `rows` x `cols` f32 elements made of up to 4 parts stacked along the rows, part i being
+ * the strided view src[i][r * rs[i] + c * cs[i]] of part_rows[i] rows, and writes
+ *   kind 0: f32   dst[r * dst_ld + c]
+ *   kind 1: bf16  dst[r * dst_ld + c]   (round to nearest even, as the optimizer's bf16 mirror)
+ *   kind 2: bf16  snvrag_sgemm_pack of the (rows = N) x (cols = D) matrix (dst_ld unused).
+ * Job j owns the output pieces (8 elements) [piece0, piece0 + pieces); jobs sorted by piece0,
+ * piece0[0] = 0, total = the last job's piece0 + pieces.  `jobs` is a DEVICE pointer. */
+typedef struct {
+  int32_t kind, nparts;
+  int64_t rows, cols, dst_ld, piece0, pieces;
+  int64_t part_rows[4], rs[4], cs[4];
+  const float* src[4];
+  void* dst;
+} snvrag_derive_job_t;
+int snvrag_derive(const snvrag_derive_job_t* jobs, int njobs, int64_t total_pieces, void* stream);
 int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,
                          const void* wstream, const float* vec, const float* r1, const float* r2,
                          int64_t period, float eps, void* out, float* probs, float* logits, void* stream);

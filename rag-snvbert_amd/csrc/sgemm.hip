@@ -648,6 +648,49 @@ __global__ void sg_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w,
   for (int j = 0; j < 8; ++j) out[pc * 8 + j] = w[n * D + sg_in_feat(s, kh, j)];
 }
 
+// snvrag_derive (see the header): one thread per 8 output elements; its job by binary search
+// over the jobs' first pieces
+__global__ __launch_bounds__(256) void derive_kernel(const snvrag_derive_job_t* __restrict__ jobs, int njobs,
+                                                     long total) {
+  const long pc = (long)blockIdx.x * 256 + threadIdx.x;
+  if (pc >= total) return;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].piece0 <= pc) lo = mid;
+    else hi = mid - 1;
+  }
+  const snvrag_derive_job_t& J = jobs[lo];
+  const long p = pc - J.piece0;
+  auto src = [&](long r, long c) -> float {
+    int i = 0;
+    while (i < J.nparts - 1 && r >= J.part_rows[i]) { r -= J.part_rows[i]; ++i; }
+    return J.src[i][r * J.rs[i] + c * J.cs[i]];
+  };
+  if (J.kind == 2) {                                  // stream-GEMM pack (sg_pack_kernel's order)
+    const int D = (int)J.cols, KS = D / 16;
+    const long F = p / 64;
+    const int l = (int)(p % 64), m = l & 31, kh = l >> 5;
+    const long T = F / KS;
+    const int sidx = (int)(F % KS);
+    const long n = 32 * T + sg_out_feat(m);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)src(n, sg_in_feat(sidx, kh, j));
+    *reinterpret_cast<bf16x8*>((bf16*)J.dst + p * 8) = o;
+    return;
+  }
+  const long nel = J.rows * J.cols;
+  for (int j = 0; j < 8; ++j) {
+    const long e = p * 8 + j;
+    if (e >= nel) break;
+    const long r = e / J.cols, c = e % J.cols;
+    const float v = src(r, c);
+    if (J.kind == 0) ((float*)J.dst)[r * J.dst_ld + c] = v;
+    else ((bf16*)J.dst)[r * J.dst_ld + c] = (bf16)v;
+  }
+}
+
 template <int D, int EPI, int ACT, bool RANK, int WAVES = 4, bool CAT = false>
 static int sg_launch(SgArgs a, hipStream_t s) {
   auto kern = sg_kernel<D, EPI, ACT, RANK, WAVES, CAT>;
@@ -708,6 +751,15 @@ extern "C" int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* s
   const long pieces = (long)N * D / 8;
   hipLaunchKernelGGL(sg_pack_kernel, dim3((unsigned)cdiv(pieces, 256)), dim3(256), 0, as_stream(stream), D, pieces,
                      (const bf16*)w, (bf16*)out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_derive(const snvrag_derive_job_t* jobs, int njobs, int64_t total_pieces, void* stream) {
+  SNV_CHECK_ARG(jobs && njobs > 0 && total_pieces >= 0, "bad job table");
+  if (total_pieces == 0) return 0;
+  hipLaunchKernelGGL(derive_kernel, dim3((unsigned)cdiv(total_pieces, 256)), dim3(256), 0, as_stream(stream), jobs,
+                     njobs, (long)total_pieces);
   SNV_LAUNCH_CHECK();
   return 0;
 }

@@ -68,35 +68,107 @@ def bf16_of(p: torch.Tensor, transposed: bool = False) -> torch.Tensor:
     tied to the live base tensor (weakref identity, so a freed parameter's address reused by
     another can never hit) and to (its version, the optimizer epoch).  Parameters held in a
     FlatParams buffer read the optimizer's bf16 mirror directly."""
-    base, key = _base_key(p)
     if not transposed and p._base is None:
         mv = _MIRROR.get(id(p))
         if mv is not None and mv[0]() is p:
             return mv[1]
-    ent = _BF16.get(key)
-    ver = (base._version, _EPOCH[0])
-    if ent is None or ent[0]() is not base or ent[1] != ver:
-        mv = _MIRROR.get(id(p)) if p._base is None else None
-        val = mv[1] if (mv is not None and mv[0]() is p) else p.detach().to(torch.bfloat16).contiguous()
-        ent = [weakref.ref(base), ver, val, None]
-        _BF16[key] = ent
-    if not transposed:
-        return ent[2]
-    if ent[3] is None:
-        ent[3] = ent[2].t().contiguous()
-    return ent[3]
+    if p.dtype != torch.float32 or not p.is_cuda or p.dim() != 2:
+        base, key = _base_key(p)
+        ent = _BF16.get(key)
+        ver = (base._version, _EPOCH[0])
+        if ent is None or ent[0]() is not base or ent[1] != ver:
+            ent = [weakref.ref(base), ver, p.detach().to(torch.bfloat16).contiguous(), None]
+            _BF16[key] = ent
+        if not transposed:
+            return ent[2]
+        if ent[3] is None:
+            ent[3] = ent[2].t().contiguous()
+        return ent[3]
+    src = p.detach().t() if transposed else p.detach()
+    return _derived(("bf16", transposed), [p], lambda: _plain_job(K.DERIVE_BF16, [src]))
 
 
 def clear_weight_cache() -> None:
     _BF16.clear()
-    _SG.clear()
+    _DER.clear()
+    _DER_TABLE[0] = None
 
 
 def weights_updated() -> None:
-    """Called after a parameter update done outside torch's version tracking (HIP kernels)."""
+    """Called after a parameter update done outside torch's version tracking (HIP kernels):
+    every derived weight tensor is refreshed from the new master weights in one launch."""
     _EPOCH[0] += 1
     _BF16.clear()
-    _SG.clear()
+    _refresh_derived()
+
+
+# Derived weight tensors (stream-GEMM packs, transposed / concatenated bf16 copies, bias tables)
+# of f32 master parameters.  An entry is built once (buffers allocated, its jobs run at once)
+# and then REFRESHED IN PLACE: after every optimizer step all live entries are recomputed by
+# one snvrag_derive launch over a cached device job table (round 3 rebuilt each of them at its
+# first use in the step with fresh allocations, cats, transposes and one pack kernel apiece:
+# ~150 cat / ~70 pack / ~50 copy launches per training step).  A torch-side in-place update
+# (version bump) refreshes the entry at its next use; a moved or freed source drops it.
+class _Derived:
+    __slots__ = ("refs", "ptrs", "vers", "jobs", "out")
+
+
+_DER: Dict[tuple, _Derived] = {}
+_DER_TABLE = [None]                         # (device job table, njobs, pieces) over all of _DER
+
+
+def _parts_state(parts):
+    bases = [_base_key(t)[0] for t in parts]
+    return bases, tuple(b.data_ptr() for b in bases), tuple(b._version for b in bases)
+
+
+def _plain_job(kind, srcs, shape=None):
+    """(out, [job]): the f32 / bf16 row-major copy of the row-stacked f32 views ``srcs``."""
+    rows = sum(t.shape[0] for t in srcs)
+    cols = srcs[0].shape[1] if srcs[0].dim() == 2 else 1
+    dt = torch.float32 if kind == K.DERIVE_F32 else torch.bfloat16
+    out = torch.empty(shape or ((rows, cols) if srcs[0].dim() == 2 else (rows,)), device=srcs[0].device, dtype=dt)
+    return out, [K.derive_job(kind, [t.detach() for t in srcs], out)]
+
+
+def _derived(tag: tuple, parts, make):
+    """The derived tensor(s) ``make() -> (out, jobs)`` of the f32 parameters (or views) ``parts``,
+    current for their present values."""
+    keys = [_base_key(t)[1] for t in parts]
+    key = tag + tuple(keys)
+    bases, ptrs, vers = _parts_state(parts)
+    ent = _DER.get(key)
+    if ent is None or ent.ptrs != ptrs or any(r() is not b for r, b in zip(ent.refs, bases)):
+        ent = _Derived()
+        ent.out, ent.jobs = make()
+        ent.refs, ent.ptrs, ent.vers = [weakref.ref(b) for b in bases], ptrs, vers
+        _DER[key] = ent
+        _DER_TABLE[0] = None
+        K.derive(K.derive_table(ent.jobs, bases[0].device))
+    elif ent.vers != vers:
+        K.derive(K.derive_table(ent.jobs, bases[0].device))
+        ent.vers = vers
+    return ent.out
+
+
+def _refresh_derived() -> None:
+    dead = []
+    for key, ent in _DER.items():
+        bases = [r() for r in ent.refs]
+        if any(b is None for b in bases) or tuple(b.data_ptr() for b in bases) != ent.ptrs:
+            dead.append(key)
+        else:
+            ent.vers = tuple(b._version for b in bases)
+    for key in dead:
+        del _DER[key]
+        _DER_TABLE[0] = None
+    if not _DER:
+        return
+    if _DER_TABLE[0] is None:
+        jobs = [j for ent in _DER.values() for j in ent.jobs]
+        dev = next(iter(_DER.values())).refs[0]().device
+        _DER_TABLE[0] = K.derive_table(jobs, dev)
+    K.derive(_DER_TABLE[0])
 
 
 def register_mirror(p: torch.Tensor, view: torch.Tensor) -> None:
@@ -133,59 +205,55 @@ def tiny_embedding(tok: torch.Tensor, W: torch.Tensor, padding_idx: Optional[int
     return _TinyVocabEmbedding.apply(tok, W, padding_idx)
 
 
-_SG: Dict[tuple, list] = {}
+def _sg_stream(ws, bs, n_out: int, extra=()):
+    """(packed weight stream, f32 vector table) of the stream GEMM (csrc/sgemm.hip) for the
+    weights ``ws`` (f32 [n_i, K] parameters or views, concatenated along the outputs) and biases
+    ``bs`` (+ ``extra`` f32 columns appended to the table: the rank-2 linear's W[:, D], W[:, D+1])."""
+    parts = list(ws) + [b for b in bs if b is not None] + list(extra)
+
+    def make():
+        Kd = ws[0].shape[1]
+        packed = torch.empty(int(K.N.lib().snvrag_sgemm_pack_bytes(Kd, n_out)), device=ws[0].device,
+                             dtype=torch.uint8)
+        jobs = [K.derive_job(K.DERIVE_SGPACK, [w.detach() for w in ws], packed)]
+        if bs[0] is None and not extra:
+            vec = torch.zeros(n_out, device=ws[0].device, dtype=torch.float32)
+        else:
+            vec, vj = _plain_job(K.DERIVE_F32, [t.detach().reshape(-1) for t in bs if t is not None] +
+                                 [t.detach() for t in extra])
+            jobs += vj
+        return (packed, vec), jobs
+    return _derived(("sg", len(extra)), parts, make)
 
 
-def _sg_stream(ws, bs, n_out: int):
-    """(packed weight stream, f32 bias table) of the stream GEMM (csrc/sgemm.hip) for the
-    concatenated weights ``ws`` / biases ``bs``, cached per (parameter identity, version,
-    optimizer epoch) — repacked once per optimizer step."""
-    keys, bases = [], []
-    for t in list(ws) + [b for b in bs if b is not None]:
-        base, key = _base_key(t)
-        keys.append(key)
-        bases.append(base)
-    key = tuple(keys)
-    ver = (tuple(b._version for b in bases), _EPOCH[0])
-    ent = _SG.get(key)
-    if ent is None or any(r() is not b for r, b in zip(ent[0], bases)) or ent[1] != ver:
-        w = bf16_of(ws[0]) if len(ws) == 1 else torch.cat([bf16_of(t) for t in ws], 0)
-        b = torch.cat([t.detach().float().reshape(-1) for t in bs]) if bs[0] is not None else \
-            torch.zeros(n_out, device=w.device, dtype=torch.float32)
-        ent = [[weakref.ref(x) for x in bases], ver, K.sgemm_pack(w), K.sgemm_vec(b)]
-        _SG[key] = ent
-    return ent[2], ent[3]
+def _cat_bf16(ws, transposed: bool = False) -> torch.Tensor:
+    """bf16 cat(ws, 0) (or its transpose) of f32 weights, refreshed with the derived tensors."""
+    def make():
+        rows, cols = sum(w.shape[0] for w in ws), ws[0].shape[1]
+        if not transposed:
+            return _plain_job(K.DERIVE_BF16, list(ws))
+        out = torch.empty(cols, rows, device=ws[0].device, dtype=torch.bfloat16)
+        jobs, off = [], 0
+        for w in ws:                                # column block of the transposed output
+            jobs.append(K.derive_job(K.DERIVE_BF16, [w.detach().t()], out.view(-1)[off:], dst_ld=rows))
+            off += w.shape[0]
+        return out, jobs
+    return _derived(("catT" if transposed else "cat",), list(ws), make)
 
 
-def _cached(tag: str, ts, make):
-    """``make()`` cached per (tag, the tensors' identities, their versions, the optimizer epoch),
-    like the packed streams: the concatenated QKV weights / biases of the row-panel GEMM path are
-    built once per optimizer step instead of by a cat kernel at every call."""
-    keys, bases = [], []
-    for t in ts:
-        base, key = _base_key(t)
-        keys.append(key)
-        bases.append(base)
-    key = (tag,) + tuple(keys)
-    ver = (tuple(b._version for b in bases), _EPOCH[0])
-    ent = _SG.get(key)
-    if ent is None or any(r() is not b for r, b in zip(ent[0], bases)) or ent[1] != ver:
-        ent = [[weakref.ref(b) for b in bases], ver, make()]
-        _SG[key] = ent
-    return ent[2]
+def _cat_f32(bs) -> torch.Tensor:
+    return _derived(("bcat",), list(bs), lambda: _plain_job(K.DERIVE_F32, [t.detach().reshape(-1) for t in bs]))
 
 
 def _sg_stream_t(w: torch.Tensor, n_out: int):
     """Packed stream of W^T (the dX = dY W GEMM of a single Linear with out_features = 384)."""
-    base, key = _base_key(w)
-    key = ("T",) + key
-    ver = (base._version, _EPOCH[0])
-    ent = _SG.get(key)
-    if ent is None or ent[0][0]() is not base or ent[1] != ver:
-        ent = [[weakref.ref(base)], ver, K.sgemm_pack(bf16_of(w, transposed=True)),
-               torch.zeros(n_out, device=w.device, dtype=torch.float32)]
-        _SG[key] = ent
-    return ent[2], ent[3]
+    def make():
+        wt = w.detach().t()
+        packed = torch.empty(int(K.N.lib().snvrag_sgemm_pack_bytes(wt.shape[1], wt.shape[0])), device=w.device,
+                             dtype=torch.uint8)
+        return (packed, torch.zeros(n_out, device=w.device, dtype=torch.float32)), \
+            [K.derive_job(K.DERIVE_SGPACK, [wt], packed)]
+    return _derived(("sgT",), [w], make)
 
 
 def _sg_ok(x2: torch.Tensor, n_out: int) -> bool:
@@ -267,9 +335,8 @@ class _HipLinear(torch.autograd.Function):
             wsp, vec = _sg_stream(ws, bs, n_out)
             y = K.sgemm(x2, wsp, n_out, vec)
         else:
-            w = bf16_of(ws[0]) if n == 1 else _cached("wcat", ws, lambda: torch.cat([bf16_of(t) for t in ws], 0))
-            b = _cached("bcat", bs, lambda: torch.cat([t.detach().float().reshape(-1) for t in bs]).contiguous()) \
-                if has_b else None
+            w = bf16_of(ws[0]) if n == 1 else _cat_bf16(ws)
+            b = (bs[0].detach() if n == 1 else _cat_f32(bs)) if has_b else None
             y = K.linear(x2, w, b)
         ctx.save_for_backward(x2, *ws)
         ctx.n, ctx.has_bias = n, has_b
@@ -309,8 +376,7 @@ class _HipLinear(torch.autograd.Function):
                 wsp, vec = _sg_stream_t(ws[0], n_in)
                 gx = K.sgemm(g2, wsp, n_in, vec)
             else:
-                wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else \
-                    _cached("wcatT", ws, lambda: torch.cat([bf16_of(t) for t in ws], 0).t().contiguous())
+                wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else _cat_bf16(ws, transposed=True)
                 gx = K.linear(g2, wt)
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
         n_all, k_in = g2.shape[1], x2.shape[1]
@@ -396,8 +462,7 @@ class _HipLinearRank2(torch.autograd.Function):
         r1 = c1.reshape(-1).float().contiguous()
         r2 = c2.reshape(-1).float().contiguous()
         assert r1.numel() == M and r2.numel() == M
-        wsp, _ = _sg_stream([W[:, :D]], [b], n_out)
-        vec = K.sgemm_vec(b, W[:, D], W[:, D + 1])                   # [bias | w_c1 | w_c2]
+        wsp, vec = _sg_stream([W[:, :D]], [b], n_out, extra=(W[:, D], W[:, D + 1]))   # [bias | w_c1 | w_c2]
         z = K.sgemm(x2, wsp, n_out, vec, rank=(r1, r2, M))
         ctx.save_for_backward(x2, r1, r2, W)
         ctx.in_shape, ctx.in_dtype, ctx.D = x.shape, x.dtype, D

@@ -741,6 +741,52 @@ def sgemm_pack(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+DERIVE_F32, DERIVE_BF16, DERIVE_SGPACK = 0, 1, 2
+
+
+def derive_job(kind: int, parts, dst: torch.Tensor, dst_ld: int = 0) -> "N.DeriveJob":
+    """One snvrag_derive job: ``parts`` = f32 2-D (strided) views stacked along their rows (1-D
+    views count as columns [n, 1]); ``dst`` receives kind DERIVE_F32 / DERIVE_BF16 (row-major with
+    row stride ``dst_ld``, default the column count) or DERIVE_SGPACK (the stream-GEMM pack of the
+    [N, D] matrix).  piece0 / pieces are filled by ``derive_table``."""
+    assert 1 <= len(parts) <= 4
+    views = [t.unsqueeze(1) if t.dim() == 1 else t for t in parts]
+    cols = views[0].shape[1]
+    assert all(v.dim() == 2 and v.shape[1] == cols and v.dtype == torch.float32 and v.is_cuda for v in views)
+    j = N.DeriveJob()
+    j.kind, j.nparts = kind, len(views)
+    j.rows, j.cols = sum(v.shape[0] for v in views), cols
+    j.dst_ld = dst_ld or cols
+    for i, v in enumerate(views):
+        j.part_rows[i], j.rs[i], j.cs[i], j.src[i] = v.shape[0], v.stride(0), v.stride(1), v.data_ptr()
+    if kind == DERIVE_SGPACK:
+        assert int(N.lib().snvrag_sgemm_pack_bytes(cols, j.rows)) == dst.numel() * dst.element_size()
+        j.pieces = j.rows * cols // 8
+    else:
+        assert dst.dtype == (torch.float32 if kind == DERIVE_F32 else torch.bfloat16)
+        assert (j.rows - 1) * j.dst_ld + cols <= dst.numel()
+        j.pieces = (j.rows * cols + 7) // 8
+    j.dst = dst.data_ptr()
+    return j
+
+
+def derive_table(jobs, device) -> Tuple[torch.Tensor, int, int]:
+    """(device job table, job count, total pieces) for :func:`derive`."""
+    total = 0
+    for j in jobs:
+        j.piece0 = total
+        total += j.pieces
+    arr = (N.DeriveJob * len(jobs))(*jobs)
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(device), len(jobs), total
+
+
+def derive(table: Tuple[torch.Tensor, int, int]) -> None:
+    """Run every job of a :func:`derive_table` in one launch (csrc/sgemm.hip derive_kernel)."""
+    t, n, total = table
+    check(N.lib().snvrag_derive(ptr(t), n, total, stream_ptr()), "derive")
+
+
 def sgemm_vec(bias: torch.Tensor, c1: Optional[torch.Tensor] = None, c2: Optional[torch.Tensor] = None,
               ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
               head: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:

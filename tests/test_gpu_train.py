@@ -1158,3 +1158,47 @@ def test_stream_gemm_repacks_after_optimizer_step():
     opt.step()
     assert (lin.weight.detach() - before).abs().max().item() > 1e-3     # the weights moved
     check()
+
+
+def test_derived_weights_refresh_in_one_launch():
+    """Stream-GEMM packs, transposed / concatenated bf16 copies and bias tables of f32 master
+    weights (autograd_ops' derived registry, csrc/sgemm.hip derive_kernel) equal the torch
+    formulas they replace — at creation, after an optimizer-style raw update + weights_updated()
+    (one refresh launch for all), and after a torch in-place update (refreshed at next use)."""
+    from src import autograd_ops as A
+    from src import kernels as K
+    g = torch.Generator(device="cpu").manual_seed(11)
+    q, k, v = (torch.nn.Parameter(torch.randn(384, 384, generator=g).to(DEV)) for _ in range(3))
+    bq, bk, bv = (torch.nn.Parameter(torch.randn(384, generator=g).to(DEV)) for _ in range(3))
+    W = torch.nn.Parameter(torch.randn(1536, 386, generator=g).to(DEV))     # rank-2 layer [W | c1 c2]
+    b = torch.nn.Parameter(torch.randn(1536, generator=g).to(DEV))
+    A.clear_weight_cache()
+
+    def check():
+        bf = lambda t: t.detach().to(torch.bfloat16)
+        pk, vec = A._sg_stream([q, k, v], [bq, bk, bv], 1152)
+        assert torch.equal(pk, K.sgemm_pack(torch.cat([bf(q), bf(k), bf(v)])))
+        assert torch.equal(vec, torch.cat([bq, bk, bv]).detach())
+        pk2, vec2 = A._sg_stream([W[:, :384]], [b], 1536, extra=(W[:, 384], W[:, 385]))
+        assert torch.equal(pk2, K.sgemm_pack(bf(W[:, :384]).contiguous()))
+        assert torch.equal(vec2, torch.cat([b, W[:, 384], W[:, 385]]).detach())
+        pt, z = A._sg_stream_t(q, 384)
+        assert torch.equal(pt, K.sgemm_pack(bf(q).t().contiguous())) and not z.any()
+        assert torch.equal(A._cat_bf16([q, k, v]), torch.cat([bf(q), bf(k), bf(v)]))
+        assert torch.equal(A._cat_bf16([q, k, v], transposed=True), torch.cat([bf(q), bf(k), bf(v)]).t())
+        assert torch.equal(A._cat_f32([bq, bk, bv]), torch.cat([bq, bk, bv]).detach())
+        assert torch.equal(A.bf16_of(W[:, :384]), bf(W[:, :384]))
+        assert torch.equal(A.bf16_of(q, transposed=True), bf(q).t())
+
+    check()
+    n0 = len(A._DER)
+    for t in (q, k, v, bq, bk, bv, W, b):          # a raw update (no version bump), like FusedAdam
+        t.data.add_(0.25)
+    A.weights_updated()
+    assert len(A._DER) == n0
+    check()
+    with torch.no_grad():                            # a torch update: version bump, refreshed at use
+        k.mul_(-1.5)
+        W.add_(1.0)
+    check()
+    A.clear_weight_cache()

@@ -38,3 +38,16 @@ rows.sort(key=lambda e: -e.device_time_total)
 print("\nATen ops by device time (ms per step, calls per step, shapes)")
 for e in rows[:60]:
     print(f"{e.device_time_total / 3e3:8.3f} ms {e.count / 3:6.1f}  {e.key:28s} {str(e.input_shapes)[:110]}")
+
+if os.environ.get("STACKS"):
+    # where the small glue ops come from: the Python stacks of the top ATen callers
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof2:
+        tr.train_step(dict(batch))
+        torch.cuda.synchronize()
+    want = {"aten::cat", "aten::zeros", "aten::copy_", "aten::add_", "aten::_to_copy", "aten::clone", "aten::fill_"}
+    rows = [e for e in prof2.key_averages(group_by_stack_n=6) if e.key in want]
+    rows.sort(key=lambda e: -e.device_time_total)
+    print("\nGlue ops by Python stack (one step: device ms, calls)")
+    for e in rows[:40]:
+        st = " <- ".join(s.split("/")[-1] for s in e.stack[:6] if "torch/" not in s)
+        print(f"{e.device_time_total / 1e3:7.3f} ms {e.count:4d}  {e.key:16s} {st[:230]}")
