@@ -315,13 +315,34 @@ def _grad_buffer(p) -> Optional[torch.Tensor]:
     return g if (g is not None and g.dtype == torch.float32 and g.is_contiguous()) else None
 
 
+class GradHandoff:
+    """A gradient handed from one backward to another instead of through autograd's accumulation.
+
+    In a transformer block the stream tensor x feeds both the next GEMM (the q/k/v projection, or
+    FeedForward's w_1) and the add+LayerNorm that closes the sublayer (sublayer.py:15-16:
+    norm(x + sublayer(x))).  Autograd would receive x's gradient twice and add the two [M, D]
+    tensors with one more elementwise kernel per sublayer (24 per step at d384/L12).  With a
+    handoff, the add+LayerNorm backward (which runs first: its other operand depends on the GEMM)
+    deposits its dx here and returns no gradient for x, and the GEMM's dX backward adds it in its
+    epilogue (the row-panel GEMM's residual operand: one f32 accumulate + one bf16 rounding)."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+    def take(self) -> Optional[torch.Tensor]:
+        g, self.g = self.g, None
+        return g
+
+
 class _HipLinear(torch.autograd.Function):
     """y = x [W_1; ..; W_n]^T + [b_1; ..; b_n]: one GEMM over weights concatenated along the
     output dim (the q/k/v Linear layers of multi_head_attention.py:44 as one N = 3D GEMM)."""
 
     @staticmethod
-    def forward(ctx, x, n, *wb):
+    def forward(ctx, x, n, handoff, *wb):
         ws, bs = wb[:n], wb[n:]
+        ctx.handoff = handoff
         Kd = x.shape[-1]
         if train_dtype() == torch.float32:
             return _HipLinear._forward_f32(ctx, x, n, ws, bs)
@@ -370,14 +391,17 @@ class _HipLinear(torch.autograd.Function):
         gx = None
         gws = [None] * ctx.n
         gbs = [None] * ctx.n
+        res = ctx.handoff.take() if ctx.handoff is not None else None
         if ctx.needs_input_grad[0]:
             n_in = ctx.in_shape[-1]
             if ctx.n == 1 and _sg_ok(g2, n_in):
                 wsp, vec = _sg_stream_t(ws[0], n_in)
                 gx = K.sgemm(g2, wsp, n_in, vec)
+                if res is not None:
+                    gx += res.reshape(gx.shape).to(gx.dtype)
             else:
                 wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else _cat_bf16(ws, transposed=True)
-                gx = K.linear(g2, wt)
+                gx = K.linear(g2, wt, resid=None if res is None else res.reshape(-1, n_in).to(torch.bfloat16))
             gx = gx.reshape(ctx.in_shape).to(ctx.in_dtype)
         n_all, k_in = g2.shape[1], x2.shape[1]
         dw_ok = n_all % 128 == 0 and k_in % 128 == 0 and all(sz % 128 == 0 for sz in sizes) and \
@@ -396,21 +420,21 @@ class _HipLinear(torch.autograd.Function):
                 for w, b, sz in zip(pws, pbs, sizes):
                     K.linear_dw(g2[:, off:off + sz], x2, dw=w.grad, db=b.grad if ctx.has_bias else None)
                     off += sz
-            return (gx, None, *([None] * ctx.n), *([None] * ctx.n))
-        if any(ctx.needs_input_grad[2:2 + ctx.n]) and dw_ok:
+            return (gx, None, None, *([None] * ctx.n), *([None] * ctx.n))
+        if any(ctx.needs_input_grad[3:3 + ctx.n]) and dw_ok:
             # dW (and db) on the split-M MFMA kernel (csrc/dw.hip), f32 accumulation and result
             gw, gb = K.linear_dw(g2, x2, bias=ctx.has_bias)
             gws = list(torch.split(gw, sizes, 0))
             if ctx.has_bias:
                 gbs = list(torch.split(gb, sizes, 0))
-            return (gx, None, *gws, *gbs)
-        if any(ctx.needs_input_grad[2:2 + ctx.n]):
+            return (gx, None, None, *gws, *gbs)
+        if any(ctx.needs_input_grad[3:3 + ctx.n]):
             gw = _mm_f32(g2.t(), x2)
             gws = list(torch.split(gw, sizes, 0))
         if ctx.has_bias:
             gb = K.colsum(g2) if g2.shape[-1] % 8 == 0 and g2.shape[-1] <= 2048 else g2.float().sum(0)
             gbs = list(torch.split(gb, sizes, 0))
-        return (gx, None, *gws, *gbs)
+        return (gx, None, None, *gws, *gbs)
 
 
 def _hip_linear_backward_f32(ctx, gy):
@@ -421,28 +445,34 @@ def _hip_linear_backward_f32(ctx, gy):
     if ctx.needs_input_grad[0]:
         wt = torch.cat([t.detach().float() for t in ws], 0).t().contiguous()
         gx = K.linear(g2, wt).reshape(ctx.in_shape).to(ctx.in_dtype)
-    gws = list(torch.split(g2.t() @ x2, sizes, 0)) if any(ctx.needs_input_grad[2:2 + ctx.n]) else [None] * ctx.n
+    res = ctx.handoff.take() if ctx.handoff is not None else None
+    if res is not None and gx is not None:
+        gx = gx + res.to(gx.dtype)
+    gws = list(torch.split(g2.t() @ x2, sizes, 0)) if any(ctx.needs_input_grad[3:3 + ctx.n]) else [None] * ctx.n
     gbs = list(torch.split(g2.sum(0), sizes, 0)) if ctx.has_bias else [None] * ctx.n
-    return (gx, None, *gws, *gbs)
+    return (gx, None, None, *gws, *gbs)
 
 
 _HipLinear._backward_f32 = staticmethod(_hip_linear_backward_f32)
 
 
-def hip_linear(x: torch.Tensor, weight, bias=None) -> torch.Tensor:
+def hip_linear(x: torch.Tensor, weight, bias=None, grad_from: Optional[GradHandoff] = None) -> torch.Tensor:
     """nn.Linear on the MFMA kernels; bf16 activations in and out.  ``weight``/``bias`` may be
-    lists (layers sharing the input, fused along the output dim)."""
+    lists (layers sharing the input, fused along the output dim).  ``grad_from``: x's other
+    gradient, deposited by an add+LayerNorm backward (:class:`GradHandoff`), joins dX."""
     ws = list(weight) if isinstance(weight, (list, tuple)) else [weight]
     bs = list(bias) if isinstance(bias, (list, tuple)) else [bias] * len(ws)
     Kd, Nn = ws[0].shape[1], sum(t.shape[0] for t in ws)
     if Kd % 8 or Nn % 8:
         if train_dtype() == torch.float32:
+            assert grad_from is None, "a gradient handoff needs the HIP Linear path"
             b = torch.cat(bs, 0) if bs[0] is not None else None
             return torch.nn.functional.linear(x.float(), torch.cat(ws, 0), b)
         w = torch.cat(ws, 0).to(torch.bfloat16)
         b = torch.cat(bs, 0).to(torch.bfloat16) if bs[0] is not None else None
+        assert grad_from is None, "a gradient handoff needs the HIP Linear path"
         return torch.nn.functional.linear(x.to(torch.bfloat16), w, b)
-    return _HipLinear.apply(x, len(ws), *ws, *bs)
+    return _HipLinear.apply(x, len(ws), grad_from, *ws, *bs)
 
 
 class _HipLinearRank2(torch.autograd.Function):
@@ -554,7 +584,8 @@ class _HipAddLayerNorm(torch.autograd.Function):
     the backward)."""
 
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, p_r, p_out, seed, slope_x=0.0, slope_r=0.0):
+    def forward(ctx, x, r, weight, bias, eps, p_r, p_out, seed, slope_x=0.0, slope_r=0.0, handoff=None):
+        ctx.handoff = handoff
         x = x.to(torch.bfloat16).contiguous()
         r = r.to(torch.bfloat16).contiguous() if r is not None else None
         y, s, stats = K.ln_fwd_train(x, r, weight.detach().float().contiguous(),
@@ -580,9 +611,12 @@ class _HipAddLayerNorm(torch.autograd.Function):
                                     p_r, p_out, seed, dg=w.grad if direct else None, db=b.grad if direct else None,
                                     slope_x=slope_x, slope_r=slope_r, r_pre=rp[0] if rp else None)
         dr = (dres if dres is not None else ds) if ctx.has_r else None
+        dx = ds
+        if ctx.handoff is not None and ctx.needs_input_grad[0]:
+            ctx.handoff.g, dx = ds, None             # x's other consumer adds it (GradHandoff)
         if direct:
-            return ds, dr, None, None, None, None, None, None, None, None
-        return ds, dr, dg, db, None, None, None, None, None, None
+            return dx, dr, None, None, None, None, None, None, None, None, None
+        return dx, dr, dg, db, None, None, None, None, None, None, None
 
 
 def _drop_seed() -> int:
@@ -590,12 +624,15 @@ def _drop_seed() -> int:
 
 
 def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln, p_r: float = 0.0,
-                      p_out: float = 0.0, act_x: float = 0.0, act_r: float = 0.0) -> torch.Tensor:
+                      p_out: float = 0.0, act_x: float = 0.0, act_r: float = 0.0,
+                      grad_to: Optional[GradHandoff] = None) -> torch.Tensor:
     """bf16 drop_o(LayerNorm(lrelu_x(x) + drop_r(lrelu_r(r)))) with the parameters of nn.LayerNorm
     ``ln`` (N % 8 == 0, N <= 2048); p_r / p_out: dropout on the residual operand / the output
     (training; the masks are a counter-based hash of a seed from torch's RNG); act_x / act_r:
-    LeakyReLU slopes (0: none) fused into the norm (act_x only without a residual).  f32 parity
-    mode: torch's f32 LeakyReLU, LayerNorm and F.dropout."""
+    LeakyReLU slopes (0: none) fused into the norm (act_x only without a residual).  ``grad_to``:
+    x's gradient is handed to x's other consumer (a ``hip_linear(x, ..., grad_from=...)`` upstream
+    of ``r``) instead of being returned.  f32 parity mode: torch's f32 LeakyReLU, LayerNorm and
+    F.dropout (no handoff: autograd adds the gradients)."""
     if train_dtype() == torch.float32:
         xx = torch.nn.functional.leaky_relu(x.float(), act_x) if act_x else x.float()
         rr = r.float() if r is not None else None
@@ -608,8 +645,9 @@ def hip_add_layernorm(x: torch.Tensor, r: Optional[torch.Tensor], ln, p_r: float
         return torch.nn.functional.dropout(y, p_out, True) if p_out > 0 else y
     assert not (act_x and r is not None), "act_x is for a norm without a residual"
     seed = _drop_seed() if (p_r > 0 or p_out > 0) else 0
+    assert grad_to is None or (r is not None and not act_x), "the handoff is for x of LN(x + r)"
     return _HipAddLayerNorm.apply(x, r, ln.weight, ln.bias, ln.eps, float(p_r), float(p_out), seed,
-                                  float(act_x), float(act_r))
+                                  float(act_x), float(act_r), grad_to)
 
 
 class _HipAttention(torch.autograd.Function):

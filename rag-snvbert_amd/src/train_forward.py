@@ -38,8 +38,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import (hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2, nbr_mean_drop,
-                           rag_mean_train, tiny_embedding, train_dtype)
+from .autograd_ops import (GradHandoff, hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2,
+                           nbr_mean_drop, rag_mean_train, tiny_embedding, train_dtype)
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -159,8 +159,11 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     a = blk.attention
     D = x.shape[-1]
     ll = a.linear_layers
+    # x feeds the q/k/v GEMM and the sublayer's add+LayerNorm: the norm's dx is handed to the GEMM's
+    # dX epilogue instead of autograd adding the two gradients (autograd_ops.GradHandoff)
+    h_attn, h_ffn = GradHandoff(), GradHandoff()
     qkv = hip_linear(x.reshape(-1, D), [ll[0].weight, ll[1].weight, ll[2].weight],
-                     [ll[0].bias, ll[1].bias, ll[2].bias])
+                     [ll[0].bias, ll[1].bias, ll[2].bias], grad_from=h_attn)
     # attention-probability dropout (attention.py:28-29), counter-based mask shared with the backward
     att = hip_attention(qkv, nseq, L, a.heads, a.dims, a.dropout.p if training else 0.0)
     o = hip_linear(att, a.output_layer.weight, a.output_layer.bias).reshape(x.shape)
@@ -170,13 +173,14 @@ def transformer_block(blk, x: torch.Tensor, nseq: int, L: int, p: float, trainin
     # dropout (transformer.py:35) folded into the output sublayer's: two independent keep masks
     # in a row are one Bernoulli((1 - p)^2) mask scaled by 1 / (1 - p)^2
     po = p if training else 0.0
-    x = hip_add_layernorm(x, o, blk.input_sublayer.norm, p_out=po)
+    x = hip_add_layernorm(x, o, blk.input_sublayer.norm, p_out=po, grad_to=h_attn)
     ff = blk.feed_forward
     # feed_forward.py:20-21: both LeakyReLUs run inside the LayerNorm kernels (w_1's on the FFN
     # norm's input, w_2's on the output sublayer's residual operand, before its dropout)
-    h = hip_linear(x, ff.w_1.weight, ff.w_1.bias)
+    h = hip_linear(x, ff.w_1.weight, ff.w_1.bias, grad_from=h_ffn)
     f = hip_linear(hip_add_layernorm(h, None, ff.norm, act_x=0.1), ff.w_2.weight, ff.w_2.bias)
-    return hip_add_layernorm(x, f, blk.output_sublayer.norm, p_r=po, p_out=1.0 - (1.0 - po) ** 2, act_r=0.1)
+    return hip_add_layernorm(x, f, blk.output_sublayer.norm, p_r=po, p_out=1.0 - (1.0 - po) ** 2, act_r=0.1,
+                             grad_to=h_ffn)
 
 
 @dataclass

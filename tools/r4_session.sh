@@ -26,7 +26,7 @@ for s in ${STEPS:-new attn bench}; do
     attn)  step attn_only 240 env REPS=8 ROUNDS=3 ATTN_VARIANTS=${ATTN_VARIANTS:-0} python tools/attn_only.py
            step train_attn 200 python tools/train_attn_micro.py ;;
     pmc)   step attn_pmc 300 env TAG=${TAG}_attn bash tools/pmc_attn.sh ;;
-    stacks) step train_stacks 400 env STACKS=1 python tools/train_torchprof.py ;;
+    stacks) step train_stacks 400 python tools/train_dispatch_log.py ;;
     tprof) step train_torchprof 400 python tools/train_torchprof.py
            step train_only 300 python tools/train_only.py ;;
     c2)    step knn_emb_micro 300 python tools/knn_emb_micro.py ;;

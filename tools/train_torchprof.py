@@ -45,9 +45,9 @@ if os.environ.get("STACKS"):
         tr.train_step(dict(batch))
         torch.cuda.synchronize()
     want = {"aten::cat", "aten::zeros", "aten::copy_", "aten::add_", "aten::_to_copy", "aten::clone", "aten::fill_"}
-    rows = [e for e in prof2.key_averages(group_by_stack_n=6) if e.key in want]
+    rows = [e for e in prof2.key_averages(group_by_input_shape=True, group_by_stack_n=6) if e.key in want]
     rows.sort(key=lambda e: -e.device_time_total)
     print("\nGlue ops by Python stack (one step: device ms, calls)")
     for e in rows[:40]:
-        st = " <- ".join(s.split("/")[-1] for s in e.stack[:6] if "torch/" not in s)
-        print(f"{e.device_time_total / 1e3:7.3f} ms {e.count:4d}  {e.key:16s} {st[:230]}")
+        st = " <- ".join(s.split("/")[-1] for s in e.stack[:6]) or "(no Python stack: autograd engine)"
+        print(f"{e.device_time_total / 1e3:7.3f} ms {e.count:4d}  {e.key:16s} {str(e.input_shapes)[:60]} {st[:260]}")
