@@ -396,10 +396,10 @@ class _TrainFlops:
         self.tf, self.flops = tf, 0
         self.saved = (tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention)
 
-        def lin(x, weight, bias=None):
+        def lin(x, weight, bias=None, **kw):
             n = sum(w.shape[0] for w in weight) if isinstance(weight, (list, tuple)) else weight.shape[0]
             self.flops += 6 * (x.numel() // x.shape[-1]) * x.shape[-1] * n
-            return self.saved[0](x, weight, bias)
+            return self.saved[0](x, weight, bias, **kw)
 
         def lin2(x, ln, c1, c2):
             self.flops += 6 * (x.numel() // x.shape[-1]) * ln.weight.shape[1] * ln.weight.shape[0]

@@ -161,3 +161,29 @@ def test_attention_dropout_mask_statistics(p):
     assert abs(cond(m[..., :, :-2], m[..., :, 2:]) - p) < tol    # neighbouring hashes
     assert abs(cond(m[:, 0], m[:, 1]) - p) < tol               # heads
     assert abs(cond(m[0], m[1]) - p) < tol                     # sequences
+
+
+def test_bench_flop_counter_wraps_the_train_graph_signatures():
+    """bench.py's _TrainFlops replaces train_forward's hip_linear / hip_linear_rank2 /
+    hip_attention while it counts FLOP: every keyword the train graph passes them must reach the
+    real functions (a wrapper without ``grad_from`` broke the bench's training leg)."""
+    import importlib.util
+    import sys
+    import torch
+    sys.path.insert(0, str(REPO / "rag-snvbert_amd"))
+    from src import train_forward as tf
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    seen = {}
+    real = (tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention)
+    tf.hip_linear = lambda x, w, b=None, **kw: seen.setdefault("lin", kw) and None
+    tf.hip_linear_rank2 = lambda x, ln, c1, c2: None
+    tf.hip_attention = lambda *a, **kw: None
+    try:
+        with bench._TrainFlops() as fl:
+            w = torch.zeros(8, 4)
+            tf.hip_linear(torch.zeros(2, 4), [w, w], [None, None], grad_from="h")
+        assert seen["lin"] == {"grad_from": "h"} and fl.flops == 6 * 2 * 4 * 16
+    finally:
+        tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention = real

@@ -25,6 +25,7 @@ for s in ${STEPS:-new attn bench}; do
     attnt) step pytest_attn 400 $PT tests/test_gpu_kernels.py tests/test_gpu_train.py -k "attention or attn" ;;
     attn)  step attn_only 240 env REPS=8 ROUNDS=3 ATTN_VARIANTS=${ATTN_VARIANTS:-0} python tools/attn_only.py
            step train_attn 200 python tools/train_attn_micro.py ;;
+    traffic) step pmc_traffic 900 bash tools/pmc.sh ;;
     pmc)   step attn_pmc 300 env TAG=${TAG}_attn bash tools/pmc_attn.sh ;;
     stacks) step train_stacks 400 python tools/train_dispatch_log.py ;;
     tprof) step train_torchprof 400 python tools/train_torchprof.py
