@@ -70,6 +70,7 @@ struct Options {
   int64_t ln_bwd_nopf;     // 1: LayerNorm backward without the next-row prefetch (A/B)
   int64_t attn_variant;    // inference attention (dh 32) A/B variant, 0 = default (attention.hip tile)
   int64_t dw_xcd;          // 1: dW workgroups of one M chunk dealt to one XCD (0: plain grid order, A/B)
+  int64_t ln_rows1;        // 1: training LayerNorm forward one row per wave also at N <= 512 (A/B)
 };
 Options& options();
 

@@ -459,6 +459,85 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long M, int N, int rows_per
   }
 }
 
+// ---- forward on 16-lane row groups (N = 128 .. 512, the d384 model's N = 384): a wave
+// normalises four rows at once, 16 lanes per row, NCH 8-column chunks per lane.  One row per wave
+// left 16 of 64 lanes idle at N = 384 (48 chunks) and paid two 6-step wave reductions per row;
+// here every lane works and the reductions are 4-step xor shuffles inside the group
+// (tools/ln_micro.py, M = 49 440: 32.7 -> 28.2 us with residual dropout, 21.7 -> 17.6 us plain).
+__device__ __forceinline__ float gsum16(float v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_train_g16(long M, int N, const bf16* __restrict__ x,
+                                                        const bf16* __restrict__ r, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float eps,
+                                                        bf16* __restrict__ y, bf16* __restrict__ s_out,
+                                                        float2* __restrict__ stats, LnDrop dr) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15;
+  const long m = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+  const bool ok = m < M;
+  const long mm = ok ? m : M - 1;                     // loads clamped, stores guarded
+  float v[NCH][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int cc = l16 + 16 * c;
+    ld8bf(x + mm * N + 8 * cc, v[c]);
+    if (dr.sl_x != 0.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)ln_lrelu(v[c][j], dr.sl_x);
+    }
+    if (r) {
+      float t[8];
+      ld8bf(r + mm * N + 8 * cc, t);
+      if (dr.sl_r != 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = (float)(bf16)ln_lrelu(t[j], dr.sl_r);
+      }
+      if (dr.th_r) {
+        float mk[8];
+        ln_drop8(dr.base_r, dr.th_r, dr.sc_r, mm, cc, mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] *= mk[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)(v[c][j] + t[j]);   // s is kept in bf16
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += v[c][j];
+  }
+  const float mean = gsum16(sum) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; q += d * d; }
+  const float rstd = 1.0f / sqrtf(gsum16(q) / N + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int cc = l16 + 16 * c;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * g[8 * cc + j] + b[8 * cc + j];
+    if (dr.th_o) {
+      float mk[8];
+      ln_drop8(dr.base_o, dr.th_o, dr.sc_o, mm, cc, mk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] *= mk[j];
+    }
+    if (ok) {
+      st8bf(y + m * N + 8 * cc, o);
+      if (s_out) st8bf(s_out + m * N + 8 * cc, v[c]);
+    }
+  }
+  if (ok && l16 == 0) stats[m] = make_float2(mean, rstd);
+}
+
 // ln_bwd_kernel<NC, 1> with the next row's s / dy / stats loads issued before the current row's
 // reductions (a wave's rows are otherwise load -> reduce -> store in series, latency-bound)
 __device__ __forceinline__ void unpack8bf(const u32x4& a, float* v) {
@@ -838,8 +917,18 @@ extern "C" int snvrag_ln_fwd_train_act(int64_t M, int N, const void* x, const vo
     hipLaunchKernelGGL(kern, dim3(cdiv(M, 4)), dim3(256), 0, as_stream(stream), (long)M, N, (const bf16*)x,
                        (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats, dr);
   };
-  const int nch = cdiv(N / 8, 64);
-  if (nch == 1) go(ln_fwd_train_kernel<1>);
+  const int nch = cdiv(N / 8, 64), nc = N / 8;
+  if (nc % 16 == 0 && nc <= 64 && options().ln_rows1 == 0) {
+    // 16-lane row groups: four rows per wave, 16 rows per workgroup
+    auto go16 = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(cdiv(M, 16)), dim3(256), 0, as_stream(stream), (long)M, N, (const bf16*)x,
+                         (const bf16*)r, g, b, eps, (bf16*)y, (bf16*)s_out, (float2*)stats, dr);
+    };
+    if (nc == 16) go16(ln_fwd_train_g16<1>);
+    else if (nc == 32) go16(ln_fwd_train_g16<2>);
+    else if (nc == 48) go16(ln_fwd_train_g16<3>);
+    else go16(ln_fwd_train_g16<4>);
+  } else if (nch == 1) go(ln_fwd_train_kernel<1>);
   else if (nch == 2) go(ln_fwd_train_kernel<2>);
   else if (nch == 3) go(ln_fwd_train_kernel<3>);
   else go(ln_fwd_train_kernel<4>);
@@ -886,6 +975,8 @@ extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s
   // next row's loads issued ahead (N = 1536: 147-150 vs 174 us; N = 384: 55 vs 52 us, so not there)
   // unless SNVRAG_LN_BWD_NOPF (A/B)
   const bool pf = !options().ln_bwd_nopf;
+  // (16-lane row groups as in the forward: 62 vs 51 us at N = 384 — the per-lane dg / db
+  // partials of 3 chunks cost occupancy, 198 VGPRs — so the backward keeps one row per wave)
   if (pf && nch > 1) {
     if (nch == 2) go(ln_bwd_pf_kernel<2>);
     else if (nch == 3) go(ln_bwd_pf_kernel<3>);

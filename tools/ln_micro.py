@@ -24,7 +24,8 @@ def tm(fn, reps=20):
     return a.elapsed_time(b) / reps * 1e3
 
 
-for N, mode in ((384, "resid"), (1536, "act_x"), (384, "plain")):
+for N, mode, rows1 in ((384, "resid", 1), (384, "resid", 0), (1536, "act_x", 0), (384, "plain", 1), (384, "plain", 0)):
+    K.set_option("ln_rows1", rows1)           # 1: one row per wave (the pre-r4 kernels)
     x = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     g = torch.ones(N, device="cuda")
@@ -46,4 +47,4 @@ for N, mode in ((384, "resid"), (1536, "act_x"), (384, "plain")):
         f = tm(lambda: K.ln_fwd_train(x, None, g, b, 1e-5, p_out=0.1, seed=3))
         bw = tm(lambda: K.ln_bwd(dy, s, st, g, 0.0, 0.1, 3))
         nb = 3 * M * N * 2
-    print(f"N={N} {mode}: fwd {f:.1f} us  bwd {bw:.1f} us ({nb / bw / 1e3:.0f} GB/s)", flush=True)
+    print(f"N={N} {mode} rows1={rows1}: fwd {f:.1f} us  bwd {bw:.1f} us ({nb / bw / 1e3:.0f} GB/s)", flush=True)

@@ -31,6 +31,7 @@ for s in ${STEPS:-new attn bench}; do
     tprof) step train_torchprof 400 python tools/train_torchprof.py
            step train_only 300 python tools/train_only.py ;;
     c2)    step knn_emb_micro 300 python tools/knn_emb_micro.py ;;
+    ln)    step ln_micro 300 python tools/ln_micro.py ;;
     dw)    step dw_micro 300 env DW_XCD=0,1 python tools/dw_micro.py ;;
     tonly) step train_only_a 300 env SNVRAG_DW_XCD=0 python tools/train_only.py
            step train_only_b 300 env SNVRAG_DW_XCD=1 python tools/train_only.py ;;
