@@ -31,6 +31,10 @@ for s in ${STEPS:-new attn bench}; do
     tprof) step train_torchprof 400 python tools/train_torchprof.py
            step train_only 300 python tools/train_only.py ;;
     c2)    step knn_emb_micro 300 python tools/knn_emb_micro.py ;;
+    tprof2) step train_rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trainprof_$TAG -o train \
+             -- python3 tools/train_only.py
+           rm -f $OUT/trainprof_$TAG/*/*.db $OUT/trainprof_$TAG/*.db
+           python3 tools/prof_top.py $OUT/trainprof_$TAG 40 > $OUT/${TAG}_train_prof_top.txt 2>&1; head -45 $OUT/${TAG}_train_prof_top.txt ;;
     ln)    step ln_micro 300 python tools/ln_micro.py ;;
     dw)    step dw_micro 300 env DW_XCD=0,1 python tools/dw_micro.py ;;
     tonly) step train_only_a 300 env SNVRAG_DW_XCD=0 python tools/train_only.py

@@ -18,7 +18,7 @@ from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimi
 from src.model import build_model  # noqa: E402
 
 WANT = ("copy_", "add_", "add.", "_to_copy", "fill_", "zero_", "zeros", "cat", "clone", "mul.", "sum.", "index_put",
-        "slice_backward", "gelu")
+        "slice_backward", "gelu", "new_zeros", "empty", "where", "sub.", "div.")
 
 
 class Log(TorchDispatchMode):
@@ -57,6 +57,10 @@ log = Log()
 with log:
     tr.train_step(dict(batch))
 torch.cuda.synchronize()
+print("by calls: calls  bytes (MB)  op  shapes  origin")
+for key, n in sorted(log.rows.items(), key=lambda kv: -kv[1])[:40]:
+    name, shp, fr = key
+    print(f"{n:5d} {log.bytes[key] / 1e6:9.1f}  {name[:28]:28s} {str(shp)[:90]:90s} {fr}", flush=True)
 print("bytes touched (MB)  calls  op  shapes  origin")
 for key, b in sorted(log.bytes.items(), key=lambda kv: -kv[1])[:60]:
     name, shp, fr = key
