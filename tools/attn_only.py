@@ -37,11 +37,12 @@ for rnd in range(int(os.environ.get("ROUNDS", 1))):
         if base is None:
             base = out.clone()
         same = torch.equal(out, base)
+        err = (out.float() - base.float()).abs().max().item()
         if reps > 1:
             ms = a.elapsed_time(b) / (reps - 1)
             res[v].append(ms)
             print(f"attention variant {v}: {ms:.4f} ms  {4.0 * L * L * dh * H * nseq / ms / 1e9:.1f} TFLOP/s  "
-                  f"bit-identical to variant {variants[0]}: {same}", flush=True)
+                  f"bit-identical to variant {variants[0]}: {same} (max |diff| {err:.2e})", flush=True)
 K.set_option("attn_variant", 0)
 for v, t in res.items():
     if t:
