@@ -288,6 +288,15 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 _DIRECT_GRADS = False
+_BLAS_DX = [True]                           # large-K dX GEMMs on hipBLASLt (set_blas_dx)
+
+
+def set_blas_dx(enabled: bool) -> bool:
+    """The K >= 1024 -> 384 dX GEMMs of the training backward on hipBLASLt (default) or on the
+    row-panel kernel (A/B: tools/train_only.py BLAS_DX=0).  Returns the previous setting."""
+    prev = _BLAS_DX[0]
+    _BLAS_DX[0] = bool(enabled)
+    return prev
 
 
 @contextlib.contextmanager
@@ -399,6 +408,14 @@ class _HipLinear(torch.autograd.Function):
                 gx = K.sgemm(g2, wsp, n_in, vec)
                 if res is not None:
                     gx += res.reshape(gx.shape).to(gx.dtype)
+            elif _BLAS_DX[0] and g2.shape[1] >= 1024 and n_in == 384:
+                # the K >= 1024 -> 384 dX GEMMs (q/k/v, FeedForward w_1) on hipBLASLt: 80 vs 102 us
+                # (K = 1536) and 59 vs 79 us (K = 1152) at M = 49 440 (tools/dx_micro.py) — the
+                # row-panel kernel's 387 workgroups of 128 rows fill 1.5 rounds of the chip; the
+                # handed-off gradient enters as addmm's C operand (one f32 add, one rounding)
+                wc = bf16_of(ws[0]) if ctx.n == 1 else _cat_bf16(ws)
+                gx = torch.mm(g2, wc) if res is None else \
+                    torch.addmm(res.reshape(-1, n_in).to(torch.bfloat16), g2, wc)
             else:
                 wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else _cat_bf16(ws, transposed=True)
                 gx = K.linear(g2, wt, resid=None if res is None else res.reshape(-1, n_in).to(torch.bfloat16))
