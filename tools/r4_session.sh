@@ -36,6 +36,7 @@ for s in ${STEPS:-new attn bench}; do
            rm -f $OUT/trainprof_$TAG/*/*.db $OUT/trainprof_$TAG/*.db
            python3 tools/prof_top.py $OUT/trainprof_$TAG 40 > $OUT/${TAG}_train_prof_top.txt 2>&1; head -45 $OUT/${TAG}_train_prof_top.txt ;;
     dx)    step dx_micro 300 python tools/dx_micro.py ;;
+    sgt)   step sg_train_micro 300 python tools/sg_train_micro.py ;;
     tblas) step train_only_blas0 300 env BLAS_DX=0 python tools/train_only.py
            step train_only_blas1 300 env BLAS_DX=1 python tools/train_only.py ;;
     ln)    step ln_micro 300 python tools/ln_micro.py ;;
