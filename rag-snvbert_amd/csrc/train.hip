@@ -827,22 +827,21 @@ __global__ __launch_bounds__(256) void nbr_mean_drop_fwd_kernel(NbrArgs a, float
   }
 }
 
-// grid (cdiv(L, LB)): block = LB positions x D / 2 feature pairs; thread (pair, position group)
-// loops its positions, every query and neighbour; dAr[l] is owned by one thread (accumulated in
-// place), dW rows get one atomic per (block, token row, feature)
-constexpr int NBR_LB = 4;
+// grid (L): block = one position x the D / 2 feature pairs (one thread each, blockDim rounded to
+// whole waves); a thread loops every query and neighbour of its (position, pair); dAr[l] is owned
+// by one thread (accumulated in place), dW rows get one atomic per (block, token row, feature).
+// (r3: 4 positions per 256-thread block, each thread 3 pairs in series: 258 blocks = one wave per
+// SIMD on a latency-bound loop, 0.50 ms per step at B = 24.)
 __global__ __launch_bounds__(256) void nbr_mean_drop_bwd_kernel(NbrArgs a, const float* __restrict__ dout,
                                                                 float* __restrict__ dW, float* __restrict__ dAr) {
   extern __shared__ float wacc[];                    // [V][D] block partials of dW
   const int npair = a.D >> 1;
   for (int i = threadIdx.x; i < a.V * a.D; i += blockDim.x) wacc[i] = 0.f;
   __syncthreads();
-  const int pidx = threadIdx.x % 64, lgp = threadIdx.x / 64;    // 4 position groups
-  for (int pp = pidx; pp < npair; pp += 64) {
+  for (int pp = threadIdx.x; pp < npair; pp += blockDim.x) {
     const int d = 2 * pp;
-    for (int li = lgp; li < NBR_LB; li += 4) {
-      const int l = blockIdx.x * NBR_LB + li;
-      if (l >= a.L) break;
+    {
+      const int l = blockIdx.x;
       float ar0 = 0.f, ar1 = 0.f;
       float w0[2] = {0.f, 0.f}, w1[2] = {0.f, 0.f};  // the two site tokens (tok0, tok0 + 1)
       float ws0 = 0.f, ws1 = 0.f;                     // the position's single token (sos / eos / pad)
@@ -1055,8 +1054,9 @@ extern "C" int snvrag_nbr_mean_drop_bwd(int64_t nq, int k, int64_t L, int D, int
     return rc;
   SNV_CHECK_ARG(dout && dW && dAr, "null pointer");
   if (nq == 0) return 0;
-  hipLaunchKernelGGL(nbr_mean_drop_bwd_kernel, dim3((unsigned)cdiv(L, NBR_LB)), dim3(256),
-                     (size_t)V * D * sizeof(float), as_stream(stream), a, dout, dW, dAr);
+  const int nthr = (int)std::min<long>(256, (D / 2 + 63) / 64 * 64);
+  hipLaunchKernelGGL(nbr_mean_drop_bwd_kernel, dim3((unsigned)L), dim3(nthr), (size_t)V * D * sizeof(float),
+                     as_stream(stream), a, dout, dW, dAr);
   SNV_LAUNCH_CHECK();
   return 0;
 }
