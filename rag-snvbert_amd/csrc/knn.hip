@@ -59,32 +59,47 @@ __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int6
   // the last chunk also takes every position past the grid (padding tokens of a sequence longer
   // than the window: constant-term contributions only), so the grid is capped at nch
   const int lend = c == (int)gridDim.x - 1 ? L : min(L, (c + 1) * LUT_CH);
-  for (int l = c * LUT_CH + wave; l < lend; l += 4) {
+  // 16 lanes per position, 4 positions per wave, 16 per workgroup step: the D-length sums are
+  // 4-step reductions inside the 16-lane group, 4 positions at a time (one position per wave with
+  // three 6-step wave reductions each kept the loop latency-bound: 355 us per training step)
+  const int g = lane >> 4, l16 = lane & 15;
+  for (int base = c * LUT_CH; base < lend; base += 16) {
+    const int l = base + 4 * wave + g;
+    if (l >= lend) continue;                       // group-uniform: shuffles stay inside the group
     const int t = (int)tok_q[(long)q * L + l];
     const bool is_site = l >= 1 && l <= n_sites;
     const bool varying = is_site && !site_mask[l - 1];
     int rt;                                        // panel token at l when not varying
     if (l == 0) rt = 2; else if (is_site) rt = mask_tok; else if (l == n_sites + 1) rt = 3; else rt = 0;
     float t0 = 0.f, t1 = 0.f, tc = 0.f;
-    for (int d = lane; d < D; d += 64) {
-      float u = W[(long)t * D + d];
-      if (Aq) u += Aq[(arow + l) * D + d];
-      if (Ar) u -= Ar[(long)l * D + d];
+    for (int d = 4 * l16; d < D; d += 64) {
+      f32x4 u = *reinterpret_cast<const f32x4*>(W + (long)t * D + d);
+      if (Aq) u += *reinterpret_cast<const f32x4*>(Aq + (arow + l) * D + d);
+      if (Ar) u -= *reinterpret_cast<const f32x4*>(Ar + (long)l * D + d);
       if (varying) {
-        const float a = u - Wp[(long)tok0 * D + d], b = u - Wp[(long)tok1 * D + d];
-        t0 = fmaf(a, a, t0);
-        t1 = fmaf(b, b, t1);
+        const f32x4 a = u - *reinterpret_cast<const f32x4*>(Wp + (long)tok0 * D + d);
+        const f32x4 b = u - *reinterpret_cast<const f32x4*>(Wp + (long)tok1 * D + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { t0 = fmaf(a[e], a[e], t0); t1 = fmaf(b[e], b[e], t1); }
       } else {
-        const float cc = u - Wp[(long)rt * D + d];
-        tc = fmaf(cc, cc, tc);
+        const f32x4 cc = u - *reinterpret_cast<const f32x4*>(Wp + (long)rt * D + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tc = fmaf(cc[e], cc[e], tc);
       }
     }
-    t0 = wave_sum(t0); t1 = wave_sum(t1); tc = wave_sum(tc);
-    if (lane == 0) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      t0 += __shfl_xor(t0, o, 64);
+      t1 += __shfl_xor(t1, o, 64);
+      tc += __shfl_xor(tc, o, 64);
+    }
+    if (l16 == 0) {
       if (is_site) delta[(long)q * n_sites_pad + l - 1] = varying ? (t1 - t0) : 0.f;
       cacc += varying ? t0 : tc;
     }
   }
+  cacc += __shfl_xor(cacc, 16, 64);                // the four groups' partials (zero off group leaders)
+  cacc += __shfl_xor(cacc, 32, 64);
   if (lane == 0) wc[wave] = cacc;
   __syncthreads();
   if (threadIdx.x == 0) cpart[(long)q * nch + c] = (wc[0] + wc[1]) + (wc[2] + wc[3]);
@@ -939,6 +954,9 @@ extern "C" int snvrag_knn_lut_panel(int64_t nq, int64_t L, int64_t D, const int6
   float* gdelta = (float*)((char*)lut_out + lut_ws_offset(nq, n_sites_pad, limbs));
   float* gcpart = gdelta + (size_t)nq * n_sites_pad;
   if (Aq || Ar) {
+    auto a16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
+    SNV_CHECK_ARG(D % 4 == 0 && a16(W) && a16(Wp) && a16(Aq) && a16(Ar),
+                  "offset LUT: D % 4 == 0 and 16-byte aligned W / Wp / Aq / Ar (float4 rows)");
     const int64_t nch = std::min<int64_t>((L + LUT_CH - 1) / LUT_CH, lut_nch_max(n_sites_pad));
     hipLaunchKernelGGL(lut_delta_kernel, dim3((unsigned)nch, (unsigned)nq), dim3(256), 0, s,
                        (int)L, (int)D, tok_q, W, Wp, Aq, (long)aq_period, Ar, site_mask, n_sites, n_sites_pad, tok0,
