@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 26
+#define SNVRAG_ABI_VERSION 27
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -394,6 +394,15 @@ typedef struct {
   void* dst;
 } snvrag_derive_job_t;
 int snvrag_derive(const snvrag_derive_job_t* jobs, int njobs, int64_t total_pieces, void* stream);
+
+/* The hap head's Linear(K, 2) (foundation_model.py:25-33 net[2]) in training: x bf16 [M, K],
+ * w f32 [2, K], b f32 [2] -> out f32 [M, 2] = x w^T + b.  Backward: dx bf16 [M, K] = g w (optional),
+ * dw f32 [2, K] = g^T x (written, or added when accumulate; optional), g f32 [M, 2];
+ * ws: snvrag_head2_ws_bytes(M, K).  K % 8 == 0. */
+int snvrag_head2_fwd(int64_t M, int K, const void* x, const float* w, const float* b, float* out, void* stream);
+size_t snvrag_head2_ws_bytes(int64_t M, int K);
+int snvrag_head2_bwd(int64_t M, int K, const float* g, const void* x, const float* w, void* dx, float* dw,
+                     int accumulate, void* ws, size_t ws_bytes, void* stream);
 int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,
                          const void* wstream, const float* vec, const float* r1, const float* r2,
                          int64_t period, float eps, void* out, float* probs, float* logits, void* stream);

@@ -892,6 +892,148 @@ __global__ __launch_bounds__(256) void nbr_mean_drop_bwd_kernel(NbrArgs a, const
     if (wacc[i] != 0.f) unsafeAtomicAdd(dW + i, wacc[i]);
 }
 
+// ---- the hap head's last Linear(4D, 2) (foundation_model.py:25-33 net[2]) under autograd: bf16
+// activations against f32 weights, f32 logits.  torch ran it as F.linear(hh.float(), W): a 300 MB
+// f32 copy of hh and f32 GEMMs with N = 2 (hipBLASLt: 0.29 ms for dW alone at M = 49 440).
+// fwd: a 16-lane group computes 4 rows (16 per wave), 8-column chunks, so each weight load
+// serves 4 rows' activations; out[m] = (x[m] . w0 + b0, x[m] . w1 + b1)
+__global__ __launch_bounds__(256) void head2_fwd_kernel(long M, int K, const bf16* __restrict__ x,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15;
+  const long m0 = (((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4)) * 4;
+  if (m0 >= M) return;                                // group-uniform
+  const bf16* xr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) xr[r] = x + min(m0 + r, M - 1) * K;   // tail rows: re-read the last
+  float a0[4] = {}, a1[4] = {};
+  for (int c = l16; c < K / 8; c += 16) {
+    float v[4][8], w0[8], w1[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ld8bf(xr[r] + 8 * c, v[r]);
+    *reinterpret_cast<float4*>(w0) = *reinterpret_cast<const float4*>(w + 8 * c);
+    *reinterpret_cast<float4*>(w0 + 4) = *reinterpret_cast<const float4*>(w + 8 * c + 4);
+    *reinterpret_cast<float4*>(w1) = *reinterpret_cast<const float4*>(w + K + 8 * c);
+    *reinterpret_cast<float4*>(w1 + 4) = *reinterpret_cast<const float4*>(w + K + 8 * c + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a0[r] = fmaf(v[r][j], w0[j], a0[r]);
+        a1[r] = fmaf(v[r][j], w1[j], a1[r]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float s0 = gsum16(a0[r]), s1 = gsum16(a1[r]);
+    if (l16 == r && m0 + r < M) reinterpret_cast<float2*>(out)[m0 + r] = make_float2(s0 + b[0], s1 + b[1]);
+  }
+}
+// fwd at K = 512 NCH (the model's 4D = 1536: NCH = 3): a wave owns 16 rows (M = 49 440: 3 090
+// waves, one round at 4 waves/SIMD for 128 VGPRs) and keeps its lanes'
+// weight chunks in registers; per 4-row batch all 4 NCH activation loads are issued before use
+template <int NCH>
+__global__ __launch_bounds__(256) void head2_fwd_wave_kernel(long M, const bf16* __restrict__ x,
+                                                             const float* __restrict__ w, const float* __restrict__ b,
+                                                             float* __restrict__ out) {
+  constexpr int K = 512 * NCH;
+  const int lane = threadIdx.x & 63;
+  const long mw = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (mw >= M) return;                                // wave-uniform
+  float w0[NCH][8], w1[NCH][8];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<float4*>(&w0[i][4 * h]) = *reinterpret_cast<const float4*>(w + 8 * (lane + 64 * i) + 4 * h);
+      *reinterpret_cast<float4*>(&w1[i][4 * h]) = *reinterpret_cast<const float4*>(w + K + 8 * (lane + 64 * i) + 4 * h);
+    }
+  const float b0 = b[0], b1 = b[1];
+  for (int rb = 0; rb < 16; rb += 4) {
+    u32x4 raw[4][NCH];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i)
+        raw[r][i] = *reinterpret_cast<const u32x4*>(x + min(mw + rb + r, M - 1) * K + 8 * (lane + 64 * i));
+    float a0[4] = {}, a1[4] = {};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float lo = __uint_as_float(raw[r][i][j] << 16), hi = __uint_as_float(raw[r][i][j] & 0xffff0000u);
+          a0[r] = fmaf(lo, w0[i][2 * j], fmaf(hi, w0[i][2 * j + 1], a0[r]));
+          a1[r] = fmaf(lo, w1[i][2 * j], fmaf(hi, w1[i][2 * j + 1], a1[r]));
+        }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        a0[r] += __shfl_xor(a0[r], o, 64);
+        a1[r] += __shfl_xor(a1[r], o, 64);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (lane == r && mw + rb + r < M) reinterpret_cast<float2*>(out)[mw + rb + r] = make_float2(a0[r] + b0, a1[r] + b1);
+  }
+}
+// dx[m, k] = g[m, 0] w[0, k] + g[m, 1] w[1, k] (bf16), one thread per 8 elements
+__global__ __launch_bounds__(256) void head2_dx_kernel(long M, int K, const float* __restrict__ g,
+                                                       const float* __restrict__ w, bf16* __restrict__ dx) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x, n8 = (long)M * (K / 8);
+  if (i >= n8) return;
+  const long m = i / (K / 8);
+  const int c = (int)(i % (K / 8));
+  const float2 gm = reinterpret_cast<const float2*>(g)[m];
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = gm.x * w[8 * c + j] + gm.y * w[K + 8 * c + j];
+  st8bf(dx + m * K + 8 * c, o);
+}
+// dW partials: block b sums rows [b R, (b + 1) R) of g[m, j] x[m, k] into part[b][j K + k]
+// (columns over the threads, 8 per thread); ln_part_sum_kernel then sums the blocks in order
+__global__ __launch_bounds__(256) void head2_dw_kernel(long M, int K, int rows_per_block, const float* __restrict__ g,
+                                                       const bf16* __restrict__ x, float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (int c = threadIdx.x; c < K / 8; c += blockDim.x) {
+    float s0[8] = {}, s1[8] = {};
+    long m = r0;
+    for (; m + 8 <= r1; m += 8) {                     // 8 rows' loads in flight
+      float2 gm[8];
+      float v[8][8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        gm[r] = reinterpret_cast<const float2*>(g)[m + r];
+        ld8bf(x + (m + r) * K + 8 * c, v[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s0[j] = fmaf(gm[r].x, v[r][j], s0[j]);
+          s1[j] = fmaf(gm[r].y, v[r][j], s1[j]);
+        }
+    }
+    for (; m < r1; ++m) {
+      const float2 gm = reinterpret_cast<const float2*>(g)[m];
+      float v[8];
+      ld8bf(x + m * K + 8 * c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s0[j] = fmaf(gm.x, v[j], s0[j]);
+        s1[j] = fmaf(gm.y, v[j], s1[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      part[(long)blockIdx.x * 2 * K + 8 * c + j] = s0[j];
+      part[(long)blockIdx.x * 2 * K + K + 8 * c + j] = s1[j];
+    }
+  }
+}
+
 }  // namespace snvrag
 
 extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
@@ -1058,5 +1200,56 @@ extern "C" int snvrag_nbr_mean_drop_bwd(int64_t nq, int k, int64_t L, int D, int
   hipLaunchKernelGGL(nbr_mean_drop_bwd_kernel, dim3((unsigned)L), dim3(nthr), (size_t)V * D * sizeof(float),
                      as_stream(stream), a, dout, dW, dAr);
   SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int snvrag_head2_fwd(int64_t M, int K, const void* x, const float* w, const float* b, float* out,
+                                void* stream) {
+  if (M == 0) return 0;
+  SNV_CHECK_ARG(x && w && b && out, "null pointer");
+  SNV_CHECK_ARG(K % 8 == 0 && K > 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0,
+                "K % 8 == 0, 16-byte aligned x and w");
+  if (K == 1536)
+    hipLaunchKernelGGL(head2_fwd_wave_kernel<3>, dim3((unsigned)cdiv(M, 64)), dim3(256), 0, as_stream(stream),
+                       (long)M, (const bf16*)x, w, b, out);
+  else
+    hipLaunchKernelGGL(head2_fwd_kernel, dim3((unsigned)cdiv(M, 64)), dim3(256), 0, as_stream(stream), (long)M, K,
+                       (const bf16*)x, w, b, out);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t snvrag_head2_ws_bytes(int64_t M, int K) {
+  const long nblk = std::min<long>(cdiv(M, 64), 1024);
+  return (size_t)nblk * 2 * K * sizeof(float);
+}
+
+extern "C" int snvrag_head2_bwd(int64_t M, int K, const float* g, const void* x, const float* w, void* dx, float* dw,
+                                int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = as_stream(stream);
+  if (M == 0) {                                       // empty batch: dW = 0
+    if (dw && !accumulate) SNV_HIP(hipMemsetAsync(dw, 0, (size_t)2 * K * sizeof(float), st));
+    return 0;
+  }
+  SNV_CHECK_ARG(g && x && w && ws, "null pointer");
+  SNV_CHECK_ARG(K % 8 == 0 && K > 0 && ((uintptr_t)x % 16) == 0 && (!dx || ((uintptr_t)dx % 16) == 0),
+                "K % 8 == 0, 16-byte aligned x / dx");
+  SNV_CHECK_ARG(ws_bytes >= snvrag_head2_ws_bytes(M, K), "workspace too small");
+  if (dx) {
+    const long n8 = (long)M * (K / 8);
+    hipLaunchKernelGGL(head2_dx_kernel, dim3((unsigned)cdiv(n8, 256)), dim3(256), 0, st, (long)M, K, g, w, (bf16*)dx);
+    SNV_LAUNCH_CHECK();
+  }
+  if (dw) {
+    const long nblk = std::min<long>(cdiv(M, 64), 1024);
+    const int rpb = (int)cdiv(M, nblk);
+    hipLaunchKernelGGL(head2_dw_kernel, dim3((unsigned)nblk), dim3(std::min(256, (K / 8 + 63) / 64 * 64)), 0, st, (long)M, K, rpb, g, (const bf16*)x,
+                       (float*)ws);
+    SNV_LAUNCH_CHECK();
+    // rows of dW = "dg" (columns < K) and "db" (columns >= K) of the LayerNorm partial-sum kernel
+    hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * K, 16)), dim3(256), 0, st, nblk, K, (const float*)ws, dw,
+                       dw + K, accumulate);
+    SNV_LAUNCH_CHECK();
+  }
   return 0;
 }

@@ -492,6 +492,45 @@ def hip_linear(x: torch.Tensor, weight, bias=None, grad_from: Optional[GradHando
     return _HipLinear.apply(x, len(ws), grad_from, *ws, *bs)
 
 
+class _Head2(torch.autograd.Function):
+    """The hap head's Linear(4D, 2) (foundation_model.py:25-33 net[2]): bf16 activations, f32
+    weights and logits (csrc/train.hip head2_*; torch ran F.linear(hh.float(), W): an f32 copy of
+    the [M, 4D] activations and N = 2 GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        y = K.head2_fwd(x2, w.detach(), b.detach())
+        ctx.save_for_backward(x2, w)
+        ctx.in_shape, ctx.params = x.shape, (w, b)
+        return y.reshape(*x.shape[:-1], 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        g2 = gy.reshape(-1, 2).float().contiguous()
+        pw, pb = ctx.params
+        direct = _DIRECT_GRADS and _grad_buffer(pw) is not None and _grad_buffer(pb) is not None
+        dx, dw = K.head2_bwd(g2, x2, w.detach(), want_dx=ctx.needs_input_grad[0],
+                             dw=pw.grad if direct else None, accumulate=direct)
+        gb = g2.sum(0)
+        if dx is not None:
+            dx = dx.reshape(ctx.in_shape)
+        if direct:
+            pb.grad.add_(gb)
+            return dx, None, None
+        return dx, (dw if ctx.needs_input_grad[1] else None), (gb if ctx.needs_input_grad[2] else None)
+
+
+def head2_linear(x: torch.Tensor, lin) -> torch.Tensor:
+    """f32 logits of ``lin`` = nn.Linear(K, 2) on bf16 ``x``; the f32 parity mode keeps
+    F.linear on f32 activations."""
+    if train_dtype() == torch.float32 or x.dtype != torch.bfloat16 or x.shape[-1] % 8 or \
+            tuple(lin.weight.shape) != (2, x.shape[-1]) or lin.bias is None:
+        return torch.nn.functional.linear(x.float(), lin.weight, lin.bias)
+    return _Head2.apply(x, lin.weight, lin.bias)
+
+
 class _HipLinearRank2(torch.autograd.Function):
     """z = Linear(cat([x, c1, c2], -1)) = x W[:, :D]^T + b + c1 W[:, D] + c2 W[:, D + 1] (bf16 out)
     with the two extra input columns as per-row rank-1 terms in the stream GEMM's epilogue

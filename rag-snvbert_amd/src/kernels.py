@@ -787,6 +787,33 @@ def derive(table: Tuple[torch.Tensor, int, int]) -> None:
     check(N.lib().snvrag_derive(ptr(t), n, total, stream_ptr()), "derive")
 
 
+def head2_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """f32 [..., 2] = x w^T + b for bf16 x [..., K], f32 w [2, K], b [2] (csrc/train.hip head2)."""
+    N.require_gpu(x)
+    Kd = x.shape[-1]
+    M = x.numel() // Kd
+    out = torch.empty(*x.shape[:-1], 2, device=x.device, dtype=torch.float32)
+    check(N.lib().snvrag_head2_fwd(M, Kd, ptr(_c(x)), ptr(_c(w.float())), ptr(_c(b.float())), ptr(out),
+                                   stream_ptr()), "head2_fwd")
+    return out
+
+
+def head2_bwd(g: torch.Tensor, x: torch.Tensor, w: torch.Tensor, want_dx: bool = True,
+              dw: Optional[torch.Tensor] = None, accumulate: bool = False):
+    """(dx bf16 [..., K] or None, dw f32 [2, K]) of :func:`head2_fwd` for the f32 gradient g [..., 2];
+    ``dw`` given: written or (accumulate) added in place."""
+    Kd = x.shape[-1]
+    M = x.numel() // Kd
+    dx = torch.empty_like(x) if want_dx else None
+    if dw is None:
+        dw = torch.empty(2, Kd, device=x.device, dtype=torch.float32)
+    wsb = int(N.lib().snvrag_head2_ws_bytes(M, Kd))
+    ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
+    check(N.lib().snvrag_head2_bwd(M, Kd, ptr(_c(g.float())), ptr(_c(x)), ptr(_c(w.float())), ptr(dx), ptr(dw),
+                                   int(accumulate), ptr(ws), wsb, stream_ptr()), "head2_bwd")
+    return dx, dw
+
+
 def sgemm_vec(bias: torch.Tensor, c1: Optional[torch.Tensor] = None, c2: Optional[torch.Tensor] = None,
               ln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
               head: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:

@@ -38,8 +38,8 @@ from typing import Dict, List, Optional
 import torch
 import torch.nn.functional as F
 
-from .autograd_ops import (GradHandoff, hip_add_layernorm, hip_attention, hip_linear, hip_linear_rank2,
-                           nbr_mean_drop, rag_mean_train, tiny_embedding, train_dtype)
+from .autograd_ops import (GradHandoff, head2_linear, hip_add_layernorm, hip_attention, hip_linear,
+                           hip_linear_rank2, nbr_mean_drop, rag_mean_train, tiny_embedding, train_dtype)
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -345,7 +345,7 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     hh = F.gelu(_linear_cat2(hx, hc.af_fusion[0], af2, afp2).to(train_dtype()))
     hh = hip_add_layernorm(hip_linear(hh, hc.af_fusion[2].weight, hc.af_fusion[2].bias), None, hc.af_fusion[3])
     hh = F.gelu(hip_linear(hh, hc.net[0].weight, hc.net[0].bias))
-    logits = F.linear(hh.float(), hc.net[2].weight, hc.net[2].bias)
+    logits = head2_linear(hh, hc.net[2])
     probs = torch.softmax(logits, -1)
     p1, p2 = probs[:B], probs[B:]
     gc = fm.gt_classifier

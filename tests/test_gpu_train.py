@@ -1223,3 +1223,35 @@ def test_ln_forward_row_groups_match_one_row_per_wave(N):
     torch.testing.assert_close(st0, st1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(y0.float(), y1.float(), rtol=1e-2, atol=1e-2)
     assert ((y0 == 0) == (y1 == 0)).all()                    # the same dropped elements
+
+
+@pytest.mark.parametrize("M,Kd", [(0, 1536), (1, 1536), (777, 1536), (49440 // 8 + 5, 1536), (3001, 1024),
+                                  (5, 40)])
+def test_head2_linear_vs_torch_fp32(M, Kd):
+    """The hap head's Linear(4D, 2) kernels (forward, dx, dW with direct .grad accumulation)
+    against torch fp32 on the same bf16 activations: logits / dW / db to f32 summation order
+    (tolerance 1e-4 relative), dx within one bf16 rounding.  K = 1536 (the model's 4D) runs the
+    wave-per-16-rows forward, other K the generic one."""
+    from src import autograd_ops as A
+    g = torch.Generator(device="cpu").manual_seed(M)
+    lin = torch.nn.Linear(Kd, 2).to(DEV)
+    x = torch.randn(M, Kd, generator=g).to(DEV).bfloat16().requires_grad_(True)
+    gy = torch.randn(M, 2, generator=g).to(DEV)
+    y = A.head2_linear(x, lin)
+    assert y.dtype == torch.float32 and y.shape == (M, 2)
+    xr = x.detach().float().requires_grad_(True)
+    w = lin.weight.detach().clone().requires_grad_(True)
+    b = lin.bias.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr, w, b)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    y.backward(gy)
+    yr.backward(gy)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(lin.weight.grad, w.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(lin.bias.grad, b.grad, rtol=1e-4, atol=1e-3)
+    # direct accumulation into existing .grad buffers (the trainer's flat gradient buffer)
+    gw0, gb0 = lin.weight.grad.clone(), lin.bias.grad.clone()
+    with A.direct_weight_grads():
+        A.head2_linear(x.detach(), lin).backward(gy)
+    torch.testing.assert_close(lin.weight.grad, gw0 + w.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(lin.bias.grad, gb0 + b.grad, rtol=1e-4, atol=1e-3)
