@@ -414,8 +414,10 @@ class _HipLinear(torch.autograd.Function):
                 # row-panel kernel's 387 workgroups of 128 rows fill 1.5 rounds of the chip; the
                 # handed-off gradient enters as addmm's C operand (one f32 add, one rounding)
                 wc = bf16_of(ws[0]) if ctx.n == 1 else _cat_bf16(ws)
+                # (in place on the handed-off gradient, which nothing else holds: out-of-place
+                # addmm first copies its C operand into a fresh output, 15 us at M = 49 440)
                 gx = torch.mm(g2, wc) if res is None else \
-                    torch.addmm(res.reshape(-1, n_in).to(torch.bfloat16), g2, wc)
+                    res.reshape(-1, n_in).to(torch.bfloat16).addmm_(g2, wc)
             else:
                 wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else _cat_bf16(ws, transposed=True)
                 gx = K.linear(g2, wt, resid=None if res is None else res.reshape(-1, n_in).to(torch.bfloat16))
