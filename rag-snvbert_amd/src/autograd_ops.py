@@ -152,13 +152,14 @@ def _derived(tag: tuple, parts, make):
 
 
 def _refresh_derived() -> None:
-    dead = []
+    dead, live = [], []                     # live: strong references to the sources until the launch
     for key, ent in _DER.items():
         bases = [r() for r in ent.refs]
         if any(b is None for b in bases) or tuple(b.data_ptr() for b in bases) != ent.ptrs:
             dead.append(key)
         else:
             ent.vers = tuple(b._version for b in bases)
+            live.append(bases)
     for key in dead:
         del _DER[key]
         _DER_TABLE[0] = None
@@ -166,8 +167,7 @@ def _refresh_derived() -> None:
         return
     if _DER_TABLE[0] is None:
         jobs = [j for ent in _DER.values() for j in ent.jobs]
-        dev = next(iter(_DER.values())).refs[0]().device
-        _DER_TABLE[0] = K.derive_table(jobs, dev)
+        _DER_TABLE[0] = K.derive_table(jobs, live[0][0].device)
     K.derive(_DER_TABLE[0])
 
 
