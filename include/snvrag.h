@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define SNVRAG_ABI_VERSION 27
+#define SNVRAG_ABI_VERSION 28
 
 enum { SNVRAG_F32 = 0, SNVRAG_BF16 = 1 };
 enum { SNVRAG_ACT_NONE = 0, SNVRAG_ACT_GELU = 1, SNVRAG_ACT_LRELU = 2, SNVRAG_ACT_SIGMOID = 3 };
@@ -401,6 +401,13 @@ int snvrag_derive(const snvrag_derive_job_t* jobs, int njobs, int64_t total_piec
  * ws: snvrag_head2_ws_bytes(M, K).  K % 8 == 0. */
 int snvrag_head2_fwd(int64_t M, int K, const void* x, const float* w, const float* b, float* out, void* stream);
 size_t snvrag_head2_ws_bytes(int64_t M, int K);
+/* Weight gradient of a V-row token table (embedding/bert.py:63-75 TokenEmbedding under autograd):
+ * dw f32 [V, D] = sum over m of onehot(tok[m]) g[m] (rows with tok = padding_idx skipped; pass -1
+ * for none); tok int64 [M], g f32 [M, D]; V <= 16, D even; deterministic; written, not added.
+ * ws: snvrag_tokgrad_ws_bytes(M, V, D). */
+size_t snvrag_tokgrad_ws_bytes(int64_t M, int V, int D);
+int snvrag_tokgrad(int64_t M, int V, int D, int padding_idx, const int64_t* tok, const float* g, float* dw,
+                   void* ws, size_t ws_bytes, void* stream);
 int snvrag_head2_bwd(int64_t M, int K, const float* g, const void* x, const float* w, void* dx, float* dw,
                      int accumulate, void* ws, size_t ws_bytes, void* stream);
 int snvrag_sgemm_forward(int64_t M, int D, int N, int epi, int act, float slope, const void* x,

@@ -1034,6 +1034,44 @@ __global__ __launch_bounds__(256) void head2_dw_kernel(long M, int K, int rows_p
   }
 }
 
+// ---- weight gradient of a token table of V <= 16 rows (BERTEmbedding's TokenEmbedding,
+// embedding/bert.py:63-75, under autograd): dW[v] = sum over rows m with tok[m] = v of g[m]; the
+// padding row (nn.Embedding padding_idx) gets none.  Per-block partials over row ranges (every
+// thread owns 2 columns and 16 x 2 accumulators, rows selected by compare, no dynamic register
+// indexing), then the fixed-order column sum: deterministic.  Replaces a one-hot f32 GEMM of
+// K = M (hipBLASLt: 104 us at M = 49 440, no split-K) and its one_hot / cast / fill kernels.
+__global__ __launch_bounds__(256) void tokgrad_part_kernel(long M, int D, int V, int pad, int rows_per_block,
+                                                           const long* __restrict__ tok, const float* __restrict__ g,
+                                                           float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (int c = threadIdx.x; c < D / 2; c += blockDim.x) {
+    float2 acc[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = make_float2(0.f, 0.f);
+    for (long m0 = r0; m0 < r1; m0 += 8) {            // 8 rows' loads in flight
+      long t[8];
+      float2 x[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const long m = min(m0 + r, r1 - 1);
+        t[r] = m0 + r < r1 ? tok[m] : -1;
+        x[r] = reinterpret_cast<const float2*>(g + m * D)[c];
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const bool hit = t[r] == v && v != pad;
+          acc[v].x += hit ? x[r].x : 0.f;
+          acc[v].y += hit ? x[r].y : 0.f;
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      if (v < V) reinterpret_cast<float2*>(part + (long)blockIdx.x * V * D + (long)v * D)[c] = acc[v];
+  }
+}
+
 }  // namespace snvrag
 
 extern "C" int snvrag_ln_fwd_train(int64_t M, int N, const void* x, const void* r, const float* g, const float* b,
@@ -1251,5 +1289,34 @@ extern "C" int snvrag_head2_bwd(int64_t M, int K, const float* g, const void* x,
                        dw + K, accumulate);
     SNV_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+extern "C" size_t snvrag_tokgrad_ws_bytes(int64_t M, int V, int D) {
+  const long nblk = std::max<long>(1, std::min<long>(cdiv(M, 64), 1024));
+  return (size_t)nblk * V * D * sizeof(float);
+}
+
+extern "C" int snvrag_tokgrad(int64_t M, int V, int D, int padding_idx, const int64_t* tok, const float* g, float* dw,
+                              void* ws, size_t ws_bytes, void* stream) {
+  SNV_CHECK_ARG(dw && ws, "null pointer");
+  SNV_CHECK_ARG(V >= 1 && V <= 16 && D % 2 == 0 && D > 0, "1 <= V <= 16 rows, even D");
+  SNV_CHECK_ARG(M == 0 || (tok && g && ((uintptr_t)g % 8) == 0), "tok / g (8-byte aligned)");
+  SNV_CHECK_ARG(ws_bytes >= snvrag_tokgrad_ws_bytes(M, V, D), "workspace too small");
+  hipStream_t st = as_stream(stream);
+  if (M == 0) {
+    SNV_HIP(hipMemsetAsync(dw, 0, (size_t)V * D * sizeof(float), st));
+    return 0;
+  }
+  const long nblk = std::max<long>(1, std::min<long>(cdiv(M, 64), 1024));
+  const int rpb = (int)cdiv(M, nblk);
+  hipLaunchKernelGGL(tokgrad_part_kernel, dim3((unsigned)nblk), dim3(std::min(256, (D / 2 + 63) / 64 * 64)), 0, st,
+                     (long)M, D, V, padding_idx, rpb, (const long*)tok, g, (float*)ws);
+  SNV_LAUNCH_CHECK();
+  // the V x D partial rows summed in block order: ln_part_sum_kernel over 2 N = V D columns
+  const int VD = V * D;                              // even (D even)
+  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(VD, 16)), dim3(256), 0, st, nblk, VD / 2, (const float*)ws, dw,
+                     dw + VD / 2, 0);
+  SNV_LAUNCH_CHECK();
   return 0;
 }

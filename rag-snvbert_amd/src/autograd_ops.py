@@ -191,6 +191,9 @@ class _TinyVocabEmbedding(torch.autograd.Function):
     def backward(ctx, g):
         (tok,) = ctx.saved_tensors
         D = g.shape[-1]
+        if ctx.V <= 16 and D % 2 == 0 and g.is_cuda:
+            # one pass over g, per-block partials + fixed-order sum (csrc/train.hip tokgrad)
+            return None, K.tokgrad(tok, g, ctx.V, ctx.padding_idx).to(ctx.wdtype), None
         oh = torch.nn.functional.one_hot(tok.reshape(-1), ctx.V).to(torch.float32)
         gW = oh.t() @ g.reshape(-1, D).float()
         if ctx.padding_idx is not None:
@@ -364,6 +367,11 @@ class _HipLinear(torch.autograd.Function):
         if _sg_ok(x2, n_out):
             wsp, vec = _sg_stream(ws, bs, n_out)
             y = K.sgemm(x2, wsp, n_out, vec)
+        elif _BLAS_DX[0] and n == 1 and Kd >= 1024 and n_out == 384 and x2.shape[0] >= 8192:
+            # FeedForward's w_2 (K = 4D -> D) on hipBLASLt, the shape of the large-K dX GEMMs below
+            # (80 vs 102 us at M = 49 440); its bias epilogue takes the bias in bf16
+            w = bf16_of(ws[0])
+            y = torch.addmm(bf16_of(bs[0]), x2, w.t()) if has_b else torch.mm(x2, w.t())
         else:
             w = bf16_of(ws[0]) if n == 1 else _cat_bf16(ws)
             b = (bs[0].detach() if n == 1 else _cat_f32(bs)) if has_b else None

@@ -787,6 +787,21 @@ def derive(table: Tuple[torch.Tensor, int, int]) -> None:
     check(N.lib().snvrag_derive(ptr(t), n, total, stream_ptr()), "derive")
 
 
+def tokgrad(tok: torch.Tensor, g: torch.Tensor, V: int, padding_idx: Optional[int] = None) -> torch.Tensor:
+    """f32 [V, D] weight gradient of W[tok] for the f32 output gradient g [..., D] (csrc/train.hip)."""
+    N.require_gpu(g)
+    D = g.shape[-1]
+    t = _c(tok.reshape(-1).long())
+    g2 = _c(g.reshape(-1, D).float())
+    M = t.numel()
+    dw = torch.empty(V, D, device=g.device, dtype=torch.float32)
+    wsb = int(N.lib().snvrag_tokgrad_ws_bytes(M, V, D))
+    ws = torch.empty(wsb // 4, device=g.device, dtype=torch.float32)
+    check(N.lib().snvrag_tokgrad(M, V, D, -1 if padding_idx is None else int(padding_idx), ptr(t), ptr(g2), ptr(dw),
+                                 ptr(ws), wsb, stream_ptr()), "tokgrad")
+    return dw
+
+
 def head2_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """f32 [..., 2] = x w^T + b for bf16 x [..., K], f32 w [2, K], b [2] (csrc/train.hip head2)."""
     N.require_gpu(x)

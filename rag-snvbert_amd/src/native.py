@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("SNVRAG_LIB", PKG_DIR / "lib" / "libsnvrag.so"))
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_LRELU, ACT_SIGMOID = 0, 1, 2, 3
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int32, C.c_float, C.c_size_t
 
@@ -154,6 +154,8 @@ _SIGS = {
     "snvrag_derive": ([vp, C.c_int, i64, vp], C.c_int),
     "snvrag_head2_fwd": ([i64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_head2_ws_bytes": ([i64, C.c_int], sz),
+    "snvrag_tokgrad_ws_bytes": ([i64, C.c_int, C.c_int], sz),
+    "snvrag_tokgrad": ([i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_head2_bwd": ([i64, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp, sz, vp], C.c_int),
     "snvrag_sgemm_forward": ([i64, C.c_int, C.c_int, C.c_int, C.c_int, f32, vp, vp, vp, vp, vp, i64, f32, vp, vp, vp,
                               vp], C.c_int),

@@ -1255,3 +1255,25 @@ def test_head2_linear_vs_torch_fp32(M, Kd):
         A.head2_linear(x.detach(), lin).backward(gy)
     torch.testing.assert_close(lin.weight.grad, gw0 + w.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(lin.bias.grad, gb0 + b.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,V,D,pad", [(0, 10, 384, 0), (1, 10, 384, 0), (49440 // 4 + 3, 10, 384, 0),
+                                       (777, 16, 6, None), (300, 1, 2, None)])
+def test_token_table_gradient_vs_onehot_fp64(M, V, D, pad):
+    """The token-table weight gradient kernel (tiny_embedding's backward) against the one-hot
+    product in float64: the padding row gets nothing, float32 summation-order tolerance, and two
+    calls on the same inputs agree bitwise (fixed-order reduction)."""
+    from src import autograd_ops as A, kernels as K
+    g = torch.Generator(device="cpu").manual_seed(M + V)
+    tok = torch.randint(0, V, (M,), generator=g)
+    gy = torch.randn(M, D, generator=g)
+    want = torch.nn.functional.one_hot(tok, V).double().t() @ gy.double()
+    if pad is not None:
+        want[pad] = 0
+    got = K.tokgrad(tok.to(DEV), gy.to(DEV), V, pad)
+    torch.testing.assert_close(got.cpu().double(), want, rtol=1e-5, atol=1e-4)
+    assert torch.equal(got, K.tokgrad(tok.to(DEV), gy.to(DEV), V, pad))
+    if M:                                   # through the autograd node
+        W = torch.randn(V, D, device=DEV, requires_grad=True)
+        A.tiny_embedding(tok.to(DEV), W, pad).backward(gy.to(DEV))
+        torch.testing.assert_close(W.grad.cpu().double(), want, rtol=1e-5, atol=1e-4)
