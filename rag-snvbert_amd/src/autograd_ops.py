@@ -290,6 +290,55 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b).float()
 
 
+def _wgrad(g2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """f32 dW = g2^T x2 for a small weight (N x K <= 2^18) over many rows M: the library GEMM runs
+    such an output on a handful of workgroups looping the whole M (47-107 us per call at M = 24 720 /
+    49 440, ~0.8 ms per training step over the AF MLPs, the rag-fusion gate / encoder and the
+    genotype head); here M is cut into 64 row chunks — one batched GEMM over the chunks, then the
+    fixed-order sum of the 64 partial products (plus the < 64 leftover rows)."""
+    M, N = g2.shape
+    Kd = x2.shape[1]
+    if M < 8192 or N * Kd > (1 << 18):
+        return _mm_f32(g2.t(), x2) if g2.dtype == torch.bfloat16 else g2.float().t() @ x2.float()
+    g2, x2 = g2.float().contiguous(), x2.float().contiguous()
+    C = 64
+    Mc = M // C
+    main = C * Mc
+    out = torch.bmm(g2[:main].reshape(C, Mc, N).transpose(1, 2), x2[:main].reshape(C, Mc, Kd)).sum(0)
+    if main < M:
+        out += g2[main:].t() @ x2[main:]
+    return out
+
+
+class _SmallLinear(torch.autograd.Function):
+    """nn.Linear in f32 for the small per-site MLPs (rag fusion's gate / joint encoder,
+    fusion.py:82-128; the genotype head, foundation_model.py:64-80): torch's forward and dX,
+    the weight gradient by :func:`_wgrad`."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        N, Kd = w.shape
+        g2 = g.reshape(-1, N)
+        gx = (g @ w.to(g.dtype)).to(x.dtype) if ctx.needs_input_grad[0] else None
+        gw = _wgrad(g2, x.reshape(-1, Kd)).to(w.dtype) if ctx.needs_input_grad[1] else None
+        gb = g2.float().sum(0).to(w.dtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def small_linear(x: torch.Tensor, lin) -> torch.Tensor:
+    """``lin(x)`` for an nn.Linear whose weight gradient is a small output over many rows."""
+    if not torch.is_grad_enabled() or not x.is_cuda:
+        return torch.nn.functional.linear(x, lin.weight, lin.bias)
+    return _SmallLinear.apply(x, lin.weight, lin.bias)
+
+
 _DIRECT_GRADS = False
 _BLAS_DX = [True]                           # large-K dX GEMMs on hipBLASLt (set_blas_dx)
 
@@ -456,7 +505,7 @@ class _HipLinear(torch.autograd.Function):
                 gbs = list(torch.split(gb, sizes, 0))
             return (gx, None, None, *gws, *gbs)
         if any(ctx.needs_input_grad[3:3 + ctx.n]):
-            gw = _mm_f32(g2.t(), x2)
+            gw = _wgrad(g2, x2)
             gws = list(torch.split(gw, sizes, 0))
         if ctx.has_bias:
             gb = K.colsum(g2) if g2.shape[-1] % 8 == 0 and g2.shape[-1] <= 2048 else g2.float().sum(0)

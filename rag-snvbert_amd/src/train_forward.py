@@ -39,7 +39,8 @@ import torch
 import torch.nn.functional as F
 
 from .autograd_ops import (GradHandoff, head2_linear, hip_add_layernorm, hip_attention, hip_linear,
-                           hip_linear_rank2, nbr_mean_drop, rag_mean_train, tiny_embedding, train_dtype)
+                           hip_linear_rank2, nbr_mean_drop, rag_mean_train, small_linear, tiny_embedding,
+                           train_dtype)
 
 
 def _drop(x: torch.Tensor, p: float, training: bool) -> torch.Tensor:
@@ -136,9 +137,8 @@ def rag_fusion(rf, orig: torch.Tensor, rag: torch.Tensor, af: torch.Tensor, af_p
     (K = 1 after the neighbour mean, so the pooling softmax weight is exactly 1)."""
     ai = rf.af_interaction
     comb = torch.stack([af, af_p], -1)
-    gate = torch.sigmoid(F.linear(F.gelu(F.linear(comb, ai.gate_net[0].weight, ai.gate_net[0].bias)),
-                                  ai.gate_net[2].weight, ai.gate_net[2].bias))
-    enc = F.gelu(_ln(F.linear(comb, ai.joint_encoder[0].weight, ai.joint_encoder[0].bias), ai.joint_encoder[1]))
+    gate = torch.sigmoid(small_linear(F.gelu(small_linear(comb, ai.gate_net[0])), ai.gate_net[2]))
+    enc = F.gelu(_ln(small_linear(comb, ai.joint_encoder[0]), ai.joint_encoder[1]))
     fused_af = af.unsqueeze(-1) + ai.res_scale * (gate * enc)
     ad = rf.af_adapter
     w = _drop(F.gelu(hip_linear(fused_af, ad[0].weight, ad[0].bias)), p, training)
@@ -350,9 +350,9 @@ def forward_train(fm, x: Dict[str, torch.Tensor]) -> List[torch.Tensor]:
     p1, p2 = probs[:B], probs[B:]
     gc = fm.gt_classifier
     gf = torch.cat([p1, p2, g("ref").unsqueeze(-1), g("het").unsqueeze(-1), g("hom").unsqueeze(-1)], -1)
-    gf = _ln(F.leaky_relu(gc.gf_fusion(gf), 0.01), gc.gf_norm)
+    gf = _ln(F.leaky_relu(small_linear(gf, gc.gf_fusion), 0.01), gc.gf_norm)
     ff = gc.layer
-    gf = F.leaky_relu(ff.w_1(gf), 0.1)
-    gf = _drop(F.leaky_relu(ff.w_2(_ln(gf, ff.norm)), 0.1), ff.dropout.p, training)
-    gt = torch.softmax(gc.classifier(gf), -1)
+    gf = F.leaky_relu(small_linear(gf, ff.w_1), 0.1)
+    gf = _drop(F.leaky_relu(small_linear(_ln(gf, ff.norm), ff.w_2), 0.1), ff.dropout.p, training)
+    gt = torch.softmax(small_linear(gf, gc.classifier), -1)
     return [p1, p2, gt, h_raw[:B], h_raw[B:], hx[:B], hx[B:]]
