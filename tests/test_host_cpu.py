@@ -187,3 +187,31 @@ def test_bench_flop_counter_wraps_the_train_graph_signatures():
         assert seen["lin"] == {"grad_from": "h"} and fl.flops == 6 * 2 * 4 * 16
     finally:
         tf.hip_linear, tf.hip_linear_rank2, tf.hip_attention = real
+
+
+@pytest.mark.parametrize("M,N,Kd", [(9000 + 13, 32, 2), (24720, 16, 7), (8192, 384, 64), (100, 4, 3)])
+def test_small_weight_gradient_chunked_vs_fp64(M, N, Kd):
+    """autograd_ops._wgrad (dW = g^T x for small weights over many rows: 64 row chunks as one batched
+    GEMM + the chunk sum, leftover rows added) against float64, including M not a multiple of 64
+    and the short-M plain path; and _SmallLinear's backward against torch autograd (CPU tensors
+    call the function directly)."""
+    import sys
+    import torch
+    sys.path.insert(0, str(REPO / "rag-snvbert_amd"))
+    from src import autograd_ops as A
+    g = torch.Generator().manual_seed(M + N)
+    g2, x2 = torch.randn(M, N, generator=g), torch.randn(M, Kd, generator=g)
+    want = g2.double().t() @ x2.double()
+    got = A._wgrad(g2, x2)
+    assert got.dtype == torch.float32 and got.shape == (N, Kd)
+    torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=1e-3 * math.sqrt(M / 1000))
+    lin = torch.nn.Linear(Kd, N)
+    x = torch.randn(M, Kd, generator=g, requires_grad=True)
+    A._SmallLinear.apply(x, lin.weight, lin.bias).backward(g2)
+    gw, gb, gx = lin.weight.grad.clone(), lin.bias.grad.clone(), x.grad.clone()
+    lin.zero_grad()
+    x.grad = None
+    torch.nn.functional.linear(x, lin.weight, lin.bias).backward(g2)
+    torch.testing.assert_close(gw, lin.weight.grad, rtol=1e-4, atol=1e-3 * math.sqrt(M / 1000))
+    torch.testing.assert_close(gb, lin.bias.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gx, x.grad)
