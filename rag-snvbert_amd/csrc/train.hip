@@ -677,30 +677,32 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(long M, int N, int rows_
 }
 
 // column sums of the ln_bwd partials [R][2N] into dg (columns < N) and db: written, or added
-// to what they hold (accumulate: the parameters' .grad buffers); fixed-order (deterministic)
-__global__ __launch_bounds__(256) void ln_part_sum_kernel(long R, int N, const float* __restrict__ x,
-                                                          float* __restrict__ dg, float* __restrict__ db,
-                                                          int accumulate) {
-  __shared__ float red[16][17];
+// to what they hold (accumulate: the parameters' .grad buffers); fixed-order (deterministic).
+// 16 columns x 64 row groups per block (1 024 threads): at N = 384 the grid is only 48 blocks, so
+// the rows are cut 64 ways (16 ways: ~32 dependent load rounds per thread at R = 2 048, 10.5 us)
+__global__ __launch_bounds__(1024) void ln_part_sum_kernel(long R, int N, const float* __restrict__ x,
+                                                           float* __restrict__ dg, float* __restrict__ db,
+                                                           int accumulate) {
+  __shared__ float red[64][17];
   const int cl = threadIdx.x & 15, gi = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl, W = 2 * N;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (c < W) {
     long r = gi;
-    for (; r + 48 < R; r += 64) {
+    for (; r + 192 < R; r += 256) {
       a0 += x[r * W + c];
-      a1 += x[(r + 16) * W + c];
-      a2 += x[(r + 32) * W + c];
-      a3 += x[(r + 48) * W + c];
+      a1 += x[(r + 64) * W + c];
+      a2 += x[(r + 128) * W + c];
+      a3 += x[(r + 192) * W + c];
     }
-    for (; r < R; r += 16) a0 += x[r * W + c];
+    for (; r < R; r += 64) a0 += x[r * W + c];
   }
   red[gi][cl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (gi == 0 && c < W) {
     float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sum += red[i][cl];
+#pragma unroll 8
+    for (int i = 0; i < 64; ++i) sum += red[i][cl];
     float* o = c < N ? dg + c : db + (c - N);
     *o = accumulate ? *o + sum : sum;
   }
@@ -1166,7 +1168,7 @@ extern "C" int snvrag_ln_bwd_act(int64_t M, int N, const void* dy, const void* s
   else go(ln_bwd_kernel<4, 1>);
   SNV_LAUNCH_CHECK();
   // dg = sum over blocks of part[:, 0, :], db of part[:, 1, :] (written or accumulated)
-  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * N, 16)), dim3(256), 0, st, (long)nblk, N, (const float*)part,
+  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * N, 16)), dim3(1024), 0, st, (long)nblk, N, (const float*)part,
                      dg, db, accumulate);
   SNV_LAUNCH_CHECK();
   return 0;
@@ -1285,7 +1287,7 @@ extern "C" int snvrag_head2_bwd(int64_t M, int K, const float* g, const void* x,
                        (float*)ws);
     SNV_LAUNCH_CHECK();
     // rows of dW = "dg" (columns < K) and "db" (columns >= K) of the LayerNorm partial-sum kernel
-    hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * K, 16)), dim3(256), 0, st, nblk, K, (const float*)ws, dw,
+    hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(2 * K, 16)), dim3(1024), 0, st, nblk, K, (const float*)ws, dw,
                        dw + K, accumulate);
     SNV_LAUNCH_CHECK();
   }
@@ -1315,7 +1317,7 @@ extern "C" int snvrag_tokgrad(int64_t M, int V, int D, int padding_idx, const in
   SNV_LAUNCH_CHECK();
   // the V x D partial rows summed in block order: ln_part_sum_kernel over 2 N = V D columns
   const int VD = V * D;                              // even (D even)
-  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(VD, 16)), dim3(256), 0, st, nblk, VD / 2, (const float*)ws, dw,
+  hipLaunchKernelGGL(ln_part_sum_kernel, dim3(cdiv(VD, 16)), dim3(1024), 0, st, nblk, VD / 2, (const float*)ws, dw,
                      dw + VD / 2, 0);
   SNV_LAUNCH_CHECK();
   return 0;
