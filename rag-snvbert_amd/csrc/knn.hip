@@ -42,7 +42,11 @@ __device__ __forceinline__ int gcd_u(int a, int b) {   // a, b >= 0; gcd(0, b) =
 // 48 queries (1.15 ms per step).  delta [nq][n_sites_pad] (sites), cpart [nq][nch]: the chunk's
 // sum of the constant-term contributions (4 wave partials in fixed order: deterministic).
 constexpr int LUT_CH = 64;
-__host__ __device__ inline int lut_nch_max(int n_sites_pad) { return n_sites_pad / LUT_CH + 4; }
+// chunk slots per query: a sequence may run past its window (training: 512 sites in a 1 030-token
+// sequence, padding tokens after <eos>) and the last chunk takes every position past the grid, so
+// the grid covers up to 2 n_sites_pad + 256 positions (with n_sites_pad / 64 + 4 slots that last
+// chunk held 326 positions against 64 and set the launch time: 115 us per training step)
+__host__ __device__ inline int lut_nch_max(int n_sites_pad) { return 2 * n_sites_pad / LUT_CH + 4; }
 
 __global__ __launch_bounds__(256) void lut_delta_kernel(int L, int D, const int64_t* __restrict__ tok_q,
                                                         const float* __restrict__ W, const float* __restrict__ Wp,
