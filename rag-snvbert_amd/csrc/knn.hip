@@ -898,6 +898,9 @@ static int scan_parts(long n_ref) {
   // workgroup per CU per round, no tail round)
   long p = (n_ref + 2047) / 2048;
   if (p >= 256) p = 256 * ((n_ref + 256L * 8192 - 1) / (256L * 8192));
+  // small panels (training: 10 000 haplotypes were 5 ranges = 5 workgroups, 190 us): ranges down
+  // to 64 refs, up to 256 of them, so the scan still spreads over the chip
+  else p = std::min<long>(256, std::max<long>(p, (n_ref + 63) / 64));
   if (p < 1) p = 1;
   if (p > 4096) p = 4096;
   return (int)p;
