@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--layers", type=int, default=12)
     p.add_argument("--heads", type=int, default=12)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    p.add_argument("--level", type=int, default=4, help="curriculum mask level (4 -> 50%%, rare 70%%)")
+    p.add_argument("--level", type=int, default=4, help="curriculum mask level (dataset.py:252 rates [0.3 .. 0.8]: 4 -> 70%%; "
+                        "sites with AF < 0.05 always 70%%)")
     p.add_argument("--f32-leg", type=int, default=2,
                    help="steps of the same batch on the exact-f32 path (bf16-vs-f32 call agreement); 0 = skip")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on host cores (rank 0)")
@@ -326,6 +327,7 @@ def main():
         "knn_queries_per_s": round(knn_qps, 1),
         "masked_snvs_per_step_per_gpu": masked_per_step,
     }
+    from src.dataset import utils as U
     cpu = None
     if args.cpu_baseline:
         cpu = cpu_baseline(args, model, vocab, af_np, ref_af, raw_mask, x, dev)
@@ -336,6 +338,8 @@ def main():
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded AF~Beta(0.3,3) panel + copied queries)",
         "config": {"workload": "configs[2]: v18 embedding-RAG imputation, window=1024 sites (L=1030 tokens), "
                                f"k={k}, {args.n_ref}-haplotype panel resident in HBM, d{args.dims}/L{args.layers}/H{args.heads}",
+                   "mask_level": args.level, "mask_rate": U.MASK_RATES[args.level], "rare_mask_rate": 0.7,
+                   "masked_site_fraction": round(float(raw_mask.mean()), 4),
                    "global_batch": B * world, "seq_len": L, "parallelism": (f"dp{world} + panel sharded {world}-way" if shard is not None
                                                   else f"dp{world} (panel replicated)")},
         "roofline": roofline, "cpu_baseline": cpu, **extra, "precision_parity": precision, "train": train,

@@ -38,7 +38,8 @@ def parse_args(argv=None):
     p = argparse.ArgumentParser(description="v18 embedding-RAG imputation (MI355X)")
     for name in ("ref_panel", "infer_dataset", "infer_panel", "freq_path", "type_path", "pop_path", "pos_path"):
         p.add_argument(f"--{name}", type=str, default=None)
-    p.add_argument("-c", "--check_point", type=str, default=None, help="state_dict checkpoint (weights_only load)")
+    p.add_argument("-c", "--check_point", type=str, default=None,
+                   help="the reference's pickled model or a state_dict (read without executing pickled code)")
     p.add_argument("-o", "--output_path", type=str, default="output/infer")
     p.add_argument("--chrom", type=str, default="21")
     p.add_argument("-d", "--dims", type=int, default=384)
@@ -240,9 +241,10 @@ def infer(argv=None):
     torch.manual_seed(args.seed)          # every rank (and every run) builds the same random-init weights
     model = build_model(len(vocab), args.dims, args.layers, args.attn_heads)
     if args.check_point:
-        ck = torch.load(args.check_point, map_location="cpu", weights_only=True)
-        sd = ck.get("model", ck) if isinstance(ck, dict) else ck
-        sd = {k.replace("module.", ""): v for k, v in sd.items()}
+        # a trainer checkpoint of either build: the reference's pickled module (its classes
+        # stubbed, nothing executed), a state_dict / {'state_dict'} / {'model'} (model/checkpoint.py)
+        from .model.checkpoint import load_state_dict_any
+        sd = load_state_dict_any(args.check_point)
         # strict: a missing or renamed key must not silently impute with random-init weights
         # (the reference loads with strict=False, infer_embedding_rag.py:99)
         model.load_state_dict(sd, strict=True)

@@ -325,8 +325,17 @@ class BERTTrainerWithValidationOptimized:
         return path
 
     def load(self, path: str) -> int:
-        ck = torch.load(path, map_location="cpu", weights_only=True)
-        sd = ck["model"] if "model" in ck else ck
+        """Resume (train_embedding_rag.py:155-191).  A checkpoint of this trainer restores the
+        weights and the optimizer / schedule / early-stopping / sampler state; the reference's
+        formats (a pickled BERTFoundationModel, a state_dict or {'state_dict': ...}, optional
+        ``module.`` prefixes) restore the weights, read by ``model.checkpoint`` without
+        executing any pickled class."""
+        from ..model.checkpoint import load_state_dict_any
+        if torch.serialization.get_unsafe_globals_in_checkpoint(path):
+            ck = {"model": load_state_dict_any(path)}
+        else:
+            ck = torch.load(path, map_location="cpu", weights_only=True)
+        sd = ck["model"] if "model" in ck else ck.get("state_dict", ck)
         sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
         self.model.load_state_dict(sd)
         self.flat.sync_mirror()

@@ -432,6 +432,21 @@ def run_infer_case(name, d, layers, heads, n_sites, n_samples, n_ref_samples, k,
           f"min kth margin h1={res['kth_margin_h1'].min():.3g} h2={res['kth_margin_h2'].min():.3g}")
 
 
+def pickled_module_case():
+    """The checkpoint object the reference trainer writes (pretrain_with_val_optimized.py:531-536:
+    ``torch.save(self.model.cpu(), path)``, a pickled BERTFoundationModel naming the reference's
+    classes) for the fwd_tiny weights (d64 / 2 layers / 2 heads, seed 0), plus the same model's
+    state_dict as arrays for the converter test (tests/test_checkpoint_cpu.py)."""
+    vocab = ref_vocab()
+    model, digest = build_model(64, 2, 2, len(vocab), 0)
+    model.train()                                  # as saved mid-training
+    torch.save(model.cpu(), OUT / "ref_module_tiny.pth")
+    sd = {k: v.detach().numpy() for k, v in model.state_dict().items()}
+    np.savez_compressed(OUT / "ref_module_tiny_sd.npz", keys=np.array(json.dumps(list(sd))), digest=np.array(digest),
+                        **{f"t{i}": v for i, v in enumerate(sd.values())})
+    print(f"ref_module_tiny: {len(sd)} tensors digest={digest}")
+
+
 def _kth_margin(dist, k):
     s = np.sort(dist, 1)
     return (s[:, k] - s[:, k - 1]) if s.shape[1] > k else np.full(s.shape[0], np.inf)
@@ -471,7 +486,8 @@ def masks_fixture():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag", "infer", "infer256", "infer384", "sweep"]
+    which = sys.argv[1:] or ["data", "tiny", "small", "full", "norag", "infer", "infer256", "infer384", "sweep",
+                             "pickled"]
     if "data" in which:
         masks_fixture()
     if "tiny" in which:
@@ -494,6 +510,8 @@ if __name__ == "__main__":
         # the v18 model shape (d384 / 12 layers / 12 heads) through the whole imputation path
         run_infer_case("infer_c5_d384", d=384, layers=12, heads=12, n_sites=1300, n_samples=4, n_ref_samples=24,
                        k=2, batch_size=8, seed=8)
+    if "pickled" in which:
+        pickled_module_case()
     if "sweep" in which:
         # C5 mask sweep end points (10 % and 90 % of the panel sites missing from the target)
         for rate, tag in ((0.1, "m10"), (0.9, "m90")):

@@ -223,6 +223,35 @@ _MAIN_ARGS = ["--synthetic", "8", "--synthetic_sites", "300", "--synthetic_windo
               "--warmup_steps", "1"]
 
 
+def _record_samples(rec):
+    """Per train / val sample (keyed by its token and mask bytes): the retrieved neighbours of both
+    haplotypes and the sample's three focal-loss parts — so a mismatch of the epoch rows below
+    names the samples and says whether retrieval or the forward moved (tools/ddp_diag.py)."""
+    import hashlib
+    from src.main import pretrain_with_val_optimized as T
+    cls = T.BERTTrainerWithValidationOptimized
+    orig_epoch, orig_loss, state = cls._run_epoch, cls.loss, {}
+
+    def run_epoch(self, epoch, dataloader, train=True):
+        state.update(epoch=epoch, train=train)
+        return orig_epoch(self, epoch, dataloader, train)
+
+    def loss(self, output, data):
+        r = orig_loss(self, output, data)
+        with torch.no_grad():
+            m = data["mask"].bool()
+            for i in range(m.shape[0]):
+                key = hashlib.sha1(b"".join(data[k][i].cpu().numpy().tobytes() for k in ("hap_1", "hap_2", "mask")))
+                parts = [float(self.hap_criterion(output[j][i:i + 1], data[lab][i:i + 1], m[i:i + 1]))
+                         for j, lab in ((0, "hap_1_label"), (1, "hap_2_label"))]
+                parts.append(float(self.gt_criterion(output[2][i:i + 1], data["gt_label"][i:i + 1], m[i:i + 1])))
+                idx = [data[k][i].cpu().tolist() if k in data else None for k in ("rag_idx_h1", "rag_idx_h2")]
+                rec[(state["epoch"], state["train"], key.hexdigest()[:16])] = (idx, parts)
+        return r
+    cls._run_epoch, cls.loss = run_epoch, loss
+    return lambda: setattr(cls, "_run_epoch", orig_epoch) or setattr(cls, "loss", orig_loss)
+
+
 def _main_worker(rank, world, port, out, q):
     import faulthandler
     faulthandler.dump_traceback_later(250, exit=True)
@@ -231,12 +260,14 @@ def _main_worker(rank, world, port, out, q):
                       LOCAL_RANK="0")
     try:
         from src import train_embedding_rag
+        rec = {}
+        _record_samples(rec)
         tr = train_embedding_rag.main(_MAIN_ARGS + ["--train_batch_size", "2", "--val_batch_size", "1",
                                                     "--dist_backend", "gloo", "--panel", "sharded",
                                                     "--metrics_csv", os.path.join(out, "m.csv"),
                                                     "--output_path", os.path.join(out, f"r{rank}", "model")])
         q.put((rank, dict(epochs=len(tr.epoch_metrics), best=tr.best_val_metric, no_imp=tr.epochs_no_improve,
-                          bn=[b.detach().cpu().numpy() for b in tr.model.buffers()])))
+                          bn=[b.detach().cpu().numpy() for b in tr.model.buffers()], samples=rec)))
     except Exception:
         q.put((rank, traceback.format_exc()))
     finally:
@@ -265,9 +296,20 @@ def test_train_main_two_ranks_global_metrics_and_early_stop(tmp_path):
     assert len(ddp) == got[0]["epochs"] and got[0]["epochs"] < 2 * 3   # stopped early (patience 1)
     from src import train_embedding_rag
     single = tmp_path / "single"
-    tr = train_embedding_rag.main(_MAIN_ARGS + ["--train_batch_size", "4", "--val_batch_size", "2",
-                                                "--metrics_csv", str(single / "m.csv"),
-                                                "--output_path", str(single / "model")])
+    one = {}
+    restore = _record_samples(one)
+    try:
+        tr = train_embedding_rag.main(_MAIN_ARGS + ["--train_batch_size", "4", "--val_batch_size", "2",
+                                                    "--metrics_csv", str(single / "m.csv"),
+                                                    "--output_path", str(single / "model")])
+    finally:
+        restore()
+    # per sample first: the same neighbours and the same loss parts as the one-process run
+    two = {**got[0]["samples"], **got[1]["samples"]}
+    assert sorted(two) == sorted(one), (len(two), len(one))
+    bad = [(k, two[k], one[k]) for k in sorted(one)
+           if two[k][0] != one[k][0] or not np.allclose(two[k][1], one[k][1], rtol=1e-5, atol=1e-6)]
+    assert not bad, f"{len(bad)} samples differ (epoch, train, key): (two-rank idx, parts) vs one process: {bad[:4]}"
     ref = _rows(single / "m.csv")
     assert len(ref) == len(ddp) and len(tr.epoch_metrics) == got[0]["epochs"]
     for a, b in zip(ddp, ref):

@@ -235,3 +235,24 @@ def test_infer_cli_two_ranks_writes_single_process_output(tmp_path):
     for k in b.files:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert (tmp_path / "ddp" / "imputed.vcf").read_text() == (tmp_path / "one" / "imputed.vcf").read_text()
+
+
+@pytest.mark.timeout(300)
+def test_infer_cli_loads_reference_pickled_module(tmp_path):
+    """``--check_point`` given the reference trainer's own checkpoint object (a pickled
+    BERTFoundationModel, tests/golden/ref_module_tiny.pth, infer_embedding_rag.py:93-103) imputes
+    exactly what the converted state_dict file does, and not what the random-init weights do."""
+    import os
+    from src.infer_embedding_rag import infer
+    from src.model.checkpoint import load_state_dict_any
+    pth = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_module_tiny.pth")
+    torch.save(load_state_dict_any(pth), tmp_path / "sd.pt")
+    args = ["--synthetic", "4", "--synthetic_sites", "1020", "--synthetic_ref", "24", "-d", "64", "-l", "2", "-a", "2",
+            "-b", "4", "--k_retrieve", "3", "--mask_rate", "0.5", "--no_vcf"]
+    infer(args + ["-o", str(tmp_path / "pickled"), "--check_point", pth])
+    infer(args + ["-o", str(tmp_path / "sd"), "--check_point", str(tmp_path / "sd.pt")])
+    infer(args + ["-o", str(tmp_path / "init")])
+    a, b, c = (np.load(tmp_path / n / "imputed.npz") for n in ("pickled", "sd", "init"))
+    for k in b.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert not np.array_equal(a["hap1"], c["hap1"])
