@@ -31,7 +31,7 @@ namespace snvrag {
 constexpr int TL_FRAG = 1024;               // one A fragment: 32 rows x 16 k bf16
 constexpr int TL_SLAB = 16 * TL_FRAG;
 constexpr int TL_NSLOT = 9;                 // ring slots (144 KiB)
-constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead (4: 1.634 ms, 8: 1.659 ms at M = 527360)
+constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead (r3: 4: 1.634 ms, 8: 1.659; r5: 8 faster, launch_tail)
 constexpr int TL_ROWS = 128;
 constexpr int TL_VEC_LDS = 11 * 1024;       // b1 [4D] + g1, be1, b_o [D] (f32, D <= 384)
 
@@ -92,6 +92,20 @@ __device__ __forceinline__ int tl_lane() {
 // x + x of the lane 32 apart (the row reductions over the two lane halves)
 __device__ __forceinline__ float tl_xsum32(float x) {
   return x + __int_as_float(__builtin_amdgcn_ds_bpermute((tl_lane() ^ 32) << 2, __float_as_int(x)));
+}
+
+// 16 consecutive floats of an LDS table at byte address `addr` (this lane's features 16 hh .. +15
+// of a 32-feature tile): reads and their wait in ONE asm statement, so the compiler can neither
+// hoist them nor keep whole tables live in registers across a phase (tailp_kernel's epilogues)
+__device__ __forceinline__ void tl_ld16(uint32_t addr, float (&v)[16]) {
+  u32x4 r[4];
+  asm volatile(
+      "ds_read_b128 %0, %4 offset:0\n ds_read_b128 %1, %4 offset:16\n ds_read_b128 %2, %4 offset:32\n"
+      " ds_read_b128 %3, %4 offset:48\n s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "v"(addr));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = __uint_as_float(r[i >> 2][i & 3]);
 }
 
 // wait until at most `younger` (<= MAXY) slabs of this wave (4 LDS-DMA instructions each) are in flight
@@ -613,6 +627,473 @@ void tail_kernel(TailArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// PERSISTENT block tail (PRE mode, the engine's path): one workgroup per CU loops over 128-row
+// tiles (tile = blockIdx.x, + gridDim.x, ...) with ONE continuous LDS-DMA ring across them.  Per
+// tile the ring streams, in consumption order,
+//   A  the tile's attention rows  (KS / 4 slabs; wave w's pieces = its 32 rows, 4 k-steps each)
+//   Wo the W_o' fragments         (NPRE slabs)
+//   R  the tile's residual rows x (KS / 4 slabs; features 32 T + 16 hh + 8 h2 per piece)
+//   W1 / W2' chunk blocks         (NCH x SPC slabs, the per-workgroup rotation of tail_kernel)
+// so the activations of tile t + 1 arrive by DMA while tile t finishes its FFN, instead of every
+// workgroup waiting on a 192 KB HBM burst of its own before its first MFMA (tail_kernel: the
+// prologue was 12 % of a wave's cycles, the ring drain + epilogue table loads another ~4 %).  The
+// epilogue's vector tables stay in LDS for the whole launch (8-slot ring: 128 KiB + 11 D floats).
+// The arithmetic is tail_kernel's, in the same order: outputs are bit-identical to it.
+// LDS-DMA is issued by inline asm (dma_x4): the compiler sees no LDS stores, so its own LDS reads
+// (vector tables, A / R pieces) get no waits on the weight stream; the ordering is this kernel's
+// counted vmcnt + barrier.  The 2 NT epilogue stores of a tile are buffer stores (rows >= M fall
+// outside the resource), so every tile issues the same vector-memory count and the first syncs of
+// the next tile wait with that count added.
+constexpr int TP_NSLOT = 8;
+
+// STAMP (diagnostics, a separate instantiation): s_memtime at the phase boundaries of each tile,
+// the last tile's kept in SGPRs and written out at exit: [workgroup][wave][TP_NSTAMP] u32
+constexpr int TP_NSTAMP = 8;
+template <int D, bool STAMP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void tailp_kernel(TailArgs p) {
+  using S = TailShape<D>;
+  constexpr int NT = S::NT, KS = S::KS;
+  constexpr int NA = KS / 4;                          // A (and R) slabs per tile
+  // per tile, NA groups of GS slabs: [A_g, W_o' (NT / 4 slabs: k-steps 4 g .. 4 g + 3), R_g],
+  // then the FFN: the activation slabs are consumed beside the out-projection's MFMAs, never
+  // several in a row (a run of MFMA-free slabs would use up the ring's lookahead)
+  constexpr int WPG = NT / 4;                         // W_o' slabs per group
+  constexpr int GS = WPG + 2;
+  constexpr int Q_FFN = NA * GS;
+  static_assert(S::NPRE == NA * WPG, "W_o' groups");
+  constexpr int NQ = Q_FFN + S::NCH * S::SPC;         // slabs per tile
+  constexpr int AHEAD = TP_NSLOT - 2;                 // sync(g) issues slab g + AHEAD
+  constexpr int RING = TP_NSLOT * TL_SLAB;
+  constexpr int VM = 4 * (TP_NSLOT - 3);              // vmcnt at a sync: the younger slabs in flight
+  constexpr int NST = 2 * NT;                         // epilogue stores per lane and tile
+  constexpr int H = S::FW1 / 16;                      // slabs per W1 / W2' block
+  constexpr int NB2 = 2 * S::NCH;                     // FFN blocks per tile
+  static_assert(VM + NST <= 63, "vmcnt range");
+  static_assert(KS % 4 == 0 && H == S::FW2 / 16, "whole A / R slabs, equal W1 / W2' blocks");
+  // FFN block layout of a tile: phase1(0), phase1(1), phase2, phase1(2), phase2, then a runtime
+  // loop of 4 blocks per iteration over chunks 3 .. NCH - 4, its last iteration peeled (compile-time
+  // issue targets there: the last block W2'(N-1) breaks the loop's block pattern), then
+  // phase1(NCH - 1), phase2, phase2
+  // loop iterations (chunk pairs 3 .. NCH - 2): the runtime ones are those whose issue targets
+  // (AHEAD slabs past their last part) stay inside plain blocks; the rest are unrolled
+  constexpr int NIT = (S::NCH - 4) / 2;
+  constexpr int LIT_MAX = ((NB2 - 1) * H - 1 - AHEAD - 9 * H);
+  constexpr int LOOP_IT = LIT_MAX < 0 ? 0 : (LIT_MAX / (4 * H) + 1 < NIT ? LIT_MAX / (4 * H) + 1 : NIT);
+  static_assert(S::NCH % 2 == 0 && S::NCH >= 6, "chunk pairs");
+  constexpr int Q_LOOP = Q_FFN + 5 * H;               // first slab of the loop
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  float* sv = reinterpret_cast<float*>(smem + RING);  // [b1 4D | b2' | c1 | g2 | be2 | g1 | be1 | b_o]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int hh = lane >> 5;
+  const int M = p.M;
+  const int ntiles = (M + TL_ROWS - 1) / TL_ROWS;
+  const int G = gridDim.x;
+
+  for (int i = tid; i < 8 * D; i += 256) sv[i] = p.vec[i];
+  for (int i = tid; i < D; i += 256) { sv[8 * D + i] = p.g1[i]; sv[9 * D + i] = p.be1[i]; sv[10 * D + i] = p.b_o[i]; }
+  // first-tile stagger (tail_kernel's desync), only for the workgroups with one tile fewer: their
+  // slack absorbs it
+  if (p.desync > 0 && ntiles % G != 0 && (int)blockIdx.x >= ntiles % G && ntiles >= 8 * G) {
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
+
+  // ---- issue side.  Every issue target is a compile-time tile-relative slab index (the loop's
+  // are compile-time offsets from the iteration's runtime block base), so an issue is a few scalar
+  // adds: the weight stream offset of an FFN block is (NPRE + H m) slabs with m = 2 rot + s + d(s)
+  // mod 2 NCH (tail_kernel's rotated order), the activation pieces through a resource starting at
+  // the tile's rows (rows >= M, and tiles >= ntiles, read as zeros).
+  const int rot2 = 2 * (int)(blockIdx.x % S::NCH);
+  const i32x4 wrs = dma_rsrc(p.ws, (long)S::NSLAB * TL_SLAB);
+  const uint32_t ring_lds = lds_addr(ring) + wave * 4 * TL_FRAG;
+  const int wave_off = wave * 4 * TL_FRAG;
+  int is_slot = 0;                                    // ring slot (byte offset) of the next issue
+  long tb = (long)blockIdx.x * TL_ROWS * D * 2;       // byte offset of the current tile's rows
+  constexpr int TB_STEP = TL_ROWS * D * 2;
+  // wave-uniform values made opaque at each use: otherwise hipcc precomputes every issue's
+  // offset (each a loop-invariant scalar) before the tile loop and spills ~250 SGPRs
+  auto opq = [](auto v) { asm volatile("" : "+s"(v)); return v; };
+  // A / R piece j of this wave: 8 of its rows x the slab's 128 B of each (4 k-steps / 2 residual
+  // tiles), i.e. 8 whole 128-B lines per DMA instruction; LDS image [32 rows][128 B] with the
+  // 16-B chunks XOR-swizzled by row & 7 (conflict-free fragment reads): lane l fills row
+  // 8 j + l / 8, slot l % 8, so it loads chunk (l % 8) ^ (row % 8).  From a fresh lane id.
+  auto voff_act = [&](int j) {
+    const int l = tl_lane();
+    return (opq(wave) * 32 + 8 * j + (l >> 3)) * (D * 2) + 16 * ((l & 7) ^ ((l >> 3) & 7));
+  };
+  auto put = [&](const i32x4& rs, int soff, bool act) {
+    const int lds = opq(ring_lds) + is_slot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dma_x4(rs, lds + j * TL_FRAG, act ? voff_act(j) : tl_lane() * 16, act ? soff : soff + j * TL_FRAG);
+    is_slot = is_slot + TL_SLAB == RING ? 0 : is_slot + TL_SLAB;
+  };
+  auto ffn_off = [&](int m) {                         // m in [0, 2 NB2)
+    m = m >= NB2 ? m - NB2 : m;
+    return (S::NPRE * TL_SLAB) + m * (H * TL_SLAB);
+  };
+  // target QG: tile-relative slab (>= NQ: the next tile's); compile-time
+  auto issue_ct = [&](auto q_tag) {
+    constexpr int QG = decltype(q_tag)::value;
+    constexpr bool NEXT = QG >= NQ;
+    constexpr int q = NEXT ? QG - NQ : QG;
+    constexpr int gq = q / GS, rq = q % GS;
+    if constexpr (q < Q_FFN && (rq == 0 || rq == GS - 1)) {
+      // A_g / R_g.  A resource over the tile's rows to the end of the array: the buffer range
+      // check covers voffset, not soffset, so the tile offset goes into the base (rows >= M read
+      // as zeros)
+      const long tbl = NEXT ? opq(tb) + (long)G * TB_STEP : opq(tb);
+      const long left = (long)M * D * 2 - tbl;
+      const char* base = reinterpret_cast<const char*>(rq == 0 ? p.act : p.resid);
+      put(dma_rsrc(base + (left > 0 ? tbl : 0), left > 0 ? left : 0), 128 * gq, true);
+    } else if constexpr (q < Q_FFN) {
+      put(wrs, (gq * WPG + rq - 1) * TL_SLAB + opq(wave_off), false);
+    } else {
+      constexpr int qq = q - Q_FFN, sb = qq / H, jb = qq % H;
+      constexpr int d = (sb == 0 || sb == NB2 - 1) ? 0 : (sb & 1) ? 1 : -1;
+      put(wrs, ffn_off(opq(rot2) + sb + d) + jb * TL_SLAB + opq(wave_off), false);
+    }
+  };
+  // loop target: slab Q_LOOP + AHEAD + 4 H it + C; mloop = rot2 + 4 it (runtime)
+  auto issue_loop = [&](auto c_tag, int mloop) {
+    constexpr int C = decltype(c_tag)::value;
+    constexpr int qq = Q_LOOP + AHEAD - Q_FFN + C, sb = qq / H, jb = qq % H;   // block of iteration 0
+    constexpr int d = (sb & 1) ? 1 : -1;
+    static_assert(sb > 0 && sb + 4 * (LOOP_IT - 1) < NB2 - 1, "loop targets are plain blocks");
+    put(wrs, ffn_off(mloop + sb + d) + jb * TL_SLAB + opq(wave_off), false);
+  };
+  // the vector tables landed (plain loads), then the first AHEAD slabs
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  tl_unroll([&](auto gc) { issue_ct(gc); }, std::make_integer_sequence<int, AHEAD>{});
+
+  // sync before reading slab g: it has landed (this wave's pieces: vmcnt; the others': barrier)
+  auto wait_bar = [&](auto vm_tag) {
+    constexpr int V = decltype(vm_tag)::value;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  using VMc = std::integral_constant<int, VM>;
+  using VMs = std::integral_constant<int, VM + NST>;
+  // the syncs of a tile's slabs 1 .. AHEAD: issued before the previous tile's epilogue stores (the
+  // first tile issues as many no-op stores at the same point), so those are among the younger
+  auto vm_of = [](auto g_tag) {
+    constexpr int g = decltype(g_tag)::value;
+    return std::conditional_t<(g >= 1 && g <= AHEAD), VMs, VMc>{};
+  };
+  // sync of compile-time slab G (then slab G + AHEAD goes into the slot of slab G - 2)
+  auto sync_ct = [&](auto g_tag, auto vm_tag) {
+    wait_bar(vm_tag);
+    issue_ct(std::integral_constant<int, decltype(g_tag)::value + AHEAD>{});
+  };
+
+  int rd_slot = 0;
+  auto rdA = [&](auto j_tag, auto fi_tag) -> u32x4 {
+    constexpr int j = decltype(j_tag)::value, fi = decltype(fi_tag)::value;
+    int so = rd_slot + j * TL_SLAB;
+    so = so >= RING ? so - RING : so;
+    return *reinterpret_cast<const u32x4*>(ring + so + lane * 16 + fi * TL_FRAG);
+  };
+  // B fragment j of this wave's rows in the current A / R slab (features 64 slab + 32 (j / 2) +
+  // 16 hh + 8 (j % 2) .. + 7 of row ln: 16-B chunk 4 (j / 2) + 2 hh + j % 2 of the row's 128 B)
+  auto rdOwn = [&](int j) -> u32x4 {
+    const int l = tl_lane(), ln = l & 31;
+    const int c = 4 * (j >> 1) + 2 * (l >> 5) + (j & 1);
+    return *reinterpret_cast<const u32x4*>(ring + rd_slot + opq(wave_off) + ln * 128 + 16 * (c ^ (ln & 7)));
+  };
+  auto advance = [&](int n) {
+    rd_slot += n * TL_SLAB;
+    rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
+  };
+
+  constexpr int PF = TL_PF_DEFAULT;
+  u32x4 a[PF];
+  // consume a part of NF fragments (whole slabs) starting at tile slab G0 (compile-time), or, with
+  // G0 < 0, the loop part at block offset P of the iteration whose issue base is mloop
+  auto run = [&](auto nf_tag, auto g0_tag, auto p_tag, int mloop, auto&& mma, auto stop_tag) {
+    constexpr int NF = decltype(nf_tag)::value;
+    constexpr int G0 = decltype(g0_tag)::value;
+    constexpr int P = decltype(p_tag)::value;
+    constexpr bool STOP = decltype(stop_tag)::value;
+    static_assert(NF % 16 == 0, "parts are whole slabs");
+    tl_unroll([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      const u32x4 cur = a[f % PF];
+      if constexpr ((f & 15) == 16 - PF) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G0 >= 0) {
+          wait_bar(vm_of(std::integral_constant<int, G0 + (f >> 4) + 1>{}));
+          issue_ct(std::integral_constant<int, G0 + (f >> 4) + 1 + AHEAD>{});
+        } else {
+          wait_bar(VMc{});
+          issue_loop(std::integral_constant<int, P + (f >> 4) + 1>{}, mloop);
+        }
+      }
+      mma(fc, cur);
+      constexpr int qn = f + PF;
+      if constexpr (!STOP || qn < NF)
+        a[f % PF] = rdA(std::integral_constant<int, (qn >> 4)>{}, std::integral_constant<int, (qn & 15)>{});
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }, std::make_integer_sequence<int, NF>{});
+    advance(NF / 16);
+  };
+  auto prime = [&]() {
+    tl_unroll([&](auto ic) { a[decltype(ic)::value] = rdA(std::integral_constant<int, 0>{}, ic); },
+              std::make_integer_sequence<int, PF>{});
+  };
+  using I0 = std::integral_constant<int, 0>;
+
+  // table t, tile T: this lane's 16 floats (features 32 T + 16 hh + i)
+  auto tab = [&](int t, int T, float (&v)[16]) {
+    tl_ld16(opq(tl_lds(reinterpret_cast<const char*>(sv))) + 4 * (t * D + 32 * T) + 64 * (tl_lane() >> 5), v);
+  };
+  enum { TB_B2 = 4, TB_C1 = 5, TB_G2 = 6, TB_BE2 = 7, TB_G1 = 8, TB_BE1 = 9, TB_BO = 10 };
+  const long out_bytes = (long)M * D * 2;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.out, (short)0, (int)(out_bytes < 0x7fffffffL ? out_bytes : 0x7fffffffL), 0x00020000);
+
+  uint32_t st[TP_NSTAMP] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+  for (int t = blockIdx.x; t < ntiles; t += G, tb += (long)G * TB_STEP) {
+    auto mark = [&](int i) {
+      if constexpr (STAMP) st[i] = (uint32_t)__builtin_amdgcn_s_memtime();
+    };
+    mark(0);
+    // ---- first tile: slab 0 and the stand-ins for the previous tile's epilogue stores
+    if (t == (int)blockIdx.x) {
+      sync_ct(std::integral_constant<int, 0>{}, VMc{});
+      const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NST; ++i) __builtin_amdgcn_raw_buffer_store_b128(a[0], nrs, 0, 0, 0);   // (dropped)
+    }
+    mark(1);
+    // ---- ao = b_o + att W_o'^T, group by group: A_g (the attention rows' k-steps 4 g .. 4 g + 3 as
+    // B fragments), the group's W_o' slabs, then R_g (residual tiles 2 g, 2 g + 1) into rr
+    f32x16 ao[NT];
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float bo[16];
+      tab(TB_BO, T, bo);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ao[T][i] = bo[i];
+    }
+    u32x4 rr[2 * NT];
+    tl_unroll([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      constexpr int QA = g * GS;
+      if constexpr (g > 0) sync_ct(std::integral_constant<int, QA>{}, vm_of(std::integral_constant<int, QA>{}));
+      u32x4 xa[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xa[j] = rdOwn(j);
+      advance(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // in registers before the slot recycles
+      sync_ct(std::integral_constant<int, QA + 1>{}, vm_of(std::integral_constant<int, QA + 1>{}));
+      prime();
+      run(std::integral_constant<int, 4 * NT>{}, std::integral_constant<int, QA + 1>{}, I0{}, 0,
+          [&](auto fc, const u32x4& A) {
+            constexpr int f = decltype(fc)::value;
+            ao[f % NT] = mfma32(A, xa[f / NT], ao[f % NT]);
+          }, std::true_type{});
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[4 * g + j] = rdOwn(j);
+      advance(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }, std::make_integer_sequence<int, NA>{});
+    mark(2);
+    sync_ct(std::integral_constant<int, Q_FFN>{}, vm_of(std::integral_constant<int, Q_FFN>{}));   // the first FFN slab
+    mark(3);
+    // ---- x1 = LN1(ao + x) -> xr
+    u32x4 xr[KS];
+    {
+      float sum = 0.f, sq = 0.f;
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float v = ao[T][i] + tl_bf(rr[2 * T + (i >> 3)], i & 7);
+          ao[T][i] = v;
+          sum += v;
+          sq = fmaf(v, v, sq);
+        }
+#pragma unroll
+      for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(ao[T]));
+      asm volatile("" ::: "memory");
+      sum = tl_xsum32(sum);
+      sq = tl_xsum32(sq);
+      const float mean = sum * (1.0f / D);
+      const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        float y[16], g1v[16], be1v[16];
+        tab(TB_G1, T, g1v);
+        tab(TB_BE1, T, be1v);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) y[i] = (ao[T][i] - mean) * rstd * g1v[i] + be1v[i];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          xr[2 * T + h2] = u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                                 tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])};
+      }
+    }
+    prime();
+#pragma unroll
+    for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(xr[k]));
+
+    mark(4);
+    // ---- FFN (tail_kernel's software pipeline)
+    f32x16 acc[NT];
+    float st1 = 0.f, st2 = 0.f;
+    f32x16 h0[2], h1[2];
+    u32x4 hf[4];
+    auto epi_pair = [&](const f32x16 (&hc)[2], int m) {
+      const int tt = m >> 3, i = 2 * (m & 7);
+      float x0 = hc[tt][i], x1 = hc[tt][i + 1];
+      x0 = tl_lrelu(x0);
+      x1 = tl_lrelu(x1);
+      st1 += x0 + x1;
+      st2 = fmaf(x0, x0, fmaf(x1, x1, st2));
+      hf[2 * tt + (i >> 3)][(i & 7) >> 1] = tl_pack2(x0, x1);
+    };
+    // G0: the part's first tile slab (compile-time) or < 0 for a loop part at block offset P
+    auto phase1 = [&](int k, f32x16 (&hn)[2], const f32x16 (&hc)[2], auto epi_tag, auto g0_tag, auto p_tag,
+                      int mloop) {
+      constexpr bool EPI = decltype(epi_tag)::value;
+      int c = k + (int)((unsigned)opq(rot2) >> 1);
+      c = c >= S::NCH ? c - S::NCH : c;
+      const uint32_t b1 = opq(tl_lds(reinterpret_cast<const char*>(sv))) + 16 * (tl_lane() >> 5) + 256 * c;
+      u32x4 bv[8];
+      asm volatile(
+          "ds_read_b128 %0, %8 offset:0\n ds_read_b128 %1, %8 offset:32\n ds_read_b128 %2, %8 offset:64\n"
+          " ds_read_b128 %3, %8 offset:96\n ds_read_b128 %4, %8 offset:128\n ds_read_b128 %5, %8 offset:160\n"
+          " ds_read_b128 %6, %8 offset:192\n ds_read_b128 %7, %8 offset:224\n s_waitcnt lgkmcnt(0)"
+          : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3]), "=&v"(bv[4]), "=&v"(bv[5]), "=&v"(bv[6]),
+            "=&v"(bv[7])
+          : "v"(b1));
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hn[tt][4 * r + e] = __uint_as_float(bv[4 * tt + r][e]);
+      run(std::integral_constant<int, S::FW1>{}, g0_tag, p_tag, mloop, [&](auto fc, const u32x4& A) {
+        constexpr int f = decltype(fc)::value;
+        hn[f & 1] = mfma32(A, xr[f >> 1], hn[f & 1]);
+        constexpr int SP = S::FW1 / 16;
+        if constexpr (EPI && f % SP == 0) epi_pair(hc, f / SP);
+      }, std::false_type{});
+    };
+    auto phase2 = [&](auto first_tag, auto stop_tag, auto g0_tag, auto p_tag, int mloop) {
+      constexpr bool FIRST = decltype(first_tag)::value;
+      run(std::integral_constant<int, S::FW2>{}, g0_tag, p_tag, mloop, [&](auto fc, const u32x4& A) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (FIRST && f < NT) acc[f] = mfma32(A, hf[0], f32x16{});
+        else acc[f % NT] = mfma32(A, hf[f / NT], acc[f % NT]);
+      }, stop_tag);
+    };
+    using F_ = std::false_type;
+    using T_ = std::true_type;
+    auto at = [](auto blk) { return std::integral_constant<int, Q_FFN + decltype(blk)::value * H>{}; };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    using B2 = std::integral_constant<int, 2>;
+    using B3 = std::integral_constant<int, 3>;
+    using B4 = std::integral_constant<int, 4>;
+    phase1(0, h0, h1, F_{}, at(B0{}), I0{}, 0);
+    phase1(1, h1, h0, T_{}, at(B1{}), I0{}, 0);
+    phase2(T_{}, F_{}, at(B2{}), I0{}, 0);
+    phase1(2, h0, h1, T_{}, at(B3{}), I0{}, 0);
+    phase2(F_{}, F_{}, at(B4{}), I0{}, 0);
+    using LP = std::integral_constant<int, -1>;
+    int mloop = rot2;
+#pragma unroll 1
+    for (int it = 0; it < LOOP_IT; ++it, mloop += 4) {
+      const int k = 3 + 2 * it;
+      phase1(k, h1, h0, T_{}, LP{}, std::integral_constant<int, 0>{}, mloop);
+      phase2(F_{}, F_{}, LP{}, std::integral_constant<int, H>{}, mloop);
+      phase1(k + 1, h0, h1, T_{}, LP{}, std::integral_constant<int, 2 * H>{}, mloop);
+      phase2(F_{}, F_{}, LP{}, std::integral_constant<int, 3 * H>{}, mloop);
+    }
+    // the remaining iterations, unrolled: compile-time issue targets (they reach W2'(N-1) and
+    // the next tile)
+    tl_unroll([&](auto ic) {
+      constexpr int it = LOOP_IT + decltype(ic)::value;
+      constexpr int kb = 5 + 4 * it;                      // its first block
+      constexpr int k = 3 + 2 * it;
+      phase1(k, h1, h0, T_{}, at(std::integral_constant<int, kb>{}), I0{}, 0);
+      phase2(F_{}, F_{}, at(std::integral_constant<int, kb + 1>{}), I0{}, 0);
+      phase1(k + 1, h0, h1, T_{}, at(std::integral_constant<int, kb + 2>{}), I0{}, 0);
+      phase2(F_{}, F_{}, at(std::integral_constant<int, kb + 3>{}), I0{}, 0);
+    }, std::make_integer_sequence<int, NIT - LOOP_IT>{});
+    static_assert(5 + 4 * NIT == NB2 - 3, "block schedule");
+    phase1(S::NCH - 1, h1, h0, T_{}, at(std::integral_constant<int, NB2 - 3>{}), I0{}, 0);
+    phase2(F_{}, F_{}, at(std::integral_constant<int, NB2 - 2>{}), I0{}, 0);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) epi_pair(h1, m);
+    // the last part syncs the next tile's slab 0 and stops reading there
+    phase2(F_{}, T_{}, at(std::integral_constant<int, NB2 - 1>{}), I0{}, 0);
+
+    mark(5);
+    // ---- epilogue: out = LN2(x1 + lrelu(rstd_f acc - rstd_f mean_f c1 + b2'))
+    st1 = tl_xsum32(st1);
+    st2 = tl_xsum32(st2);
+    const float hm = st1 * (1.0f / (4 * D));
+    const float hr = 1.0f / sqrtf(fmaxf(st2 * (1.0f / (4 * D)) - hm * hm, 0.f) + p.eps);
+    float sum = 0.f, sq = 0.f;
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float c1v[16], b2v[16];
+      tab(TB_C1, T, c1v);
+      tab(TB_B2, T, b2v);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float u = hr * fmaf(-hm, c1v[i], acc[T][i]) + b2v[i];
+        u = tl_lrelu(u);
+        const float v = u + tl_bf(xr[2 * T + (i >> 3)], i & 7);
+        acc[T][i] = v;
+        sum += v;
+        sq = fmaf(v, v, sq);
+      }
+    }
+#pragma unroll
+    for (int T = 0; T < NT; ++T) asm volatile("" : "+a"(acc[T]));
+    asm volatile("" ::: "memory");
+    sum = tl_xsum32(sum);
+    sq = tl_xsum32(sq);
+    const float mean = sum * (1.0f / D);
+    const float rstd = 1.0f / sqrtf(fmaxf(sq * (1.0f / D) - mean * mean, 0.f) + p.eps);
+    const float nmr = -mean * rstd;
+    const int row_off = (int)(((long)t * TL_ROWS + wave * 32 + (tl_lane() & 31)) * D + 16 * (tl_lane() >> 5)) * 2;
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      float y[16], g2v[16], be2v[16];
+      tab(TB_G2, T, g2v);
+      tab(TB_BE2, T, be2v);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) y[i] = fmaf(fmaf(acc[T][i], rstd, nmr), g2v[i], be2v[i]);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{tl_pack2(y[8 * h2], y[8 * h2 + 1]), tl_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                  tl_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), tl_pack2(y[8 * h2 + 6], y[8 * h2 + 7])},
+            ors, row_off + 64 * T + 16 * h2, 0, 0);
+    }
+    mark(6);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the ring overrun has landed before exit
+  if constexpr (STAMP) {
+    st[7] = (uint32_t)__builtin_amdgcn_s_memtime();
+    uint32_t* o = reinterpret_cast<uint32_t*>(p.stamps) + ((long)blockIdx.x * 4 + wave) * TP_NSTAMP;
+#pragma unroll
+    for (int i = 0; i < TP_NSTAMP; ++i) o[i] = st[i];
+  }
+}
+
 // One thread per 16-byte piece (8 bf16) of the stream: slab order = consumption order
 // (W_o' fragments, then per 64-unit chunk: W1 then W2').  Fragment lane l = (m = l % 32,
 // kh = l / 32) holds A[m][8 kh .. 8 kh + 7].
@@ -671,12 +1152,48 @@ static int launch_proj(const TailArgs& a, hipStream_t s) {
 
 static unsigned long long* g_tail_stamps = nullptr;   // snvrag_tail_stamps (diagnostics)
 
+static int cu_count() {
+  static int n[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (n[dev] <= 0) {
+    int v = 0;
+    n[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  return n[dev];
+}
+
+template <int D>
+static int launch_tailp(TailArgs a, hipStream_t s) {
+  const long ntiles = cdiv(a.M, TL_ROWS);
+  const int grid = (int)std::min<long>(ntiles, cu_count());
+  const int64_t dz = options().tail_desync;
+  a.desync = ntiles >= 8L * grid ? (dz >= 0 ? (int)dz : 25000 * D / 384 * D / 384) : 0;
+  constexpr size_t lds = (size_t)TP_NSLOT * TL_SLAB + 11 * D * 4;   // ring + [vec 8D | g1 | be1 | b_o]
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  auto kern = tailp_kernel<D>;
+  if (options().tail_variant == 7 && g_tail_stamps) {     // phase stamps (tools/tail_micro.py)
+    kern = tailp_kernel<D, true>;
+    a.stamps = g_tail_stamps;
+  }
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int D, bool PRE>
 static int launch_tail(TailArgs a, hipStream_t s) {
   const int var = (int)options().tail_variant;
-  auto kern = var == 1 ? tail_kernel<D, PRE, 8> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
+  // the persistent kernel (option tail_persist; measured no faster, see tailp_kernel): 32-bit
+  // byte offsets of the in-place rows
+  if constexpr (PRE)
+    if ((var == 0 || var == 7) && options().tail_persist && (long)a.M * D * 2 < 0x7fffffffL) return launch_tailp<D>(a, s);
+  // default: 8 fragments read ahead (r5: 1.530 vs 1.553 ms at PF 4, mean of 5 sessions of
+  // tools/tail_micro.py at M = 527 360; variant 1 = PF 4, the r4 default)
+  auto kern = var == 1 ? tail_kernel<D, PRE, TL_PF_DEFAULT> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
               : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false>
-              : var == 5 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 3> : tail_kernel<D, PRE>;
+              : var == 5 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 3> : tail_kernel<D, PRE, 8>;
   if (var == 4 && D == 384 && g_tail_stamps) {           // phase stamps (tools/tail_micro.py)
     kern = tail_kernel<D, PRE, TL_PF_DEFAULT, 2>;
     a.stamps = g_tail_stamps;

@@ -71,9 +71,10 @@ ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
 xs = c["x"].clone()
 out = torch.empty_like(c["x"])
 fl9, fl8 = 18.0 * M * D * D, 16.0 * M * D * D
-def tail_var(v, desync=-1):
+def tail_var(v, desync=-1, persist=0):
     def fn():
         K.set_option("tail_variant", int(v))
+        K.set_option("tail_persist", int(persist))
         if desync < 0:
             K.set_option("tail_desync", -1)         # the library default
         else:
@@ -84,17 +85,25 @@ def tail_var(v, desync=-1):
 
 for _ in range(30):                                  # clock warm-up before the first timing
     tail_var(0)()
+# persistent kernel (default) == tail_kernel bit for bit at the bench shape
+ya, yb = c["x"].clone(), c["x"].clone()
+tail_var(0, persist=1)()
+K.tail_forward(c["att"], ya, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+tail_var(0)()
+K.tail_forward(c["att"], yb, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+print(f"persistent vs tail_kernel at M = {M}: bitwise equal {torch.equal(ya, yb)}, "
+      f"differing outputs {int((ya != yb).sum())} of {ya.numel()}", flush=True)
 for name, fn, fl in (
-        ("tail.hip PRE", tail_var(0), fl9),
+        ("tailp (persistent)", tail_var(0, persist=1), fl9),
+        ("tailp no desync", tail_var(0, 0, 1), fl9),
+        ("tail_kernel PRE (PF 8, default)", tail_var(0), fl9),
+        ("tail_kernel PRE PF 4", tail_var(1), fl9),
+        ("tailp (again)", tail_var(0, persist=1), fl9),
         ("tail.hip PRE residual at group 3", tail_var(5), fl9),
-        ("tail.hip PRE PF=8", tail_var(1), fl9),
+        ("tail_kernel PRE PF 8 (again)", tail_var(0), fl9),
         ("tail.hip PRE no-DMA (diag)", tail_var(2), fl9),
         ("tail.hip PRE no sched groups", tail_var(3), fl9),
-        ("tail.hip PRE (again)", tail_var(0), fl9),
-        ("tail.hip PRE no desync", tail_var(0, 0), fl9),
-        ("tail.hip PRE desync 12k", tail_var(0, 12000), fl9),
-        ("tail.hip PRE desync 25k", tail_var(0, 25000), fl9),
-        ("tail.hip PRE desync 40k", tail_var(0, 40000), fl9),
+        ("tail.hip PRE no desync", tail_var(0, 0, 0), fl9),
         ("tail.hip FFN only", lambda: (K.set_option("tail_variant", 0),
                                        K.tail_ffn_forward(c["x"], ts, c["vec"], out=out)), fl8)):
     ms = timeit(fn)
@@ -133,3 +142,28 @@ print(f"  workgroup residency: span {span / 100:.1f} us, sum of workgroup lifeti
 order = np.sort(r0 - r0.min()) / 100
 print("  workgroup start times (us) at ranks 0/256/512/.../end: " +
       " ".join(f"{order[i]:.1f}" for i in range(0, nwg, 256)) + f" | last {order[-1]:.1f}", flush=True)
+
+# ---- persistent kernel phase stamps (SNVRAG_TAIL_VARIANT=7): the last tile of every wave
+import ctypes  # noqa: E402
+nbuf = ctypes.create_string_buffer(64)
+n_cu = N.lib().snvrag_device_info(0, nbuf, 64)
+G = min((M + 127) // 128, n_cu)
+print(f"device {nbuf.value.decode()}: {n_cu} CUs -> persistent grid {G}", flush=True)
+stp = torch.zeros(max(G, 1024) * 4 * 8, dtype=torch.int32, device=dev)
+N.lib().snvrag_tail_stamps(stp.data_ptr())
+for _ in range(10):
+    tail_var(0, persist=1)()
+tail_var(7, persist=1)()
+torch.cuda.synchronize()
+N.lib().snvrag_tail_stamps(None)
+K.set_option("tail_variant", 0)
+t = stp[:G * 4 * 8].view(G * 4, 8).cpu().numpy().astype(np.int64) & 0xffffffff
+ph = ["tile start (first tile: slab 0 + no-op stores)", "out-projection groups (A_g, W_o', R_g; 288 MFMA)",
+      "sync of the first FFN slab", "LN1", "FFN (2304 MFMA)", "LN2 + stores"]
+tot = (t[:, 6] - t[:, 0]) % (1 << 32)
+print(f"tailp stamped launch: {G} workgroups, last tile of each wave", flush=True)
+for i, nm in enumerate(ph):
+    d = (t[:, i + 1] - t[:, i]) % (1 << 32)
+    print(f"  {nm:40s} median {np.median(d):9.0f} cyc  p10 {np.percentile(d, 10):9.0f}  p90 {np.percentile(d, 90):9.0f}"
+          f"  ({np.median(d) / np.median(tot):.3f} of the tile)", flush=True)
+print(f"  {'tile total':40s} median {np.median(tot):9.0f} cyc  (MFMA floor 82944)", flush=True)
