@@ -383,7 +383,8 @@ int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
  * the strided view src[i][r * rs[i] + c * cs[i]] of part_rows[i] rows, and writes
  *   kind 0: f32   dst[r * dst_ld + c]
  *   kind 1: bf16  dst[r * dst_ld + c]   (round to nearest even, as the optimizer's bf16 mirror)
- *   kind 2: bf16  snvrag_sgemm_pack of the (rows = N) x (cols = D) matrix (dst_ld unused).
+ *   kind 2: bf16  snvrag_sgemm_pack of the (rows = N) x (cols = D) matrix (dst_ld unused),
+ *   kind 3: bf16  snvrag_gemm256_pack of the (rows = N) x (cols = K) matrix (dst_ld unused).
  * Job j owns the output pieces (8 elements) [piece0, piece0 + pieces); jobs sorted by piece0,
  * piece0[0] = 0, total = the last job's piece0 + pieces.  `jobs` is a DEVICE pointer. */
 typedef struct {
@@ -394,6 +395,18 @@ typedef struct {
   void* dst;
 } snvrag_derive_job_t;
 int snvrag_derive(const snvrag_derive_job_t* jobs, int njobs, int64_t total_pieces, void* stream);
+
+/* Wide-row GEMM (gemm256.hip) for the large-K projections onto N = 384 features of training:
+ * FeedForward's w_2 forward (feed_forward.py:20, K = 4D) and the dX GEMMs with K = 3D / 4D of the
+ * backward of the attention projections and of w_1 (the autograd of pretrain_with_val_optimized.py:
+ * 235).  out bf16 [M, N] (ldo) = A bf16 [M, K] (lda) W^T (+ bias f32 [N]) (+ resid bf16 [M, N]),
+ * f32 accumulation, one rounding.  W bf16 [N, K] (ldw) is packed once into
+ * snvrag_gemm256_pack_bytes(N, K) bytes (or by snvrag_derive kind 3).  N = 384, K % 64 == 0, rows
+ * and pointers 16-byte aligned. */
+size_t snvrag_gemm256_pack_bytes(int N, int K);
+int snvrag_gemm256_pack(int N, int K, const void* w, int64_t ldw, void* out, void* stream);
+int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, int64_t lda, const void* wpacked, const float* bias,
+                           const void* resid, int64_t ld_resid, void* out, int64_t ldo, void* stream);
 
 /* The hap head's Linear(K, 2) (foundation_model.py:25-33 net[2]) in training: x bf16 [M, K],
  * w f32 [2, K], b f32 [2] -> out f32 [M, 2] = x w^T + b.  Backward: dx bf16 [M, K] = g w (optional),

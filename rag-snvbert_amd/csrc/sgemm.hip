@@ -680,6 +680,18 @@ __global__ __launch_bounds__(256) void derive_kernel(const snvrag_derive_job_t* 
     *reinterpret_cast<bf16x8*>((bf16*)J.dst + p * 8) = o;
     return;
   }
+  if (J.kind == 3) {                                  // wide-row GEMM pack (gemm256.hip g2_pack_kernel's order)
+    const int NT = (int)(J.rows / 32);
+    const long F = p / 64;
+    const int l = (int)(p % 64), m = l & 31, kh = l >> 5;
+    const long k16 = F / NT;
+    const long n = 32 * (F % NT) + sg_out_feat(m);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)src(n, 16 * k16 + 8 * kh + j);
+    *reinterpret_cast<bf16x8*>((bf16*)J.dst + p * 8) = o;
+    return;
+  }
   const long nel = J.rows * J.cols;
   for (int j = 0; j < 8; ++j) {
     const long e = p * 8 + j;

@@ -1151,6 +1151,7 @@ static int launch_proj(const TailArgs& a, hipStream_t s) {
 }
 
 static unsigned long long* g_tail_stamps = nullptr;   // snvrag_tail_stamps (diagnostics)
+unsigned long long* diag_stamps() { return g_tail_stamps; }
 
 static int cu_count() {
   static int n[16] = {0};

@@ -741,14 +741,53 @@ def sgemm_pack(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-DERIVE_F32, DERIVE_BF16, DERIVE_SGPACK = 0, 1, 2
+def gemm256_pack(w: torch.Tensor) -> torch.Tensor:
+    """Fragment stream of W [N, K] for the wide-row GEMM (csrc/gemm256.hip)."""
+    N.require_gpu(w)
+    Nn, Kk = w.shape
+    nbytes = int(N.lib().snvrag_gemm256_pack_bytes(Nn, Kk))
+    if nbytes == 0:
+        raise ValueError(f"wide-row GEMM pack needs N % 128 == 0 and K % 64 == 0, got {tuple(w.shape)}")
+    wb = w.to(torch.bfloat16)
+    if wb.stride(1) != 1:
+        wb = wb.contiguous()
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    check(N.lib().snvrag_gemm256_pack(Nn, Kk, ptr(wb), wb.stride(0), ptr(out), stream_ptr()), "gemm256_pack")
+    return out
+
+
+def gemm256(a: torch.Tensor, wpacked: torch.Tensor, n_out: int, bias: Optional[torch.Tensor] = None,
+            resid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 [M, N] = a [M, K] W^T (+ bias f32 [N]) (+ resid bf16 [M, N]) on the wide-row GEMM
+    (csrc/gemm256.hip; W packed by :func:`gemm256_pack` or derive kind DERIVE_G2PACK).  ``out`` may
+    alias ``resid`` (each element is read before it is written, by the same lane)."""
+    N.require_gpu(a)
+    assert a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(1) == 1
+    M, Kk = a.shape
+    assert wpacked.numel() * wpacked.element_size() == int(N.lib().snvrag_gemm256_pack_bytes(n_out, Kk))
+    if out is None:
+        out = torch.empty(M, n_out, device=a.device, dtype=torch.bfloat16)
+    assert out.dtype == torch.bfloat16 and out.shape == (M, n_out) and out.stride(1) == 1
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == n_out
+    if resid is not None:
+        assert resid.dtype == torch.bfloat16 and resid.shape == (M, n_out) and resid.stride(1) == 1
+    check(N.lib().snvrag_gemm256_forward(M, n_out, Kk, ptr(a), a.stride(0), ptr(wpacked),
+                                         ptr(bias) if bias is not None else None,
+                                         ptr(resid) if resid is not None else None,
+                                         resid.stride(0) if resid is not None else 0, ptr(out), out.stride(0),
+                                         stream_ptr()), "gemm256")
+    return out
+
+
+DERIVE_F32, DERIVE_BF16, DERIVE_SGPACK, DERIVE_G2PACK = 0, 1, 2, 3
 
 
 def derive_job(kind: int, parts, dst: torch.Tensor, dst_ld: int = 0) -> "N.DeriveJob":
     """One snvrag_derive job: ``parts`` = f32 2-D (strided) views stacked along their rows (1-D
     views count as columns [n, 1]); ``dst`` receives kind DERIVE_F32 / DERIVE_BF16 (row-major with
-    row stride ``dst_ld``, default the column count) or DERIVE_SGPACK (the stream-GEMM pack of the
-    [N, D] matrix).  piece0 / pieces are filled by ``derive_table``."""
+    row stride ``dst_ld``, default the column count), DERIVE_SGPACK (the stream-GEMM pack of the
+    [N, D] matrix) or DERIVE_G2PACK (the wide-row GEMM pack of the [N, K] matrix).  piece0 / pieces are filled by ``derive_table``."""
     assert 1 <= len(parts) <= 4
     views = [t.unsqueeze(1) if t.dim() == 1 else t for t in parts]
     cols = views[0].shape[1]
@@ -761,6 +800,9 @@ def derive_job(kind: int, parts, dst: torch.Tensor, dst_ld: int = 0) -> "N.Deriv
         j.part_rows[i], j.rs[i], j.cs[i], j.src[i] = v.shape[0], v.stride(0), v.stride(1), v.data_ptr()
     if kind == DERIVE_SGPACK:
         assert int(N.lib().snvrag_sgemm_pack_bytes(cols, j.rows)) == dst.numel() * dst.element_size()
+        j.pieces = j.rows * cols // 8
+    elif kind == DERIVE_G2PACK:
+        assert int(N.lib().snvrag_gemm256_pack_bytes(j.rows, cols)) == dst.numel() * dst.element_size()
         j.pieces = j.rows * cols // 8
     else:
         assert dst.dtype == (torch.float32 if kind == DERIVE_F32 else torch.bfloat16)

@@ -592,3 +592,61 @@ def test_tail_persistent_equals_tail_kernel(M):
     ulp = yb.float().abs().clamp_min(2 ** -10) * 2 ** -7
     assert bool((d <= ulp * 1.01).all()), float((d / ulp).max())
     assert int((d > 0).sum()) <= max(8, ya.numel() // 1000), int((d > 0).sum())
+
+
+def _bf16_step(x: torch.Tensor) -> torch.Tensor:
+    """One bf16 unit in the last place at |x| (the spacing of bf16 values around x)."""
+    e = torch.floor(torch.log2(x.abs().clamp_min(1e-30)))
+    return torch.exp2(e - 7)
+
+
+@pytest.mark.parametrize("M,Kd,lda_pad,bias,res", [(777, 1536, 0, True, False), (49440, 1536, 0, True, False),
+                                                   (256, 1152, 64, False, True), (1, 64, 0, True, True),
+                                                   (255, 128, 0, False, False), (49440, 1152, 0, False, True),
+                                                   (513, 1536, 8, True, True)])
+def test_gemm256_vs_fp32(M, Kd, lda_pad, bias, res):
+    """snvrag_gemm256_forward (csrc/gemm256.hip: 256-row workgroups, transposed 32x32x16 MFMA over
+    an LDS-DMA ring) vs torch fp32 on the same bf16 operands: ragged M (the last workgroup's rows
+    past M read as zeros and are not stored), strided A, bias and residual epilogues, out aliasing
+    the residual.  The kernel rounds once from its f32 sum, so each output is within one bf16
+    step (+ f32 summation-order noise) of the f32 reference rounded to bf16."""
+    g = torch.Generator(device="cpu").manual_seed(M + Kd)
+    a_full = torch.randn(M, Kd + lda_pad, generator=g).to(DEV, torch.bfloat16)
+    a = a_full[:, :Kd]
+    w = (torch.randn(384, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(384, generator=g).to(DEV) if bias else None
+    r = torch.randn(M, 384, generator=g).to(DEV, torch.bfloat16) if res else None
+    ref = a.float() @ w.float().t()
+    if b is not None:
+        ref = ref + b
+    if r is not None:
+        ref = ref + r.float()
+    wp = K().gemm256_pack(w)
+    out = K().gemm256(a, wp, 384, bias=b, resid=r.clone() if r is not None else None)
+    tol = _bf16_step(ref) + 1e-4 * (1 + ref.abs())
+    bad = (out.float() - ref).abs() > tol
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} of {bad.numel()} outside one bf16 step, first at " \
+                                f"{bad.nonzero()[:4].tolist()}"
+    if r is not None:                                 # in place: out aliases the residual
+        r2 = r.clone()
+        K().gemm256(a, wp, 384, bias=b, resid=r2, out=r2)
+        assert torch.equal(r2, out)
+
+
+def test_gemm256_derive_pack_matches_pack():
+    """snvrag_derive kind 3 from f32 masters (plain, two stacked parts, and the transposed view a
+    dX GEMM packs) == snvrag_gemm256_pack of the bf16-rounded matrix, byte for byte."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    w = torch.randn(384, 1536, generator=g).to(DEV)
+    w1, w2 = torch.randn(192, 1152, generator=g).to(DEV), torch.randn(192, 1152, generator=g).to(DEV)
+    wt = torch.randn(1152, 384, generator=g).to(DEV)               # [K, N]: pack W = wt^T
+    kk = K()
+    outs = [torch.empty_like(kk.gemm256_pack(w.to(torch.bfloat16))),
+            torch.empty_like(kk.gemm256_pack(torch.cat([w1, w2]).to(torch.bfloat16))),
+            torch.empty_like(kk.gemm256_pack(wt.t().to(torch.bfloat16)))]
+    jobs = [kk.derive_job(kk.DERIVE_G2PACK, [w], outs[0]), kk.derive_job(kk.DERIVE_G2PACK, [w1, w2], outs[1]),
+            kk.derive_job(kk.DERIVE_G2PACK, [wt.t()], outs[2])]
+    kk.derive(kk.derive_table(jobs, DEV))
+    assert torch.equal(outs[0], kk.gemm256_pack(w.to(torch.bfloat16)))
+    assert torch.equal(outs[1], kk.gemm256_pack(torch.cat([w1, w2]).to(torch.bfloat16)))
+    assert torch.equal(outs[2], kk.gemm256_pack(wt.t().to(torch.bfloat16)))
