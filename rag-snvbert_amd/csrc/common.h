@@ -71,6 +71,7 @@ struct Options {
   int64_t attn_variant;    // inference attention (dh 32) A/B variant, 0 = default (attention.hip tile)
   int64_t dw_xcd;          // 1: dW workgroups of one M chunk dealt to one XCD (0: plain grid order, A/B)
   int64_t ln_rows1;        // 1: training LayerNorm forward one row per wave also at N <= 512 (A/B)
+  int64_t g2_groups;       // wide-row GEMM token groups per workgroup (4 .. 8; 0: by M)
   int64_t g2_variant;      // wide-row GEMM diagnostics: 1 no LDS-DMA, 2 no MFMA (wrong results; timing only),
                            // 3 stamps into the snvrag_tail_stamps buffer
   int64_t tail_persist;    // 1: the persistent block tail (tailp_kernel, A/B); 0 (default): tail_kernel

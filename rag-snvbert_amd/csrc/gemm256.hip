@@ -44,7 +44,8 @@ __device__ __forceinline__ void g2_unroll(Body&& body, std::integer_sequence<int
 // 384 accumulator registers per lane: the first G2_NACC tiles live in AGPRs, the rest in VGPRs.
 // The MFMA is inline asm so that the register class of every accumulator is fixed (the builtin's
 // single AGPR-or-VGPR form for the whole kernel spills half of them); the compiler then does not
-// know these are MFMAs — the epilogue waits out the last results itself (g2_drain).
+// know these are MFMAs, so nothing may read an accumulator within 18 wait states of its last MFMA
+// unless g2_drain runs in between — including the compiler's own register moves (see g3_kernel).
 template <bool AGPR>
 __device__ __forceinline__ void g2_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
   if constexpr (AGPR)
@@ -247,9 +248,9 @@ void g2_kernel(G2Args p) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }, std::make_integer_sequence<int, FPK>{});
     adv(WS);
+    if (k == nk - 1) g2_drain();                      // (inside the loop: see g3_kernel)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the ring overrun has landed
-  g2_drain();
   stamp(3, __builtin_amdgcn_s_memtime());
   stamp(6, st_wait);
   stamp(7, st_b);
@@ -303,6 +304,222 @@ void g2_kernel(G2Args p) {
   }
   stamp(4, __builtin_amdgcn_s_memtime());
   stamp(5, __builtin_amdgcn_s_memrealtime());
+}
+
+// ---- v2 (default): the W fragments in registers, A alone through LDS
+//
+// Wave w owns output features 96 w .. 96 w + 95 (feature tiles 3 w .. 3 w + 2) for all 256 rows of
+// the workgroup (8 token groups): 24 accumulator tiles (16 in AGPRs, 8 in VGPRs).  Per K-step of 64
+// a wave needs 12 W fragments (k16 step s, its 3 tiles): loaded straight into registers by
+// buffer_load_dwordx4 one K-step ahead (the register of fragment (s, t) is reloaded for the next
+// K-step right after its last MFMA), so W never passes through LDS; only the 256 x 128 B image of
+// A is staged (LDS-DMA, 8 whole-line pieces per wave per K-step, G3_AH images ahead, one barrier per
+// K-step), and each B-fragment read from it feeds 3 MFMAs.  Per wave and K-step: 96 MFMA, 32
+// ds_read_b128, 12 register loads, 8 DMA pieces.
+//
+// Memory-op order per K-step phase s (8 token groups): DMA piece at groups 1 and 5, the three W
+// loads after group 7 — 5 vector-memory ops per phase, so the W fragments of phase s issued one
+// K-step earlier have exactly 15 younger ops at the next phase s: s_waitcnt vmcnt(15).
+//
+// G token groups per workgroup (32 G rows, G = 4 .. 8): chosen per launch so that the workgroups
+// fit one round of the CUs (M = 49 440: G = 7, 221 workgroups) — a wave's G DMA pieces per K-step
+// go to phases j % 4 (d_s of them in phase s), so phase s waits with vmcnt(G + 9 - d_s).
+constexpr int G3_AH = 3;                              // A images in flight ahead of the one read
+constexpr int G3_NS = G3_AH + 1;                      // A image slots
+constexpr int G3_PF = 3;                              // B-fragment reads ahead
+__host__ __device__ constexpr int g3_img(int G) { return 32 * G * 128; }   // one A image: 32 G rows x 128 B
+__host__ __device__ constexpr int g3_pieces_in_phase(int G, int s) { return G / 4 + (s < G % 4 ? 1 : 0); }
+
+template <int G, int VAR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void g3_kernel(G2Args p) {
+  constexpr int N = 384, TW = 3, G3_IMG = g3_img(G);
+  static_assert(G >= 4 && G <= 8, "4 .. 8 token groups");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sb = reinterpret_cast<float*>(smem + G3_NS * G3_IMG);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int M = p.M, nk = p.K / 64;
+  unsigned long long st_wait = 0, st_t = 0;
+  auto stamp = [&](int i, unsigned long long v) {
+    if constexpr (VAR == 3)
+      if ((threadIdx.x & 63) == 0) p.stamps[((long)blockIdx.x * 4 + wave) * 8 + i] = v;
+  };
+  stamp(0, __builtin_amdgcn_s_memtime());
+  stamp(1, __builtin_amdgcn_s_memrealtime());
+  const long row0 = (long)blockIdx.x * (32 * G);
+  for (int i = threadIdx.x; i < N; i += 256) sb[i] = p.bias ? p.bias[i] : 0.f;
+
+  const i32x4 ars = dma_rsrc(p.A + row0 * p.lda, ((long)M - row0) * p.lda * 2);   // rows >= M read as 0
+  const i32x4 wrs = dma_rsrc(p.ws, (long)nk * 4 * 12 * G2_FRAG);
+  const uint32_t img_lds = lds_addr(smem);
+  // per-lane offsets (VGPRs for the whole kernel): the lane's 16 B of a fragment; its piece of an A
+  // image (row l / 8 of the piece, swizzled chunk); its B-fragment bytes per k16 step s (row n,
+  // chunk 2 s + kh stored at (2 s + kh) ^ (n % 8))
+  int lane16, voffA, boff[4];
+  {
+    const int l = g2_lane(), n = l & 31, kh = l >> 5;
+    lane16 = l * 16;
+    voffA = (int)((l >> 3) * p.lda * 2) + 16 * ((l & 7) ^ ((l >> 3) & 7));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) boff[s] = n * 128 + 16 * ((2 * s + kh) ^ (n & 7));
+  }
+  asm volatile("" : "+v"(lane16), "+v"(voffA), "+v"(boff[0]), "+v"(boff[1]), "+v"(boff[2]), "+v"(boff[3]));
+
+  // piece j (0 .. G - 1) of A image kt into the slot at byte offset slot: rows 8 (G w + j) .. + 7
+  auto putA = [&](int slot, int j, int kt) {
+    if constexpr (VAR == 1) return;                   // diagnostic: no A loads
+    const int pc = G * g2_opq(wave) + j;
+    dma_x4(ars, img_lds + slot + pc * G2_FRAG, voffA + (int)(8 * pc * p.lda * 2), 128 * kt);
+  };
+  auto loadW = [&](u32x4& w, int kt, int s, int t) {
+    const int so = ((4 * kt + s) * 12 + 3 * g2_opq(wave) + t) * G2_FRAG;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(w) : "v"(lane16), "s"(wrs), "s"(so) : "memory");
+  };
+
+  f32x16 acc[G][TW];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) acc[g][t] = f32x16{};
+  u32x4 w[4][TW];
+  // prologue: the first K-step's W fragments, A images 0 .. AH - 1; wait for the W fragments and
+  // image 0 only
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) loadW(w[s][t], 0, s, t);
+#pragma unroll
+  for (int q = 0; q < G3_AH; ++q)
+#pragma unroll
+    for (int j = 0; j < G; ++j) putA(q * G3_IMG, j, q < nk ? q : nk - 1);
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((G3_AH - 1) * G) : "memory");
+  __builtin_amdgcn_s_barrier();
+  stamp(2, __builtin_amdgcn_s_memtime());
+
+  int slot_rd = 0, slot_wr = G3_AH * G3_IMG;
+#pragma unroll 1
+  for (int k = 0; k < nk; ++k) {
+    int ka = k + G3_AH, kw = k + 1;
+    ka = ka < nk ? ka : nk - 1;                       // past the end: re-read the last K-step
+    kw = kw < nk ? kw : nk - 1;
+    u32x4 bq[G3_PF];
+    auto rdB = [&](int i) -> u32x4 {                  // B fragment i = G s + g of this K-step
+      return *reinterpret_cast<const u32x4*>(smem + slot_rd + boff[i / G] + (i % G) * 4096);
+    };
+    g2_unroll([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (VAR == 3) st_t = __builtin_amdgcn_s_memtime();
+      asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(w[s][2])
+                   : "n"(G + 9 - g3_pieces_in_phase(G, s)) : "memory");
+      if constexpr (s == 0) {
+        __builtin_amdgcn_s_barrier();                 // A(k) landed for every wave; A(k - 1)'s slot free
+#pragma unroll
+        for (int i = 0; i < G3_PF; ++i) bq[i] = rdB(i);
+      }
+      if constexpr (VAR == 3) st_wait += __builtin_amdgcn_s_memtime() - st_t;
+      g2_unroll([&](auto gc) {
+        constexpr int g = decltype(gc)::value, i = G * s + g;
+        const u32x4 b = bq[i % G3_PF];
+        if constexpr (i + G3_PF < 4 * G) bq[i % G3_PF] = rdB(i + G3_PF);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          if constexpr (VAR != 2) {
+            if (g * TW + t < G2_NACC) g2_mfma<true>(acc[g][t], w[s][t], b);
+            else g2_mfma<false>(acc[g][t], w[s][t], b);
+          } else {
+            asm volatile("" ::"v"(w[s][t]), "v"(b));
+          }
+        }
+        // pieces s and s + 4 of the phase at groups 1 and min(5, G - 1)
+        if constexpr (g == 1) putA(slot_wr, s, ka);
+        if constexpr (g == (G - 1 < 5 ? G - 1 : 5) && s + 4 < G) putA(slot_wr, s + 4, ka);
+        if constexpr (g == G - 1) {
+#pragma unroll
+          for (int t = 0; t < TW; ++t) loadW(w[s][t], kw, s, t);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }, std::make_integer_sequence<int, G>{});
+    }, std::make_integer_sequence<int, 4>{});
+    slot_rd = slot_rd + G3_IMG == G3_NS * G3_IMG ? 0 : slot_rd + G3_IMG;
+    slot_wr = slot_wr + G3_IMG == G3_NS * G3_IMG ? 0 : slot_wr + G3_IMG;
+    // the last K-step's MFMA results: the drain sits INSIDE the loop body, so that the register
+    // moves the compiler places on the loop exit (re-homing accumulators for the epilogue) come
+    // after it — after the loop they were seen reading an AGPR before its last MFMA had written it
+    if (k == nk - 1) g2_drain();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the overrun loads have landed
+  stamp(3, __builtin_amdgcn_s_memtime());
+  stamp(6, st_wait);
+
+  // ---- epilogue: + bias (+ resid) -> bf16, two 16-B stores per (token group, feature tile)
+  const long rows_left = (long)M - row0;
+  const long o_bytes = rows_left * p.ldo * 2;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.out + row0 * p.ldo), (short)0, (int)(o_bytes < 0x7fffffffL ? o_bytes : 0x7fffffffL), 0x00020000);
+  const long r_bytes = p.resid ? rows_left * p.ld_resid * 2 : 0;
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.resid ? p.resid + row0 * p.ld_resid : p.out), (short)0,
+      (int)(r_bytes < 0x7fffffffL ? r_bytes : 0x7fffffffL), 0x00020000);
+  const bool has_res = p.resid != nullptr;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int l = g2_lane();
+    const int f0 = 96 * wave + 32 * t + 16 * (l >> 5);
+    u32x4 bv[4];
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:0\n ds_read_b128 %1, %4 offset:16\n ds_read_b128 %2, %4 offset:32\n"
+        " ds_read_b128 %3, %4 offset:48\n s_waitcnt lgkmcnt(0)"
+        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+        : "v"(lds_addr(sb) + 4 * f0));
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int rl = 32 * g + (g2_lane() & 31);
+      float y[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) y[i] = acc[g][t][i] + __uint_as_float(bv[i >> 2][i & 3]);
+      if (has_res) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rrs, (int)(rl * p.ld_resid + f0 + 8 * h2) * 2, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            y[8 * h2 + 2 * e] += __uint_as_float(r[e] << 16);
+            y[8 * h2 + 2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+          }
+        }
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{g2_pack2(y[8 * h2], y[8 * h2 + 1]), g2_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                  g2_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), g2_pack2(y[8 * h2 + 6], y[8 * h2 + 7])},
+            ors, (int)(rl * p.ldo + f0 + 8 * h2) * 2, 0, 0);
+    }
+  }
+  stamp(4, __builtin_amdgcn_s_memtime());
+  stamp(5, __builtin_amdgcn_s_memrealtime());
+}
+
+template <int G, int VAR>
+static int g3_launch(const G2Args& a, hipStream_t s) {
+  auto kern = g3_kernel<G, VAR>;
+  constexpr size_t lds = (size_t)G3_NS * g3_img(G) + 384 * 4;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 32 * G)), dim3(256), lds, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int VAR>
+static int g3_dispatch(int G, const G2Args& a, hipStream_t s) {
+  switch (G) {
+    case 4: return g3_launch<4, VAR>(a, s);
+    case 5: return g3_launch<5, VAR>(a, s);
+    case 6: return g3_launch<6, VAR>(a, s);
+    case 7: return g3_launch<7, VAR>(a, s);
+    default: return g3_launch<8, VAR>(a, s);
+  }
 }
 
 // One thread per 16-byte piece: fragment F = k16 NT + T, lane l = (m = l % 32, kh = l / 32) holds
@@ -368,8 +585,30 @@ extern "C" int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, in
   const int64_t var = options().g2_variant;
   G2Args b = a;
   b.stamps = diag_stamps();
-  const int rc = var == 1 ? g2_launch<12, 1>(a, s) : var == 2 ? g2_launch<12, 2>(a, s)
-               : var == 3 && b.stamps ? g2_launch<12, 3>(b, s) : g2_launch<12, 0>(a, s);
+  // token groups per workgroup: the fewest rows that still fit one round of the CUs (4 .. 8
+  // groups of 32; option g2_groups overrides)
+  static int n_cu = 0;
+  if (n_cu <= 0) {
+    int dev = 0, v = 0;
+    n_cu = hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0
+               ? v : 256;
+  }
+  int G = (int)std::min<long>(8, std::max<long>(4, (M + 32L * n_cu - 1) / (32L * n_cu)));
+  if (options().g2_groups >= 4 && options().g2_groups <= 8) G = (int)options().g2_groups;
+  // g2_variant: 0 v2 (default); 1 / 2 / 3: v2 without A loads / without MFMA / with stamps;
+  // 4: v1 (W through LDS); 5 / 6 / 7: v1 without loads / without MFMA / with stamps
+  int rc;
+  switch (var) {
+    case 1: rc = g3_dispatch<1>(G, a, s); break;
+    case 2: rc = g3_dispatch<2>(G, a, s); break;
+    case 3: rc = b.stamps ? g3_dispatch<3>(G, b, s) : g3_dispatch<0>(G, a, s); break;
+    case 4: rc = g2_launch<12, 0>(a, s); break;
+    case 5: rc = g2_launch<12, 1>(a, s); break;
+    case 6: rc = g2_launch<12, 2>(a, s); break;
+    case 7: rc = b.stamps ? g2_launch<12, 3>(b, s) : g2_launch<12, 0>(a, s); break;
+    default: rc = g3_dispatch<0>(G, a, s);
+  }
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)N * K);
   return 0;

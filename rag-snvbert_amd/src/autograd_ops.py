@@ -4,7 +4,8 @@ The training graph (``src/train_forward.py``) is ordinary autograd; its heavy no
 are these Functions, whose forward and backward run the HIP kernels:
 
   hip_linear      Linear layers on the MFMA GEMMs (bf16 in, f32 accumulate):
-                  forward  y = x W^T + b             (stream GEMM at K = 384, else snvrag_linear)
+                  forward  y = x W^T + b             (stream GEMM at K = 384, wide-row GEMM for
+                                                      the large-K -> 384 ones, else snvrag_linear)
                   backward dx = dy W                 (the same GEMMs on W^T)
                            dW = dy^T x, db = sum dy  (snvrag_linear_dw: split-M MFMA kernel on
                                                       LDS-transposed tiles, f32 result; shapes
@@ -259,6 +260,49 @@ def _sg_stream_t(w: torch.Tensor, n_out: int):
     return _derived(("sgT",), [w], make)
 
 
+def _g2_stream(ws, bs):
+    """(packed stream, f32 bias or None) of the wide-row GEMM (csrc/gemm256.hip) for the weights
+    ``ws`` concatenated along the outputs (FeedForward's w_2: one [384, 1536] weight)."""
+    parts = list(ws) + [b for b in bs if b is not None]
+
+    def make():
+        n_out, Kd = sum(w.shape[0] for w in ws), ws[0].shape[1]
+        packed = torch.empty(int(K.N.lib().snvrag_gemm256_pack_bytes(n_out, Kd)), device=ws[0].device,
+                             dtype=torch.uint8)
+        jobs = [K.derive_job(K.DERIVE_G2PACK, [w.detach() for w in ws], packed)]
+        if bs[0] is None:
+            return (packed, None), jobs
+        vec, vj = _plain_job(K.DERIVE_F32, [t.detach().reshape(-1) for t in bs])
+        return (packed, vec), jobs + vj
+    return _derived(("g2",), parts, make)
+
+
+def _g2_stream_t(ws):
+    """Packed stream of [W_1; ..; W_n]^T for the wide-row GEMM (the dX = dY [W_1; ..; W_n] GEMM
+    onto 384 inputs): the pack is K-major, so the pack of the column blocks W_i^T is the
+    concatenation of their packs — one derive job per weight."""
+    def make():
+        n_in = ws[0].shape[1]
+        total = int(K.N.lib().snvrag_gemm256_pack_bytes(n_in, sum(w.shape[0] for w in ws)))
+        packed = torch.empty(total, device=ws[0].device, dtype=torch.uint8)
+        jobs, off = [], 0
+        for w in ws:
+            nb = int(K.N.lib().snvrag_gemm256_pack_bytes(n_in, w.shape[0]))
+            jobs.append(K.derive_job(K.DERIVE_G2PACK, [w.detach().t()], packed[off:off + nb]))
+            off += nb
+        return packed, jobs
+    return _derived(("g2T",), list(ws), make)
+
+
+def _g2_ok(k_in: int, n_out: int, parts=()) -> bool:
+    """The wide-row GEMM takes the large-K projections onto 384 features: FeedForward's w_2
+    forward (K = 4D) and the dX GEMMs of q/k/v (K = 3D) and w_1 (K = 4D).  62 / 49 us at
+    M = 49 440, K = 1536 / 1152, vs hipBLASLt's 68-78 / 54-58 and the row panel's 78 / 60
+    (tools/gemm256_micro.py)."""
+    return (n_out == 384 and k_in >= 1024 and k_in % 64 == 0 and all(t % 64 == 0 for t in parts)
+            and not _BLAS_LARGE_K[0])
+
+
 def _sg_ok(x2: torch.Tensor, n_out: int) -> bool:
     """The stream GEMM takes the K = 384, no-activation projections (QKV, FFN w_1, fusion /
     head Linear layers): 850-900 TFLOP/s vs the row panel's ~550 at the training shapes."""
@@ -340,14 +384,15 @@ def small_linear(x: torch.Tensor, lin) -> torch.Tensor:
 
 
 _DIRECT_GRADS = False
-_BLAS_DX = [True]                           # large-K dX GEMMs on hipBLASLt (set_blas_dx)
+_BLAS_LARGE_K = [False]                     # A/B only: the large-K -> 384 GEMMs on hipBLASLt
 
 
 def set_blas_dx(enabled: bool) -> bool:
-    """The K >= 1024 -> 384 dX GEMMs of the training backward on hipBLASLt (default) or on the
-    row-panel kernel (A/B: tools/train_only.py BLAS_DX=0).  Returns the previous setting."""
-    prev = _BLAS_DX[0]
-    _BLAS_DX[0] = bool(enabled)
+    """A/B switch (tools/train_only.py BLAS_DX=1): the large-K -> 384 GEMMs of training (w_2
+    forward, the q/k/v and w_1 dX) on hipBLASLt instead of the wide-row kernel (the default).
+    Returns the previous setting."""
+    prev = _BLAS_LARGE_K[0]
+    _BLAS_LARGE_K[0] = bool(enabled)
     return prev
 
 
@@ -416,10 +461,12 @@ class _HipLinear(torch.autograd.Function):
         if _sg_ok(x2, n_out):
             wsp, vec = _sg_stream(ws, bs, n_out)
             y = K.sgemm(x2, wsp, n_out, vec)
-        elif _BLAS_DX[0] and n == 1 and Kd >= 1024 and n_out == 384 and x2.shape[0] >= 8192:
-            # FeedForward's w_2 (K = 4D -> D) on hipBLASLt, the shape of the large-K dX GEMMs below
-            # (80 vs 102 us at M = 49 440); its bias epilogue takes the bias in bf16
-            w = bf16_of(ws[0])
+        elif _g2_ok(Kd, n_out, [t.shape[0] for t in ws]):
+            # FeedForward's w_2 (K = 4D -> D) on the wide-row GEMM, f32 bias in its epilogue
+            wsp, vec = _g2_stream(ws, bs)
+            y = K.gemm256(x2, wsp, n_out, bias=vec)
+        elif _BLAS_LARGE_K[0] and n == 1 and Kd >= 1024 and n_out == 384:
+            w = bf16_of(ws[0])                      # A/B: hipBLASLt (bias taken in bf16)
             y = torch.addmm(bf16_of(bs[0]), x2, w.t()) if has_b else torch.mm(x2, w.t())
         else:
             w = bf16_of(ws[0]) if n == 1 else _cat_bf16(ws)
@@ -465,11 +512,20 @@ class _HipLinear(torch.autograd.Function):
                 gx = K.sgemm(g2, wsp, n_in, vec)
                 if res is not None:
                     gx += res.reshape(gx.shape).to(gx.dtype)
-            elif _BLAS_DX[0] and g2.shape[1] >= 1024 and n_in == 384:
-                # the K >= 1024 -> 384 dX GEMMs (q/k/v, FeedForward w_1) on hipBLASLt: 80 vs 102 us
-                # (K = 1536) and 59 vs 79 us (K = 1152) at M = 49 440 (tools/dx_micro.py) — the
-                # row-panel kernel's 387 workgroups of 128 rows fill 1.5 rounds of the chip; the
-                # handed-off gradient enters as addmm's C operand (one f32 add, one rounding)
+            elif _g2_ok(g2.shape[1], n_in, sizes):
+                # the K >= 1024 -> 384 dX GEMMs (q/k/v, FeedForward w_1) on the wide-row GEMM; the
+                # handed-off gradient enters its epilogue (one f32 add, one rounding), in place (the
+                # handed-off tensor is held by nothing else)
+                wsp = _g2_stream_t(ws)
+                if res is None:
+                    gx = K.gemm256(g2, wsp, n_in)
+                else:
+                    r2 = res.reshape(-1, n_in).to(torch.bfloat16)
+                    if r2.stride(1) != 1 or r2.stride(0) % 8 or r2.data_ptr() % 16:
+                        r2 = r2.contiguous()
+                    gx = K.gemm256(g2, wsp, n_in, resid=r2, out=r2)
+            elif _BLAS_LARGE_K[0] and g2.shape[1] >= 1024 and n_in == 384:
+                # A/B: hipBLASLt, the handed-off gradient as addmm's C operand
                 wc = bf16_of(ws[0]) if ctx.n == 1 else _cat_bf16(ws)
                 # (in place on the handed-off gradient, which nothing else holds: out-of-place
                 # addmm first copies its C operand into a fresh output, 15 us at M = 49 440)

@@ -1,0 +1,64 @@
+"""The wide-row GEMM (csrc/gemm256.hip) issues its MFMAs as inline asm (to pin each accumulator's
+register class), so the compiler's hazard recognizer does not know they are MFMAs: an instruction
+it places right after one — e.g. a register move re-homing an accumulator on the loop exit —
+could read the accumulator before the MFMA has written it (seen once: 4 of 384 outputs of one
+tile off by their last k16 step, only at 7 token groups).  This compiles the kernel to assembly
+for gfx950 and checks that no instruction reads an MFMA's destination registers before the
+drain (s_nop 7) or three further MFMAs."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "..", "rag-snvbert_amd", "csrc", "gemm256.hip")
+
+
+def _regs(tok):
+    m = re.fullmatch(r"([av])\[(\d+):(\d+)\]", tok)
+    if m:
+        return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.fullmatch(r"([av])(\d+)", tok)
+    return {(m.group(1), int(m.group(2)))} if m else set()
+
+
+def _reads(ins):
+    ops = [o.strip() for o in ins.split(None, 1)[1].split(",")] if " " in ins else []
+    src = ops[1:] if ops else []
+    out = set()
+    for o in src:
+        out |= _regs(o.split()[0]) if o else set()
+    return out
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_no_accumulator_read_inside_mfma_latency(tmp_path):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    out = tmp_path / "g.s"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only", SRC, "-o",
+                    str(out)], check=True, capture_output=True)
+    lines = [ln.strip() for ln in out.read_text().split("\n")]
+    ins = [ln for ln in lines if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
+    n_mfma = 0
+    bad = []
+    for i, t in enumerate(ins):
+        if not t.startswith("v_mfma"):
+            continue
+        n_mfma += 1
+        dst = _regs(t.split()[1].rstrip(","))
+        later = 0
+        for u in ins[i + 1:i + 80]:
+            if u.startswith("s_nop 7") or u.startswith("s_endpgm"):
+                break
+            if u.startswith("v_mfma"):
+                later += 1
+                if later >= 3:
+                    break
+                continue
+            if _reads(u) & dst:
+                bad.append((t, u))
+                break
+    assert n_mfma > 1000
+    assert not bad, bad[:5]

@@ -650,3 +650,31 @@ def test_gemm256_derive_pack_matches_pack():
     assert torch.equal(outs[0], kk.gemm256_pack(w.to(torch.bfloat16)))
     assert torch.equal(outs[1], kk.gemm256_pack(torch.cat([w1, w2]).to(torch.bfloat16)))
     assert torch.equal(outs[2], kk.gemm256_pack(wt.t().to(torch.bfloat16)))
+
+
+@pytest.mark.parametrize("groups", [4, 5, 6, 7, 8])
+def test_gemm256_row_groups_bit_identical(groups):
+    """Every workgroup height (option g2_groups: 32 x 4 .. 8 rows; the default picks it by M) and
+    the v1 kernel (g2_variant 4: W through LDS) give the same bits: the K order of each output's sum
+    does not depend on the tiling."""
+    kk = K()
+    g = torch.Generator(device="cpu").manual_seed(groups)
+    M, Kd = 2 * 32 * groups * 3 + 77, 1152
+    a = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(384, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(384, generator=g).to(DEV)
+    r = torch.randn(M, 384, generator=g).to(DEV, torch.bfloat16)
+    wp = kk.gemm256_pack(w)
+    ref = kk.gemm256(a, wp, 384, bias=b, resid=r)
+    try:
+        kk.set_option("g2_groups", groups)
+        y = kk.gemm256(a, wp, 384, bias=b, resid=r)
+        kk.set_option("g2_groups", 0)
+        kk.set_option("g2_variant", 4)
+        y1 = kk.gemm256(a, wp, 384, bias=b, resid=r)
+    finally:
+        kk.set_option("g2_groups", 0)
+        kk.set_option("g2_variant", 0)
+    assert torch.equal(y, ref) and torch.equal(y1, ref)
+    e = (ref.float() - (a.float() @ w.float().t() + b + r.float())).abs()
+    assert e.max().item() < 0.1

@@ -18,7 +18,7 @@ from src.model import build_model  # noqa: E402
 
 from src import autograd_ops  # noqa: E402
 
-autograd_ops.set_blas_dx(os.environ.get("BLAS_DX", "1") != "0")
+autograd_ops.set_blas_dx(os.environ.get("BLAS_DX", "0") == "1")    # A/B: hipBLASLt large-K GEMMs
 dev = torch.device("cuda")
 Bt, S = int(os.environ.get("TR_B", 24)), int(os.environ.get("TR_WINDOW", 512))
 ds, vocab = make_rag_dataset(n_samples=Bt, n_sites=S, n_windows=1, n_ref_samples=5000, seed=7, name="train")
