@@ -514,8 +514,8 @@ class _HipLinear(torch.autograd.Function):
                     gx += res.reshape(gx.shape).to(gx.dtype)
             elif _g2_ok(g2.shape[1], n_in, sizes):
                 # the K >= 1024 -> 384 dX GEMMs (q/k/v, FeedForward w_1) on the wide-row GEMM; the
-                # handed-off gradient enters its epilogue (one f32 add, one rounding), in place (the
-                # handed-off tensor is held by nothing else)
+                # handed-off gradient enters its epilogue (one f32 add, one rounding) into a fresh
+                # output (the handed-off tensor may also be another node's returned gradient)
                 wsp = _g2_stream_t(ws)
                 if res is None:
                     gx = K.gemm256(g2, wsp, n_in)
@@ -523,14 +523,12 @@ class _HipLinear(torch.autograd.Function):
                     r2 = res.reshape(-1, n_in).to(torch.bfloat16)
                     if r2.stride(1) != 1 or r2.stride(0) % 8 or r2.data_ptr() % 16:
                         r2 = r2.contiguous()
-                    gx = K.gemm256(g2, wsp, n_in, resid=r2, out=r2)
+                    gx = K.gemm256(g2, wsp, n_in, resid=r2)
             elif _BLAS_LARGE_K[0] and g2.shape[1] >= 1024 and n_in == 384:
                 # A/B: hipBLASLt, the handed-off gradient as addmm's C operand
                 wc = bf16_of(ws[0]) if ctx.n == 1 else _cat_bf16(ws)
-                # (in place on the handed-off gradient, which nothing else holds: out-of-place
-                # addmm first copies its C operand into a fresh output, 15 us at M = 49 440)
                 gx = torch.mm(g2, wc) if res is None else \
-                    res.reshape(-1, n_in).to(torch.bfloat16).addmm_(g2, wc)
+                    torch.addmm(res.reshape(-1, n_in).to(torch.bfloat16), g2, wc)
             else:
                 wt = bf16_of(ws[0], transposed=True) if ctx.n == 1 else _cat_bf16(ws, transposed=True)
                 gx = K.linear(g2, wt, resid=None if res is None else res.reshape(-1, n_in).to(torch.bfloat16))

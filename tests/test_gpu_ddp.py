@@ -120,12 +120,16 @@ def _ddp_worker(rank, world, port, panel, q):
             early = [(b, i) for t, (b, _) in enumerate(trace) for i in bk.buckets[b]
                      if fin(i) is not None and fin(i) > t]
             unused = sorted(i for b, _ in trace for i in bk.buckets[b] if fin(i) is None)
+            # buckets launched from the post-accumulate hooks during backward (every member final),
+            # as opposed to by finish() after it
+            hooked = sum(1 for b, ready in trace if len(ready) == len(bk.buckets[b]))
             checks.append(dict(order=order, complete=complete, early=early, n_final=len(final_at),
-                               unused=unused))
+                               unused=unused, hooked=hooked))
         names = {id(p): n for n, p in m.named_parameters()}
         q.put((rank, dict(checks=checks, steps=[(g.numpy(), f.numpy(), s) for g, f, s in captured],
                           post=[dict(d, flat=d["flat"].numpy()) for d in tr._post],
                           final=tr.flat.flat.detach().cpu().numpy(), n_buckets=len(bk.buckets),
+                          buckets=[list(b) for b in bk.buckets],
                           names=[names[id(p)] for p in tr.flat.params], offsets=list(tr.flat.offsets))))
     except Exception:
         q.put((rank, traceback.format_exc()))
@@ -189,6 +193,16 @@ def test_ddp_train_step_buckets_final_and_ranks_equal(panel):
             assert c["order"] == list(range(got[r]["n_buckets"])), (r, s, c["order"])
             assert c["complete"] and not c["early"], (r, s, c)
             assert c["unused"] == got[0]["checks"][0]["unused"] and c["n_final"] > 50, (r, s, c)
+            # every parameter in the graph reports through its hook — Linear / LayerNorm weights
+            # under direct_weight_grads included — so all buckets but those holding a parameter
+            # with no gradient this step (and the ones after it) launch during backward
+            # (rag_fusion.pooling: its softmax runs over ONE neighbour mean, train_forward.py:137,
+            # so its weight is exactly 1 and its Linear gets no gradient — zero in the reference)
+            unused_names = [got[r]["names"][i] for i in c["unused"]]
+            assert all(".pooling." in n for n in unused_names), (r, s, unused_names)
+            first_unused = min((b for b, members in enumerate(got[r]["buckets"]) if set(members) & set(c["unused"])),
+                               default=got[r]["n_buckets"])
+            assert c["hooked"] >= first_unused, (r, s, c["hooked"], first_unused, unused_names)
         g0, f0, sc0 = r0["steps"][s]
         g1, f1, sc1 = r1["steps"][s]
         assert sc0 == sc1 == 1.0
