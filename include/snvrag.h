@@ -465,8 +465,13 @@ int snvrag_attention_bwd(int64_t nseq, int64_t L, int heads, int dh, const void*
  * weight * dFL/dprobs (0 on unmasked rows). */
 int snvrag_focal_loss(int64_t M, int C, const float* probs, const int64_t* labels, const uint8_t* mask,
                       float gamma, float weight, float* loss_sum, float* grad, void* stream);
-/* acc = sum x^2 (acc is zeroed on the stream first). x 16-byte aligned. */
+/* acc = sum x^2 in a fixed reduction order (bit-identical for identical x). x 16-byte aligned.
+ * snvrag_sqnorm keeps its per-block partials in one process-wide device buffer: one call in flight
+ * per device (stream-ordered); snvrag_sqnorm_ws takes a caller-owned workspace of
+ * snvrag_sqnorm_ws_bytes() bytes instead, so calls on different streams may overlap. */
 int snvrag_sqnorm(int64_t n, const float* x, float* acc, void* stream);
+size_t snvrag_sqnorm_ws_bytes(void);
+int snvrag_sqnorm_ws(int64_t n, const float* x, float* acc, float* ws, size_t ws_bytes, void* stream);
 typedef struct {
   float lr, beta1, beta2, eps, weight_decay;
   float grad_scale;     /* g <- g * grad_scale (1/world for summed DDP gradients) */

@@ -893,14 +893,20 @@ static void launch_scan2(int n_parts, int nq, hipStream_t s, const uint8_t* code
                      wide, n_parts, G, nt);
 }
 
-static int scan_parts(long n_ref) {
+static int scan_parts(long n_ref, int nq) {
   // ~2048 refs per range at least; large panels get a multiple of 256 ranges (one
   // workgroup per CU per round, no tail round)
   long p = (n_ref + 2047) / 2048;
   if (p >= 256) p = 256 * ((n_ref + 256L * 8192 - 1) / (256L * 8192));
   // small panels (training: 10 000 haplotypes were 5 ranges = 5 workgroups, 190 us): ranges down
-  // to 64 refs, up to 256 of them, so the scan still spreads over the chip
-  else p = std::min<long>(256, std::max<long>(p, (n_ref + 63) / 64));
+  // to 64 refs, so the scan still spreads over the chip — up to 256 workgroups counting the query
+  // groups (G of them run per range): many queries fill the chip by themselves, and each range
+  // adds nq x k partial entries to the merge
+  else {
+    const long G = std::max<long>(1, ((long)(nq > 0 ? nq : 1) + 127) / 128);
+    const long spread = std::max<long>(1, 256 / G);
+    p = std::min<long>(256, std::max<long>(p, std::min<long>(spread, (n_ref + 63) / 64)));
+  }
   if (p < 1) p = 1;
   if (p > 4096) p = 4096;
   return (int)p;
@@ -997,7 +1003,7 @@ extern "C" int snvrag_knn_threshold(const uint64_t* keys, int32_t nq, int k, int
   return 0;
 }
 
-extern "C" int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq) { (void)nq; return scan_parts(n_ref); }
+extern "C" int snvrag_knn_scan_parts(int64_t n_ref, int32_t nq) { return scan_parts(n_ref, nq); }
 
 extern "C" int snvrag_knn_scan(const uint8_t* codes, int64_t n_ref, int64_t ld_codes, int32_t n_sites_pad,
                                const void* lut, int32_t nq, int limbs, int k, int64_t ref_offset,

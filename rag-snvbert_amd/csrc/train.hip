@@ -59,9 +59,11 @@ __global__ __launch_bounds__(256) void focal_kernel(long M, int C, const float* 
 // job holds the same reduced gradient and must derive the same clip coefficient bit for bit,
 // or the replicas drift apart after the first optimizer step.
 constexpr int kSqBlocks = 2048;
-__device__ float g_sq_partials[kSqBlocks];   // one launch pair in flight per process (stream-ordered)
+// the partials of snvrag_sqnorm (no workspace: one call in flight per device, stream-ordered);
+// snvrag_sqnorm_ws takes the caller's buffer, so calls on different streams do not share it
+__device__ float g_sq_partials[kSqBlocks];
 
-__global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __restrict__ x) {
+__global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __restrict__ x, float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
   const long n4 = n / 4;
@@ -74,13 +76,15 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(long n, const float* __rest
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) g_sq_partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) (part ? part : g_sq_partials)[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void sqnorm_final_kernel(int nblocks, float* __restrict__ acc) {
+__global__ __launch_bounds__(256) void sqnorm_final_kernel(int nblocks, const float* __restrict__ part,
+                                                           float* __restrict__ acc) {
   __shared__ float red[4];
   float s = 0.f;
-  for (int i = threadIdx.x; i < nblocks; i += 256) s += g_sq_partials[i];
+  const float* pp = part ? part : g_sq_partials;
+  for (int i = threadIdx.x; i < nblocks; i += 256) s += pp[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -158,19 +162,29 @@ extern "C" int snvrag_focal_loss(int64_t M, int C, const float* probs, const int
   return 0;
 }
 
-extern "C" int snvrag_sqnorm(int64_t n, const float* x, float* acc, void* stream) {
+static int sqnorm_impl(int64_t n, const float* x, float* acc, float* part, hipStream_t s) {
   SNV_CHECK_ARG(x && acc && ((uintptr_t)x % 16) == 0, "null or misaligned pointer");
-  hipStream_t s = as_stream(stream);
   if (n == 0) {
     SNV_HIP(hipMemsetAsync(acc, 0, sizeof(float), s));
     return 0;
   }
   const int grid = (int)std::min<long>(cdiv(n / 4 + 1, 256), kSqBlocks);
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, (long)n, x);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid), dim3(256), 0, s, (long)n, x, part);
   SNV_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, grid, acc);
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, grid, (const float*)part, acc);
   SNV_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int snvrag_sqnorm(int64_t n, const float* x, float* acc, void* stream) {
+  return sqnorm_impl(n, x, acc, nullptr, as_stream(stream));
+}
+
+extern "C" size_t snvrag_sqnorm_ws_bytes(void) { return kSqBlocks * sizeof(float); }
+
+extern "C" int snvrag_sqnorm_ws(int64_t n, const float* x, float* acc, float* ws, size_t ws_bytes, void* stream) {
+  SNV_CHECK_ARG(ws && ws_bytes >= kSqBlocks * sizeof(float), "workspace smaller than snvrag_sqnorm_ws_bytes()");
+  return sqnorm_impl(n, x, acc, ws, as_stream(stream));
 }
 
 extern "C" int snvrag_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16,

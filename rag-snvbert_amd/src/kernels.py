@@ -549,12 +549,19 @@ def focal_loss(probs: torch.Tensor, labels: torch.Tensor, mask: torch.Tensor, ga
     return loss_acc, grad
 
 
-def sqnorm(x: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+def sqnorm(x: torch.Tensor, acc: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """sum x^2 (f32, fixed reduction order) into acc [1]; the per-block partials go to ``ws`` (a
+    caller-owned f32 buffer of snvrag_sqnorm_ws_bytes(), allocated here when not given) — never
+    shared between calls on different streams."""
     N.require_gpu(x)
     assert x.dtype == torch.float32
     if acc is None:
         acc = torch.empty(1, device=x.device, dtype=torch.float32)
-    check(N.lib().snvrag_sqnorm(x.numel(), ptr(_c(x)), ptr(acc), stream_ptr()), "sqnorm")
+    nb = int(N.lib().snvrag_sqnorm_ws_bytes())
+    if ws is None or ws.numel() * ws.element_size() < nb:
+        ws = torch.empty(nb // 4, device=x.device, dtype=torch.float32)
+    check(N.lib().snvrag_sqnorm_ws(x.numel(), ptr(_c(x)), ptr(acc), ptr(ws), ws.numel() * ws.element_size(),
+                                   stream_ptr()), "sqnorm")
     return acc
 
 

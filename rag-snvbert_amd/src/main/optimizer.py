@@ -85,6 +85,8 @@ class FusedAdam:
         self.m = torch.zeros_like(flat.flat)
         self.v = torch.zeros_like(flat.flat)
         self.sq = torch.zeros(1, device=flat.flat.device, dtype=torch.float32)
+        self.sq_ws = torch.empty(int(K.N.lib().snvrag_sqnorm_ws_bytes()) // 4, device=flat.flat.device,
+                                 dtype=torch.float32)      # the norm's per-block partials (this optimizer's own)
         self.step_count = 0
         self.param_groups = [{"lr": lr}]          # ScheduledOptim writes the LR here
 
@@ -95,7 +97,7 @@ class FusedAdam:
         self.step_count += 1
         lr = float(self.param_groups[0]["lr"])
         if self.max_grad_norm and self.max_grad_norm > 0:
-            self.K.sqnorm(self.fp.grad, self.sq)
+            self.K.sqnorm(self.fp.grad, self.sq, ws=self.sq_ws)
         self.K.adam_step(self.fp.flat, self.fp.grad, self.m, self.v, lr=lr, betas=self.betas, eps=self.eps,
                          weight_decay=self.weight_decay, step=self.step_count, grad_scale=grad_scale,
                          max_norm=self.max_grad_norm or 0.0, sq=self.sq if self.max_grad_norm else None,

@@ -142,6 +142,8 @@ _SIGS = {
                               C.c_uint64, vp], C.c_int),
     "snvrag_focal_loss": ([i64, C.c_int, vp, vp, vp, f32, f32, vp, vp, vp], C.c_int),
     "snvrag_sqnorm": ([i64, vp, vp, vp], C.c_int),
+    "snvrag_sqnorm_ws_bytes": ([], sz),
+    "snvrag_sqnorm_ws": ([i64, vp, vp, vp, sz, vp], C.c_int),
     "snvrag_adam_step": ([i64, vp, vp, vp, vp, vp, vp, C.POINTER(AdamS), vp], C.c_int),
     "snvrag_confusion": ([i64, C.c_int, vp, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_infer_post": ([i64, vp, vp, vp, vp, vp, vp], C.c_int),
