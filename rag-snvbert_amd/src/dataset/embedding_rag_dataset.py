@@ -62,7 +62,7 @@ class EmbeddingRAGDataset(TrainDataset):
         if panel_cache not in ("window", "fresh"):
             raise ValueError("panel_cache must be 'window' (the reference's per-window snapshot) or 'fresh'")
         self.panel_cache = panel_cache
-        self._panel_snap = None          # (window, W snapshot, A_r snapshot) of the cached window
+        self._panel_snap = None          # (window, W snapshot, A_r snapshot, weights token) of the cached window
         self.maf_mask_percentage, self.use_dynamic_mask = maf_mask_percentage, use_dynamic_mask
         self.current_epoch, self.name = 0, name
         self.ref_tokens_complete: List[np.ndarray] = []
@@ -207,6 +207,27 @@ class EmbeddingRAGDataset(TrainDataset):
                    ref_gt=ref_gt, ref_pos=ref_pos, embedding_layer=embedding_layer, name=name)
 
 
+def _weights_token(P) -> tuple:
+    """Host-side identity of the weights the retrieval embeds with: the optimizer's update count
+    (the fused Adam updates in place without bumping tensor versions) and the token table's
+    storage and version (torch in-place updates, e.g. load_state_dict)."""
+    from .. import autograd_ops
+    base = P.W._base if P.W._base is not None else P.W
+    return autograd_ops._EPOCH[0], base.data_ptr(), base._version
+
+
+def h2d(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    """Host -> device copy that does not synchronise the host with the device queue: a pageable
+    source is staged through the pinned caching allocator first (a pageable copy waits for the
+    stream to drain — at the start of a training step that left the GPU idle while the host
+    ran the retrieval's Python)."""
+    if t.device == dev or dev.type != "cuda" or t.device.type != "cpu":
+        return t.to(dev)
+    if not t.is_pinned():
+        t = t.pin_memory()
+    return t.to(dev, non_blocking=True)
+
+
 def panel_index_of(alleles: np.ndarray, ref_af: np.ndarray, device, shard=None):
     """PanelIndex of one window's panel, or of this rank's contiguous range of it."""
     from ..retrieval import PanelIndex
@@ -230,9 +251,9 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
     train = embedding_layer.training
     P = eng.packed(allow_train=True)
     dev = torch.device(device)
-    h1 = batch["hap_1"].to(dev, non_blocking=True).long()
-    h2 = batch["hap_2"].to(dev, non_blocking=True).long()
-    af = batch["af"].to(dev, non_blocking=True).float()
+    h1 = h2d(batch["hap_1"], dev).long()
+    h2 = h2d(batch["hap_2"], dev).long()
+    af = h2d(batch["af"], dev).float()
     B, L = h1.shape
     D = P.W.shape[1]
     groups = defaultdict(list)
@@ -255,15 +276,22 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
         # the reference's cache trigger (:334-336): another window cached, or reset at epoch start
         new_snap = stale and (ds.jit_cache_win_idx != w or ds._panel_snap is None or ds._panel_snap[0] != w)
         index = ds.panel_index(w, dev)
-        rows_t = torch.tensor(rows, device=dev, dtype=torch.long)
+        rows_t = h2d(torch.tensor(rows, dtype=torch.long), dev)
         tok = torch.cat([h1[rows_t], h2[rows_t]], 0).contiguous()
         n = index.n_sites
-        site_mask = torch.as_tensor(np.asarray(masks[w][1:1 + n], np.uint8), device=dev)
+        site_mask = h2d(torch.from_numpy(np.ascontiguousarray(masks[w][1:1 + n], np.uint8)), dev)
         ref_af = index.ref_af
         # A_q - A_r vanishes when the query AF rows equal the panel's window AF (always for
         # windows built from one freq table); otherwise pass both AF embeddings (exact LUT form).
+        # (a device -> host answer: asked only where the search needs it — not under train-mode
+        # dropout, whose exact-LUT offsets carry the AF embeddings anyway)
         afw = af[rows_t]
-        same = bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw)))
+        same_memo = []
+
+        def same_af() -> bool:
+            if not same_memo:
+                same_memo.append(bool(torch.equal(afw, ref_af.unsqueeze(0).expand_as(afw))))
+            return same_memo[0]
         counts = uniq = None
         p_drop = embedding_layer.dropout.p if train else 0.0
         with torch.no_grad():
@@ -271,11 +299,14 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                 if P.af is not None else None
             Wp, stale_w = None, False
             if stale:
+                wtok = _weights_token(P)
                 if new_snap:   # eval-mode panel embedding of this window under the weights of now
-                    ds._panel_snap = (w, P.W.detach().float().clone(), Ar_emb)
-                _, W_s, Ar_s = ds._panel_snap
-                # weights unchanged since the snapshot (its first batch): the plain search is the same
-                stale_w = not (torch.equal(W_s, P.W) and (Ar_s is None or torch.equal(Ar_s, Ar_emb)))
+                    ds._panel_snap = (w, P.W.detach().float().clone(), Ar_emb, wtok)
+                _, W_s, Ar_s, wtok_s = ds._panel_snap
+                # weights untouched since the snapshot (its first batch): the plain search is the
+                # same.  Decided on the host from the weights' update count (optimizer steps, torch
+                # in-place updates) — comparing the tensors was a device sync per training step
+                stale_w = wtok != wtok_s
                 if stale_w:
                     Wp, Ar_emb = W_s, Ar_s
             Aq_drop = None
@@ -290,7 +321,7 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                 from ..retrieval.shards import any_rank, kernel_ops, sharded_neighbours
                 drop_any = any_rank(p_drop > 0, dev, shard.group)
                 # a snapshot A_r differs from the queries' current AF embedding even for equal AF
-                exact = P.af is not None and not drop_any and (stale_w or any_rank(not same, dev, shard.group))
+                exact = P.af is not None and not drop_any and (stale_w or any_rank(not same_af(), dev, shard.group))
                 ops = kernel_ops(index, P.W, site_mask, k, limbs,
                                  aq_fn=lambda a: eng.af_embedding(a, True).float().contiguous(),
                                  Ar=Ar_emb if (exact or drop_any) else None, Wp=Wp)
@@ -312,7 +343,7 @@ def retrieve(ds, batch: dict, embedding_layer, device, k: int, masks: List[np.nd
                 if Aq_drop is not None:
                     Aq, aq_period = Aq_drop, 2 * len(rows)
                     Ar = Ar_emb if Ar_emb is not None else torch.zeros(L, D, device=dev)
-                elif (stale_w or not same) and P.af is not None:
+                elif P.af is not None and (stale_w or not same_af()):
                     Aq = eng.af_embedding(afw, True).float().contiguous()
                     Ar = Ar_emb
                 idx, _ = index.search(tok, P.W, site_mask, k, limbs=limbs, Aq=Aq, aq_period=aq_period, Ar=Ar,

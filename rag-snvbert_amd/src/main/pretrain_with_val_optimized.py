@@ -110,9 +110,12 @@ class BERTTrainerWithValidationOptimized:
 
     # ------------------------------------------------------------------ batch --
     def to_device(self, data: Dict) -> Dict:
+        """Batch tensors to the device without a host sync (pageable ones through pinned staging)."""
+        from ..dataset.embedding_rag_dataset import h2d
+        dev = torch.device(self.device)
         out = {}
         for k, v in data.items():
-            out[k] = v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v
+            out[k] = h2d(v, dev) if torch.is_tensor(v) else v
         return out
 
     def loss(self, output, data) -> torch.Tensor:

@@ -262,6 +262,21 @@ def neighbour_embeddings(emb, groups: List[NeighbourGroup], B: int, L: int, dens
     return out
 
 
+def _unique_padded(x: torch.Tensor):
+    """(uniq, inverse) of torch.unique(x, return_inverse=True) with ``uniq`` padded to x.numel()
+    by repeating its largest value — computed by sort + run starts + prefix sum, no host sync."""
+    flat = x.reshape(-1)
+    srt, perm = torch.sort(flat)
+    start = torch.ones_like(srt, dtype=torch.bool)
+    start[1:] = srt[1:] != srt[:-1]
+    rank = torch.cumsum(start, 0) - 1
+    inv = torch.empty_like(flat)
+    inv[perm] = rank
+    uniq = srt[-1:].expand(flat.numel()).clone()
+    uniq[rank] = srt
+    return uniq, inv.view_as(x)
+
+
 def _unique_neighbour_embed(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor, g: NeighbourGroup,
                             pe: torch.Tensor, L: int, p: float, dense: bool, tok0: int = 5, sos: int = 2,
                             eos: int = 3, pad: int = 0) -> torch.Tensor:
@@ -270,14 +285,21 @@ def _unique_neighbour_embed(W: torch.Tensor, Ar: torch.Tensor, idx: torch.Tensor
     nq, k = idx.shape
     n_sites = g.index.n_sites
     valid = idx >= 0
+    fused = not dense and train_dtype() != torch.float32 and W.shape[0] * W.shape[1] <= 16384
     if g.uniq is not None:
         uniq, rows_codes = g.uniq, g.uniq_codes
         inv = torch.searchsorted(uniq, idx.clamp(min=0))
+    elif fused:
+        # torch.unique's inverse without its host sync (the unique COUNT is device data): the
+        # same sorted ranks, the unique list padded to nq * k with its last value (the fused
+        # kernels touch only the rows ``inv`` names)
+        uniq, inv = _unique_padded(idx.clamp(min=0))
+        rows_codes = g.index.codes[uniq - g.index.ref_offset]
     else:
         uniq, inv = torch.unique(idx.clamp(min=0), return_inverse=True)
         rows_codes = g.index.codes[uniq - g.index.ref_offset]
     U = uniq.numel()
-    if not dense and train_dtype() != torch.float32 and W.shape[0] * W.shape[1] <= 16384:
+    if fused:
         # fused: no [U, L, D] embeddings, one dropout mask per unique neighbour (csrc/train.hip)
         inv_v = torch.where(valid, inv, torch.full_like(inv, -1))
         return nbr_mean_drop(W, Ar, inv_v, rows_codes[:, :n_sites], n_sites, pe[:L], p)

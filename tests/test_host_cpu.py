@@ -215,3 +215,18 @@ def test_small_weight_gradient_chunked_vs_fp64(M, N, Kd):
     torch.testing.assert_close(gw, lin.weight.grad, rtol=1e-4, atol=1e-3 * math.sqrt(M / 1000))
     torch.testing.assert_close(gb, lin.bias.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gx, x.grad)
+
+
+def test_unique_padded_matches_torch_unique():
+    """train_forward._unique_padded (the neighbour dedup of the fused re-encode, no host sync) ==
+    torch.unique(return_inverse=True): same inverse, same sorted unique values, padded with the
+    largest one."""
+    import torch
+    from src.train_forward import _unique_padded
+    g = torch.Generator().manual_seed(3)
+    for shape in [(1, 1), (48, 8), (7, 3), (384, 1)]:
+        x = torch.randint(0, 40, shape, generator=g)
+        u, i = torch.unique(x, return_inverse=True)
+        up, ip = _unique_padded(x)
+        assert torch.equal(ip, i)
+        assert up.numel() == x.numel() and torch.equal(up[:u.numel()], u) and bool((up[u.numel():] == u[-1]).all())
