@@ -562,7 +562,7 @@ def pmc_traffic(kernel_name):
     on this bench, committed as profiles/pmc_traffic.json), launch-weighted over the kernel class."""
     f = REPO / "profiles" / "pmc_traffic.json"
     cls = {"rows_gemm_kernel": "gemm", "tail_kernel": "ffn", "ffn_kernel": "ffn", "attn32_bf16": "attention",
-           "knn_emb_dot_kernel": "knn_emb"}
+           "attn32_dma": "attention", "knn_emb_dot_kernel": "knn_emb"}
     key = next((v for k, v in cls.items() if kernel_name.startswith(k)), None)
     if key is None or not f.exists():
         return None

@@ -1186,6 +1186,16 @@ static int launch_tailp(TailArgs a, hipStream_t s) {
 template <int D, bool PRE>
 static int launch_tail(TailArgs a, hipStream_t s) {
   const int var = (int)options().tail_variant;
+  // the wide-row form (tailw.hip): every weight fragment loaded once per workgroup into the
+  // registers of the one wave that uses it
+  if constexpr (PRE && D == 384)
+    if (var == 0 && options().tail_wide) {
+      const long nwg = cdiv(a.M, TL_ROWS);
+      const int64_t dz = options().tail_desync;
+      const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 25000) : 0;
+      return tailw_launch(a.M, a.act, a.resid, a.out, a.ws, a.vec, a.b_o, a.g1, a.be1, a.eps, desync,
+                          (int)options().tail_wide == 2 ? 1 : 0, s);
+    }
   // the persistent kernel (option tail_persist; measured no faster, see tailp_kernel): 32-bit
   // byte offsets of the in-place rows
   if constexpr (PRE)

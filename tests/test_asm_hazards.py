@@ -4,7 +4,8 @@ it places right after one — e.g. a register move re-homing an accumulator on t
 could read the accumulator before the MFMA has written it (seen once: 4 of 384 outputs of one
 tile off by their last k16 step, only at 7 token groups).  This compiles the kernel to assembly
 for gfx950 and checks that no instruction reads an MFMA's destination registers before the
-drain (s_nop 7) or three further MFMAs."""
+drain (s_nop 7) or three further MFMAs.  The wide-row block tail (csrc/tailw.hip) is checked the
+same way."""
 import os
 import re
 import shutil
@@ -13,7 +14,7 @@ import subprocess
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "..", "rag-snvbert_amd", "csrc", "gemm256.hip")
+CSRC = os.path.join(HERE, "..", "rag-snvbert_amd", "csrc")
 
 
 def _regs(tok):
@@ -34,7 +35,10 @@ def _reads(ins):
 
 
 @pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
-def test_no_accumulator_read_inside_mfma_latency(tmp_path):
+@pytest.mark.parametrize("src", ["gemm256.hip", "tailw.hip"])
+def test_no_accumulator_read_inside_mfma_latency(tmp_path, src):
+    """Also the wide-row block tail (csrc/tailw.hip), whose MFMAs are inline asm for the same reason."""
+    SRC = os.path.join(CSRC, src)
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     out = tmp_path / "g.s"
     subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only", SRC, "-o",

@@ -324,6 +324,49 @@ def test_tail32_kernel(D, M):
     assert (out.double() - ref).abs().mean() < 1e-2
 
 
+@pytest.mark.parametrize("M", [777, 128 * 3, 1, 4 * 1030 + 5, 64 * 1030])
+def test_tail_wide_kernel(M):
+    """Wide-row block tail (csrc/tailw.hip, option tail_wide: wave w owns features 96w..96w+95 and
+    hidden chunks 4c + w, its weight fragments loaded straight into its registers; att / x1 and the
+    hidden of a round are the LDS-resident operands) vs float64 torch with test_tail32_kernel's bar,
+    in place; and close to tail_kernel on the same operands (the same function; the accumulation
+    order of the bias and of the cross-wave row statistics differs).  Ragged M: 777, one row, a
+    partial last tile, 515 workgroups."""
+    D = 384
+    g = torch.Generator(device="cpu").manual_seed(11 * M + 3)
+    bf, F = torch.bfloat16, torch.nn.functional
+    x = torch.randn(M, D, generator=g).to(DEV, bf)
+    att = (0.5 * torch.randn(M, D, generator=g)).to(DEV, bf)
+    w_o = (torch.randn(D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    b_o = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    g1, be1 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w1 = (torch.randn(4 * D, D, generator=g) / math.sqrt(D)).to(DEV, bf)
+    w2 = (torch.randn(D, 4 * D, generator=g) / math.sqrt(4 * D)).to(DEV)
+    b1, b2 = torch.randn(4 * D, generator=g).to(DEV), torch.randn(D, generator=g).to(DEV)
+    gf, bff = (1 + 0.2 * torch.randn(4 * D, generator=g)).to(DEV), (0.1 * torch.randn(4 * D, generator=g)).to(DEV)
+    g2, be2 = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV), (0.1 * torch.randn(D, generator=g)).to(DEV)
+    w2g, b2g, _ = K().fold_layernorm(w2, b2, gf, bff, bf)
+    vec = K().ffn_vec(b1, b2g, w2g, g2, be2)
+    ts = K().tail_pack(w_o, w1, w2g)
+    x1 = F.layer_norm(x.double() + att.double() @ w_o.double().T + b_o.double(), (D,), g1.double(), be1.double(), 1e-5)
+    h = F.leaky_relu(x1 @ w1.double().T + b1.double(), 0.1)
+    hn = F.layer_norm(h, (4 * D,), gf.double(), bff.double(), 1e-5)
+    f = F.leaky_relu(hn @ w2.double().T + b2.double(), 0.1)
+    ref = F.layer_norm(x1 + f, (D,), g2.double(), be2.double(), 1e-5)
+    ya, yb = x.clone(), x.clone()
+    with K().option("tail_wide", 1):
+        out = K().tail_forward(att, ya, ts, b_o, g1, be1, vec)
+    assert out.data_ptr() == ya.data_ptr()
+    K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
+    assert torch.isfinite(ya.float()).all()
+    torch.testing.assert_close(ya.double(), ref, rtol=5e-2, atol=5e-2)
+    ea, eb = (ya.double() - ref).abs().mean(), (yb.double() - ref).abs().mean()
+    assert ea < 1e-2 and ea < 1.25 * eb + 1e-4, (float(ea), float(eb))
+    # vs tail_kernel: a few bf16 steps at most (the hidden is rounded to bf16 in both)
+    d = (ya.float() - yb.float()).abs()
+    assert bool((d <= 4 * _bf16_step(yb.float().abs().clamp_min(2 ** -6))).all()), float(d.max())
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_encoder_fused_equals_unfused(dt, monkeypatch):
     """Encoder stack with LN fused into GEMM epilogues/prologues == the 8-launch unfused stack."""

@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 CLASSES = {"rows_gemm_kernel": "gemm", "wsg_kernel": "gemm", "sg_kernel": "gemm", "mlp_kernel": "gemm", "ffn_kernel": "ffn",
-           "tail_kernel": "ffn", "attn32_bf16": "attention", "scan2_kernel": "knn_scan", "knn_emb_dot_kernel": "knn_emb"}
+           "tail_kernel": "ffn", "attn32_bf16": "attention", "attn32_dma": "attention", "scan2_kernel": "knn_scan", "knn_emb_dot_kernel": "knn_emb"}
 
 
 def load(d, counter):
@@ -25,7 +25,9 @@ def load(d, counter):
             name = r["Kernel_Name"]
             for key, cls in CLASSES.items():
                 if key in name:
-                    vals[(cls, r.get("Grid_Size", ""))].append(float(r["Counter_Value"]))
+                    short = name.split("(")[0].replace("void ", "").replace("snvrag::", "")
+                    vals[(cls, r.get("Grid_Size", ""), short)].append(float(r["Counter_Value"]))
+                    break
     return vals, files
 
 
@@ -33,10 +35,10 @@ def main(d):
     out = {}
     fetch, ff = load(d, "FETCH_SIZE")
     write, wf = load(d, "WRITE_SIZE")
-    for (cls, grid), v in fetch.items():
-        w = write.get((cls, grid), [])
+    for (cls, grid, short), v in fetch.items():
+        w = write.get((cls, grid, short), [])
         e = out.setdefault(cls, [])
-        e.append({"grid": grid, "launches": len(v), "fetch_bytes": 2 * 1024 * sum(v) / len(v),
+        e.append({"kernel": short, "grid": grid, "launches": len(v), "fetch_bytes": 2 * 1024 * sum(v) / len(v),
                   "write_bytes": 1024 * sum(w) / len(w) if w else None})
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of bench.py --steps 2",
            "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB -> bytes", "kernels": out,
