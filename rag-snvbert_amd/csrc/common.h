@@ -75,7 +75,7 @@ struct Options {
   int64_t g2_variant;      // wide-row GEMM diagnostics: 1 no LDS-DMA, 2 no MFMA (wrong results; timing only),
                            // 3 stamps into the snvrag_tail_stamps buffer
   int64_t tail_persist;    // 1: the persistent block tail (tailp_kernel, A/B); 0 (default): tail_kernel
-  int64_t tail_wide;       // block tail at D = 384 (PRE): 1 the wide-row form (tailw.hip), 0 tail_kernel,
+  int64_t tail_wide;       // block tail at D = 384 (PRE): 1 (default) the wide-row form (tailw.hip), 0 tail_kernel,
                            // 2 the wide-row form with phase stamps into the snvrag_tail_stamps buffer
 };
 Options& options();

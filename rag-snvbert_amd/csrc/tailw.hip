@@ -32,6 +32,10 @@
 
 namespace snvrag {
 
+#ifndef TW_PACKED_LN
+#define TW_PACKED_LN 1                               // LayerNorm epilogues in packed f32 (v_pk_*) math
+#endif
+
 constexpr int TW_D = 384, TW_NT = 12, TW_KS = 24;
 constexpr int TW_FRAG = 1024;
 constexpr int TW_FPRE = TW_NT * TW_KS;               // W_o' fragments (288)
@@ -40,55 +44,110 @@ constexpr int TW_NFRAG = TW_FPRE + 24 * TW_FPC;      // whole stream (2592)
 constexpr int TW_X = 0;                              // LDS: X images (96 KiB)
 constexpr int TW_H = 96 * 1024;                      // LDS: H images (64 KiB)
 constexpr int TW_LDS = 160 * 1024;
-constexpr int TW_L = 3;                              // k16 steps of W loads in flight ahead
-constexpr int TW_R = TW_L + 1;                       // W register slots (divides 24 and 40)
-constexpr int TW_QA = 24;                            // phase-A (out-projection) steps
-constexpr int TW_RS = 40;                            // steps per FFN round: 24 FFN1 + 16 FFN2
-constexpr int TW_IB = 20;                            // FFN1 step after which the chunk's b1 loads issue
-constexpr int TW_NB1 = 8;                            // b1 loads per chunk
-static_assert(TW_QA % TW_R == 0 && TW_RS % TW_R == 0, "W slots periodic over phase A and the rounds");
+// W fragments: one stream per wave in consumption order, TW_AH fragments in flight ahead of the
+// step being consumed, in a ring of TW_RING registers (fragment n in register n % 12)
+constexpr int TW_AH = 9;
+constexpr int TW_RING = 12;
+// k16 steps: q in [0, 24) phase A (3 W_o' fragments each); [24, 48) FFN1 of half-round 0 (1 W1
+// fragment); half-round h = 1 .. 11: 32 steps at 48 + 32 (h - 1): FFN1(h) x 24 (1), FFN2(h - 1) x 8
+// (3 W2' fragments); [400, 408) FFN2(11)
+constexpr int TW_QA = 24;
+constexpr int TW_Q0 = 48;
+constexpr int TW_HS = 32;
+constexpr int TW_QF = TW_Q0 + 11 * TW_HS;
+constexpr int TW_QEND = TW_QF + 8;
+constexpr int TW_QREP = TW_Q0 + TW_HS;               // half-round 2: the loop's representative steps
+constexpr int TW_NB1 = 4;                            // b1 loads of one half-round's tile
 
-// W fragments loaded for global step q (phase A: 3 W_o' tiles; FFN1: 2 W1 tiles; FFN2: 3 W2' tiles)
-__host__ __device__ constexpr int tw_nf(int q) { return q < TW_QA ? 3 : ((q - TW_QA) % TW_RS < 24 ? 2 : 3); }
-// other vector-memory ops a wave issues during step q, after that step's W loads (the b1 loads)
-__host__ __device__ constexpr int tw_extra(int q) { return q >= TW_QA && (q - TW_QA) % TW_RS == TW_IB ? TW_NB1 : 0; }
-// vector-memory ops issued after step q's W loads up to the wait before step q's MFMAs: the loads
-// of steps q+1 .. q+L-1 (issued during steps q-L+1 .. q-1) and the extras of steps q-L .. q-1
+__host__ __device__ constexpr int tw_nf(int q) {
+  return q < 0 ? 0 : q < TW_QA ? 3 : q < TW_Q0 ? 1 : q < TW_QF ? ((q - TW_Q0) % TW_HS < 24 ? 1 : 3) : q < TW_QEND ? 3 : 0;
+}
+__host__ __device__ constexpr int tw_f0(int q) {     // first fragment of step q
+  if (q <= TW_QA) return 3 * q;
+  if (q <= TW_Q0) return 72 + (q - TW_QA);
+  if (q <= TW_QF) {
+    const int k = (q - TW_Q0) / TW_HS, r = (q - TW_Q0) % TW_HS;
+    return 96 + 48 * k + (r <= 24 ? r : 24 + 3 * (r - 24));
+  }
+  return q <= TW_QEND ? 624 + 3 * (q - TW_QF) : 648;
+}
+__host__ __device__ constexpr int tw_step_of(int m) {  // the step that consumes fragment m
+  if (m < 72) return m / 3;
+  if (m < 96) return TW_QA + (m - 72);
+  if (m < 624) {
+    const int k = (m - 96) / 48, r = (m - 96) % 48;
+    return TW_Q0 + TW_HS * k + (r < 24 ? r : 24 + (r - 24) / 3);
+  }
+  return TW_QF + (m - 624) / 3;
+}
+constexpr int TW_NFRAGW = 648;                       // fragments per wave
+// the b1 loads (after the step's W loads): half-round 0's at its FFN1 step 16, half-round h's
+// (h >= 1) at the first FFN2 step of its iteration
+__host__ __device__ constexpr int tw_extra(int q) {
+  return (q == TW_QA + 16 || (q >= TW_Q0 && q < TW_QF && (q - TW_Q0) % TW_HS == 24)) ? TW_NB1 : 0;
+}
+// the step during which fragment n is issued (-1: the prologue); step q issues [f0(q) + AH, + nf(q))
+__host__ __device__ constexpr int tw_issuer(int n) { return n < TW_AH ? -1 : tw_step_of(n - TW_AH); }
+__host__ __device__ constexpr int tw_min(int a, int b) { return a < b ? a : b; }
+// vector-memory ops issued after step q's last fragment up to the wait before step q's MFMAs
 __host__ __device__ constexpr int tw_younger(int q) {
-  int n = 0;
-  for (int j = 1; j < TW_L; ++j) n += tw_nf(q + j);
-  for (int j = q - TW_L; j < q; ++j)
-    if (j >= 0) n += tw_extra(j);
+  const int nl = tw_f0(q) + tw_nf(q) - 1;
+  int n = tw_min(tw_f0(q) + TW_AH, TW_NFRAGW) - 1 - nl;
+  const int qi = tw_issuer(nl);
+  for (int j = qi < 0 ? 0 : qi; j < q; ++j) n += tw_extra(j);
   return n;
 }
-// ops issued after the b1 loads (during step IB) up to the chunk epilogue (after step 23)
-__host__ __device__ constexpr int tw_b1_younger() {
+// ops issued during steps qa+1 .. qb
+__host__ __device__ constexpr int tw_ops_between(int qa, int qb) {
   int n = 0;
-  for (int i = TW_IB + 1; i < 24; ++i) n += tw_nf(TW_QA + i + TW_L);
+  for (int q = qa + 1; q <= qb; ++q) n += (tw_f0(q) + TW_AH < TW_NFRAGW ? tw_nf(q) : 0) + tw_extra(q);
   return n;
 }
-static_assert(tw_younger(TW_QA + TW_RS) == tw_younger(TW_QA) && tw_younger(TW_QA + TW_RS + 1) == tw_younger(TW_QA + 1) &&
-                  tw_younger(TW_QA + TW_RS + 2) == tw_younger(TW_QA + 2),
-              "round waits periodic");
+// b1 of half-round h - 1 waited for at FFN1 step 2 of half-round h (h = 1: loaded at step 40; h >= 2:
+// at the previous iteration's first FFN2 step): the smaller count is safe for every h
+constexpr int TW_B1_WAIT = tw_min(tw_ops_between(TW_QA + 16, TW_Q0 + 2), tw_ops_between(TW_Q0 + 24, TW_QREP + 2));
+// b1 of half-round 11 (loaded at step 392), waited for after step 399
+constexpr int TW_B1_WAIT_END = tw_ops_between(TW_Q0 + 10 * TW_HS + 24, TW_QF - 1);
+// the loop body serves half-rounds 1 .. 11: its wait at step i of an iteration is the smallest
+// count over them (h = 1 sees half-round 0's b1 loads in its first windows) — a smaller count only
+// waits for more
+__host__ __device__ constexpr int tw_younger_it(int i) {
+  int m = 63;
+  for (int h = 1; h <= 11; ++h) m = tw_min(m, tw_younger(TW_Q0 + (h - 1) * TW_HS + i));
+  return m;
+}
+// step q's wait: in the loop (the representative half-round's steps) the iteration minimum
+__host__ __device__ constexpr int tw_wait_of(int q) {
+  return (q >= TW_QREP && q < TW_QREP + TW_HS) ? tw_younger_it(q - TW_QREP) : tw_younger(q);
+}
+__host__ __device__ constexpr bool tw_ring_periodic() {
+  return tw_f0(TW_QEND) == TW_NFRAGW && tw_f0(TW_QA) % TW_RING == 0 && tw_f0(TW_Q0) % TW_RING == 0 &&
+         tw_f0(TW_QREP) % TW_RING == 0 && (tw_f0(TW_QREP + TW_HS) - tw_f0(TW_QREP)) % TW_RING == 0 &&
+         tw_f0(TW_QF) % TW_RING == 0;
+}
+static_assert(tw_ring_periodic(), "fragment ring registers periodic over the sections");
+static_assert(TW_B1_WAIT_END <= 63 && tw_younger(0) <= 63, "vmcnt range");
 
 template <typename Body, int... Is>
 __device__ __forceinline__ void tw_unroll(Body&& body, std::integer_sequence<int, Is...>) {
   (body(std::integral_constant<int, Is>{}), ...);
 }
+// (s_nop 1 first: hipcc pads nothing inside an asm string, and it may place a VALU write of an
+// operand — a register copy, an AGPR read — right before it; 2 wait states cover that hazard)
 template <bool AGPR>
 __device__ __forceinline__ void tw_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
   if constexpr (AGPR)
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
   else
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
 }
 // zero C operand: the accumulator's first k-step
 template <bool AGPR>
 __device__ __forceinline__ void tw_mfma0(f32x16& c, const u32x4& a, const u32x4& b) {
   if constexpr (AGPR)
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
   else
-    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
 }
 // a 32x32x16 result is readable 18 wait states after issue
 __device__ __forceinline__ void tw_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
@@ -100,11 +159,11 @@ __device__ __forceinline__ void tw_drain_o(f32x16 (&a)[3][4]) {
                  "+a"(a[1][2]), "+a"(a[1][3]), "+a"(a[2][0]), "+a"(a[2][1]), "+a"(a[2][2]), "+a"(a[2][3])
                :: "memory");
 }
-__device__ __forceinline__ void tw_drain_h(f32x16 (&h)[2][4]) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
-               : "+v"(h[0][0]), "+v"(h[1][0]), "+v"(h[0][1]), "+v"(h[1][1]), "+a"(h[0][2]), "+a"(h[1][2]),
-                 "+a"(h[0][3]), "+a"(h[1][3])
-               :: "memory");
+template <bool AGPR> __device__ __forceinline__ void tw_drain_h4(f32x16 (&h)[4]) {
+  if constexpr (AGPR)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(h[0]), "+a"(h[1]), "+a"(h[2]), "+a"(h[3]) :: "memory");
+  else
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]) :: "memory");
 }
 __device__ __forceinline__ int tw_lane() {
   int l;
@@ -121,6 +180,16 @@ __device__ __forceinline__ float tw_lrelu(float x) {
   float r;
   asm("v_mul_f32 %0, 0x3dcccccd, %1\n v_max_f32 %0, %1, %0" : "=&v"(r) : "v"(x));
   return r;
+}
+typedef float tw_f2 __attribute__((ext_vector_type(2)));
+// the two bf16 of a packed word as floats (low half first)
+__device__ __forceinline__ tw_f2 tw_bf2(uint32_t w) { return tw_f2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
+__device__ __forceinline__ tw_f2 tw_lrelu2(tw_f2 x) {
+  const tw_f2 m = x * 0.1f;                           // one v_pk_mul_f32
+  float a, b;
+  asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(x.x), "v"(m.x));
+  asm("v_max_f32 %0, %1, %2" : "=v"(b) : "v"(x.y), "v"(m.y));
+  return tw_f2{a, b};
 }
 __device__ __forceinline__ float tw_bf(const u32x4& v, int j) {
   return (j & 1) ? __uint_as_float(v[j >> 1] & 0xffff0000u) : __uint_as_float(v[j >> 1] << 16);
@@ -139,10 +208,17 @@ __device__ __forceinline__ void tw_ld16(uint32_t addr, float (&v)[16]) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = __uint_as_float(r[i >> 2][i & 3]);
 }
-// wait until at most Y younger vector-memory ops are in flight; w's uses are ordered after it
-template <int Y> __device__ __forceinline__ void tw_waitw(u32x4 (&w)[3]) {
+// wait until at most Y younger vector-memory ops are in flight; the fragments' uses are ordered after it
+#ifndef TW_ASM_WAITS
+#define TW_ASM_WAITS 0                                 // 1: hand-counted waits on asm loads (diagnostics)
+#endif
+template <int Y> __device__ __forceinline__ void tw_wait1(u32x4& a) {
   static_assert(Y >= 0 && Y <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]) : "n"(Y) : "memory");
+  if constexpr (TW_ASM_WAITS) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(Y) : "memory");
+}
+template <int Y> __device__ __forceinline__ void tw_wait3(u32x4& a, u32x4& b, u32x4& c) {
+  static_assert(Y >= 0 && Y <= 63, "vmcnt range");
+  if constexpr (TW_ASM_WAITS) asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(Y) : "memory");
 }
 template <int OFF> __device__ __forceinline__ void tw_load_off(u32x4& r, int voff, const i32x4& rsrc, int so) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4" : "=v"(r) : "v"(voff), "s"(rsrc), "s"(so), "n"(OFF) : "memory");
@@ -197,32 +273,27 @@ void tailw_kernel(TwArgs p) {
     for (int s = 0; s < TW_KS; ++s)
       dma_x4(ars, lds0 + TW_X + (s * 4 + wave) * TW_FRAG, voff, 64 * (s >> 1) + 16 * (s & 1));
   }
-  u32x4 wr[TW_R][3];
+  u32x4 wf[TW_RING];                                 // W fragment ring
   // W fragment F of the stream into register r (soffset: scalar)
-  auto loadW = [&](u32x4& r, int F) {
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(lane16), "s"(wrs), "s"(F * TW_FRAG) : "memory");
+  // (compiler-visible loads: its waitcnt pass places the waits before every read of the register —
+  // hand-counted asm loads were seen copied into AGPRs by the register allocator before they landed)
+  const __amdgpu_buffer_rsrc_t wrb = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, TW_NFRAG * TW_FRAG, 0x00020000);
+  auto loadW = [&](u32x4& r, int F) { r = __builtin_amdgcn_raw_buffer_load_b128(wrb, lane16, F * TW_FRAG, 0); };
+  // stream offsets: FFN1(h) step i = wave w's tile of chunk 4 (h >> 1) + w, half h & 1;
+  // FFN2(h) step u, tile t = chunk 4 (h >> 1) + u / 2, k16 step 2 (h & 1) + u % 2, tile 3w + t
+  auto f_ffn1 = [&](int h, int i) { return TW_FPRE + (4 * (h >> 1) + wave) * TW_FPC + 2 * i + (h & 1); };
+  auto f_ffn2 = [&](int h, int u, int t) {
+    return TW_FPRE + (4 * (h >> 1) + (u >> 1)) * TW_FPC + 48 + (2 * (h & 1) + (u & 1)) * NT + 3 * wave + t;
   };
-  // the loads of global step q (compile-time position in the pattern; c = its round, runtime)
-  auto issueW = [&](auto q_tag, int c) {
-    constexpr int q = decltype(q_tag)::value;
-    constexpr int slot = q % TW_R;
-    if constexpr (q < TW_QA) {
-#pragma unroll
-      for (int t = 0; t < 3; ++t) loadW(wr[slot][t], q * NT + 3 * wave + t);
-    } else {
-      constexpr int i = (q - TW_QA) % TW_RS;
-      const int cc = c < 5 ? c : 5;                  // overrun steps past the last round re-read it
-      if constexpr (i < 24) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) loadW(wr[slot][t], TW_FPRE + (4 * cc + wave) * TW_FPC + 2 * i + t);
-      } else {
-        constexpr int u = i - 24, cl = u >> 2, s2 = u & 3;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) loadW(wr[slot][t], TW_FPRE + (4 * cc + cl) * TW_FPC + 48 + s2 * NT + 3 * wave + t);
-      }
-    }
+  // fragment n of the prologue / phase A / half-round 0 (n < 120: W_o' k16 step n / 3 tile n % 3,
+  // FFN1(0), FFN1(1))
+  auto issue_a = [&](auto n_tag) {
+    constexpr int n = decltype(n_tag)::value;
+    if constexpr (n < 72) loadW(wf[n % TW_RING], (n / 3) * NT + 3 * wave + n % 3);
+    else if constexpr (n < 96) loadW(wf[n % TW_RING], f_ffn1(0, n - 72));
+    else loadW(wf[n % TW_RING], f_ffn1(1, n - 96));
   };
-  tw_unroll([&](auto qc) { issueW(qc, 0); }, std::make_integer_sequence<int, TW_L>{});
+  tw_unroll([&](auto nc) { issue_a(nc); }, std::make_integer_sequence<int, TW_AH>{});
   u32x4 rr[3][4][2];                                 // residual x: tile t, group g, half h2
   {
     const int l = tw_lane();
@@ -255,28 +326,29 @@ void tailw_kernel(TwArgs p) {
 
   // ---- phase A: ao = att W_o'^T (wave w: tiles 3w .. 3w+2 x 4 token groups, AGPRs)
   f32x16 acc[3][4];
-  u32x4 bq[2][4];
+  u32x4 bq[3][4];                                     // B fragments, read two k16 steps ahead
   auto rdB = [&](uint32_t base, int blk) -> u32x4 {
     return *reinterpret_cast<const u32x4*>(smem + base + blk * TW_FRAG + lane16);
   };
-  auto waitW = [&](auto q_tag) {
-    constexpr int q = decltype(q_tag)::value;
-    tw_waitw<tw_younger(q)>(wr[q % TW_R]);
-  };
+  // (B fragments one step ahead in two buffers here: 12 MFMAs per step cover the LDS latency, and
+  // a third buffer beside the residual rows pushed the W fragments into AGPR copies taken before
+  // their loads had landed)
 #pragma unroll
   for (int g = 0; g < 4; ++g) bq[0][g] = rdB(TW_X, g);
   tw_unroll([&](auto qc) {
-    constexpr int q = decltype(qc)::value, slot = q % TW_R;
-    waitW(qc);
+    constexpr int q = decltype(qc)::value, n0 = 3 * q;
+    tw_wait3<tw_younger(q)>(wf[n0 % TW_RING], wf[(n0 + 1) % TW_RING], wf[(n0 + 2) % TW_RING]);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        if constexpr (q == 0) tw_mfma0<true>(acc[t][g], wr[slot][t], bq[q & 1][g]);
-        else tw_mfma<true>(acc[t][g], wr[slot][t], bq[q & 1][g]);
+        if constexpr (q == 0) tw_mfma0<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
+        else tw_mfma<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
       }
       if constexpr (q + 1 < TW_KS) bq[(q + 1) & 1][g] = rdB(TW_X, (q + 1) * 4 + g);
-      if (g == 1) issueW(std::integral_constant<int, q + TW_L>{}, 0);
+      if (g == 1)
+        tw_unroll([&](auto tc) { issue_a(std::integral_constant<int, n0 + TW_AH + decltype(tc)::value>{}); },
+                  std::make_integer_sequence<int, 3>{});
     }
     __builtin_amdgcn_sched_barrier(0);
   }, std::make_integer_sequence<int, TW_QA>{});
@@ -287,6 +359,34 @@ void tailw_kernel(TwArgs p) {
   float2* s1 = reinterpret_cast<float2*>(smem + TW_H + 8 * 1024);          // [wave][128 rows]
   {
     const uint32_t tb = lds0 + TW_H + 64 * (tw_lane() >> 5);
+#if TW_PACKED_LN
+    // (packed f32 math: pairs of features per v_pk_* instruction)
+    tw_f2 s2v[4], q2v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      float bo[16];
+      tw_ld16(tb + 4 * 32 * (3 * wave + t), bo);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const tw_f2 v = tw_f2{acc[t][g][2 * e], acc[t][g][2 * e + 1]} + tw_f2{bo[2 * e], bo[2 * e + 1]} +
+                          tw_bf2(rr[t][g][e >> 2][e & 3]);
+          acc[t][g][2 * e] = v.x;
+          acc[t][g][2 * e + 1] = v.y;
+          s2v[g] += v;
+          q2v[g] = v * v + q2v[g];
+        }
+    }
+    float sum[4], sq[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      sum[g] = s2v[g].x + s2v[g].y;
+      sq[g] = q2v[g].x + q2v[g].y;
+    }
+#else
     float sum[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -302,6 +402,7 @@ void tailw_kernel(TwArgs p) {
           sq[g] = fmaf(v, v, sq[g]);
         }
     }
+#endif
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -340,8 +441,19 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float y[16];
+#if TW_PACKED_LN
+        const float nmr = -mean[g] * rstd[g];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const tw_f2 z = (tw_f2{acc[t][g][2 * e], acc[t][g][2 * e + 1]} * rstd[g] + nmr) * tw_f2{gg[2 * e], gg[2 * e + 1]} +
+                          tw_f2{bb[2 * e], bb[2 * e + 1]};
+          y[2 * e] = z.x;
+          y[2 * e + 1] = z.y;
+        }
+#else
 #pragma unroll
         for (int i = 0; i < 16; ++i) y[i] = (acc[t][g][i] - mean[g]) * rstd[g] * gg[i] + bb[i];
+#endif
         // x1 features 32T + 16hh + 8h2 + j = k16 step 2T + h2, lane slot (n, kh = hh)
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2)
@@ -354,10 +466,15 @@ void tailw_kernel(TwArgs p) {
   tw_barrier();                                       // x1 complete in X
   stamp(3);
 
-  // ---- FFN rounds
-#pragma unroll
-  for (int g = 0; g < 4; ++g) bq[0][g] = rdB(TW_X, g);
-  f32x16 hac[2][4];                                   // FFN1 accumulators: groups 0, 1 VGPRs, 2, 3 AGPRs
+  // ---- FFN in 12 half-rounds.  Half-round h: wave w's FFN1 tile (32 hidden units: chunk
+  // 4 (h >> 1) + w, half h & 1) over all 128 rows into hv / ha (even / odd h: VGPRs / AGPRs), while
+  // the chunk epilogue of half-round h - 1 (b1, LeakyReLU, LN_f sums, bf16) is interleaved between
+  // its MFMAs and writes that hidden into H half (h - 1) & 1; one barrier; then FFN2 of half-round
+  // h - 1 (the 4 waves' tiles = 8 k16 steps) from that H half.  H is double-buffered, so the next
+  // half-round's epilogue writes the other half while this FFN2 reads.
+  // B fragments: FFN2 step u uses bq[u % 3], FFN1 step i bq[(i + 2) % 3] (so that FFN2's
+  // last two steps prefetch the next FFN1's first two), each read two steps ahead.
+  f32x16 hv[4], ha[4];
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -366,83 +483,156 @@ void tailw_kernel(TwArgs p) {
   for (int t = 0; t < 3; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(acc[t][g]));
-  float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
-  u32x4 b1v[2][4];
-#pragma unroll 1
-  for (int c = 0; c < 6; ++c) {
-    // FFN1: hac = x1 W1_{4c+w}^T (k16 step i: tiles t = 0, 1 of the chunk)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 sf1[4], sf2[4];                                  // LN_f partial sums (pairs of hidden units)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) sf1[g] = sf2[g] = f2{0.f, 0.f};
+  u32x4 b1v[4];                                       // b1 of the tile whose epilogue runs next
+  const __amdgpu_buffer_rsrc_t b1b = __builtin_amdgcn_make_buffer_rsrc((void*)p.vec, (short)0, 4 * D * 4, 0x00020000);
+  auto b1_load = [&](int h) {                         // b1[64 c' + 32 (h & 1) + 8 r + 4 hh .. + 3]
+    const int so = 4 * (64 * (4 * (h >> 1) + wave) + 32 * (h & 1));
+    const int vo = 16 * (tw_lane() >> 5);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b1v[r] = __builtin_amdgcn_raw_buffer_load_b128(b1b, vo + 32 * r, so, 0);
+  };
+  // epilogue unit k (0 .. 7: group k / 2, k16 step j = k % 2 of the tile) of the half-round with
+  // parity Q: 8 hidden units of this lane's token -> its 16-B slot of an FFN2 B fragment in H half Q
+  auto epi_unit = [&](auto k_tag, auto q_tag) {
+    constexpr int k = decltype(k_tag)::value, Q = decltype(q_tag)::value, g = k >> 1, j = k & 1;
+    const f32x16& a = Q ? ha[g] : hv[g];
+    uint32_t pk[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      const int i0 = 8 * j + 2 * e2;
+      f2 x = f2{a[i0], a[i0 + 1]} +
+             f2{__uint_as_float(b1v[i0 >> 2][i0 & 3]), __uint_as_float(b1v[(i0 + 1) >> 2][(i0 + 1) & 3])};
+      x = f2{tw_lrelu(x.x), tw_lrelu(x.y)};
+      sf1[g] += x;
+      sf2[g] = x * x + sf2[g];
+      pk[e2] = tw_pack2(x.x, x.y);
+    }
+    *reinterpret_cast<u32x4*>(smem + TW_H + Q * 32768 + ((wave * 2 + j) * 4 + g) * TW_FRAG + lane16) =
+        u32x4{pk[0], pk[1], pk[2], pk[3]};
+  };
+  // fragment r of an iteration (r relative to its first fragment; h = the iteration's half-round):
+  // [0, 24) FFN1(h), [24, 48) FFN2(h - 1), then the next iteration's FFN1(h + 1) (LAST: FFN2(11))
+  auto issue_it = [&](auto r_tag, int h, auto last_tag) {
+    constexpr int r = decltype(r_tag)::value, n = r;  // iteration starts are multiples of the ring
+    if constexpr (r < 24) loadW(wf[n % TW_RING], f_ffn1(h, r));
+    else if constexpr (r < 48) loadW(wf[n % TW_RING], f_ffn2(h - 1, (r - 24) / 3, (r - 24) % 3));
+    else if constexpr (decltype(last_tag)::value) loadW(wf[n % TW_RING], f_ffn2(h, (r - 48) / 3, (r - 48) % 3));
+    else loadW(wf[n % TW_RING], f_ffn1(h + 1, r - 48));
+  };
+  // FFN1(h), parity P; Q0 = its first global step (the representative half-round for h >= 1);
+  // EPI: with the epilogue of half-round h - 1 (units at steps 2, 5, ..., 23)
+  auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag) {
+    constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
+    constexpr bool EPI = decltype(epi_tag)::value;
+    constexpr int F0 = tw_f0(Q0);
     tw_unroll([&](auto ic) {
-      constexpr int i = decltype(ic)::value, q = TW_QA + i;
-      constexpr int slot = q % TW_R;
-      waitW(std::integral_constant<int, q>{});
+      constexpr int i = decltype(ic)::value, q = Q0 + i, n = F0 + i;
+      tw_wait1<tw_wait_of(q)>(wf[n % TW_RING]);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          if constexpr (i == 0) {
-            if (g < 2) tw_mfma0<false>(hac[t][g], wr[slot][t], bq[i & 1][g]);
-            else tw_mfma0<true>(hac[t][g], wr[slot][t], bq[i & 1][g]);
-          } else {
-            if (g < 2) tw_mfma<false>(hac[t][g], wr[slot][t], bq[i & 1][g]);
-            else tw_mfma<true>(hac[t][g], wr[slot][t], bq[i & 1][g]);
-          }
+        if constexpr (P == 0) {
+          if constexpr (i == 0) tw_mfma0<false>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          else tw_mfma<false>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+        } else {
+          if constexpr (i == 0) tw_mfma0<true>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          else tw_mfma<true>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
         }
-        if constexpr (i + 1 < 24) bq[(i + 1) & 1][g] = rdB(TW_X, (i + 1) * 4 + g);
-        if (g == 1) issueW(std::integral_constant<int, q + TW_L>{}, c);
+        if constexpr (i + 2 < 24) bq[(i + 4) % 3][g] = rdB(TW_X, (i + 2) * 4 + g);
+        if (g == 1) {
+          if constexpr (Q0 == TW_QA) issue_a(std::integral_constant<int, n + TW_AH>{});
+          else issue_it(std::integral_constant<int, i + TW_AH>{}, h, std::false_type{});
+        }
       }
-      if constexpr (i == TW_IB) {
-        // b1 of chunk 4c + w: bv[t][r] = b1[64 (4c + w) + 32 t + 8 r + 4 hh .. + 3]
-        const int so = 4 * 64 * (4 * c + wave);
-        tw_unroll([&](auto kc) {
-          constexpr int k = decltype(kc)::value, t = k >> 2, r = k & 3;
-          tw_load_off<4 * (32 * t + 8 * r)>(b1v[t][r], 16 * (tw_lane() >> 5), brs, so);
-        }, std::make_integer_sequence<int, 8>{});
+      if constexpr (Q0 == TW_QA && i == 16) b1_load(0);
+      if constexpr (EPI && i >= 2 && (i - 2) % 3 == 0) {
+        epi_unit(std::integral_constant<int, (i - 2) / 3>{}, std::integral_constant<int, 1 - P>{});
       }
       __builtin_amdgcn_sched_barrier(0);
     }, std::make_integer_sequence<int, 24>{});
-    tw_drain_h(hac);
-    asm volatile("s_barrier" ::: "memory");           // every wave done reading H (last round's FFN2)
-    asm volatile("s_waitcnt vmcnt(%8)"
-                 : "+v"(b1v[0][0]), "+v"(b1v[0][1]), "+v"(b1v[0][2]), "+v"(b1v[0][3]), "+v"(b1v[1][0]),
-                   "+v"(b1v[1][1]), "+v"(b1v[1][2]), "+v"(b1v[1][3])
-                 : "n"(tw_b1_younger()) : "memory");
-    // chunk epilogue: h = lrelu(acc + b1), LN_f sums, bf16 -> H block (w, 2t + h2, g), this lane's slot
+    if constexpr (P == 0) tw_drain_h4<false>(hv);
+    else tw_drain_h4<true>(ha);
+  };
+  // FFN2(h) from H half h & 1 (P = h & 1); in the loop (Q0 = representative) its iteration is h + 1;
+  // LAST: the iteration of h = 10, whose lookahead loads FFN2(11); FINAL: FFN2(11) itself
+  auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag) {
+    constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
+    constexpr bool LAST = decltype(last_tag)::value, FINAL = decltype(final_tag)::value;
+    constexpr uint32_t HB = TW_H + P * 32768;
+    constexpr int F0 = tw_f0(Q0);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float h[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          h[i] = tw_lrelu(hac[t][g][i] + __uint_as_float(b1v[t][i >> 2][i & 3]));
-          st1[g] += h[i];
-          st2[g] = fmaf(h[i], h[i], st2[g]);
-        }
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
-          *reinterpret_cast<u32x4*>(smem + TW_H + ((wave * 4 + 2 * t + h2) * 4 + g) * TW_FRAG + lane16) =
-              u32x4{tw_pack2(h[8 * h2], h[8 * h2 + 1]), tw_pack2(h[8 * h2 + 2], h[8 * h2 + 3]),
-                    tw_pack2(h[8 * h2 + 4], h[8 * h2 + 5]), tw_pack2(h[8 * h2 + 6], h[8 * h2 + 7])};
-      }
-    tw_barrier();                                     // the round's hidden complete in H
-#pragma unroll
-    for (int g = 0; g < 4; ++g) bq[0][g] = rdB(TW_H, g);
-    // FFN2: acc += W2'_{4c+cl} h^T (k16 step u = 4 cl + s2: tiles 3w .. 3w+2)
+    for (int g = 0; g < 4; ++g) {
+      bq[0][g] = rdB(HB, g);
+      bq[1][g] = rdB(HB, 4 + g);
+    }
     tw_unroll([&](auto uc) {
-      constexpr int u = decltype(uc)::value, q = TW_QA + 24 + u;
-      constexpr int slot = q % TW_R;
-      waitW(std::integral_constant<int, q>{});
+      constexpr int u = decltype(uc)::value, q = Q0 + u, n0 = F0 + 3 * u;
+      tw_wait3<tw_wait_of(q)>(wf[n0 % TW_RING], wf[(n0 + 1) % TW_RING], wf[(n0 + 2) % TW_RING]);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
 #pragma unroll
-        for (int t = 0; t < 3; ++t) tw_mfma<true>(acc[t][g], wr[slot][t], bq[u & 1][g]);
-        if constexpr (u + 1 < 16) bq[(u + 1) & 1][g] = rdB(TW_H, (u + 1) * 4 + g);
-        else bq[(u + 1) & 1][g] = rdB(TW_X, g);       // the next round's first FFN1 step
-        if (g == 1) issueW(std::integral_constant<int, q + TW_L>{}, c + (q + TW_L >= TW_QA + TW_RS ? 1 : 0));
+        for (int t = 0; t < 3; ++t) tw_mfma<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
+        if constexpr (u + 2 < 8) bq[(u + 2) % 3][g] = rdB(HB, (u + 2) * 4 + g);
+        else if constexpr (!FINAL && !LAST) bq[(u + 2) % 3][g] = rdB(TW_X, (u - 6) * 4 + g);   // next FFN1 steps 0, 1
+        if (g == 1) {
+          if constexpr (FINAL) {
+            if constexpr (n0 + TW_AH < TW_NFRAGW)
+              tw_unroll([&](auto tc) {
+                constexpr int m = n0 + TW_AH + decltype(tc)::value;
+                if constexpr (m < TW_NFRAGW) loadW(wf[m % TW_RING], f_ffn2(h, (m - F0) / 3, (m - F0) % 3));
+              }, std::make_integer_sequence<int, 3>{});
+          } else {
+            tw_unroll([&](auto tc) {
+              issue_it(std::integral_constant<int, 24 + 3 * u + TW_AH + decltype(tc)::value>{}, h + 1, last_tag);
+            }, std::make_integer_sequence<int, 3>{});
+          }
+        }
       }
+      // b1 of the FFN1 tile just computed (half-round h + 1), after this step's W loads (tw_extra)
+      if constexpr (u == 0 && !FINAL) b1_load(h + 1);
       __builtin_amdgcn_sched_barrier(0);
-    }, std::make_integer_sequence<int, 16>{});
+    }, std::make_integer_sequence<int, 8>{});
     tw_drain_o(acc);
+  };
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bq[2][g] = rdB(TW_X, g);
+    bq[0][g] = rdB(TW_X, 4 + g);
+  }
+  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{});
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bq[2][g] = rdB(TW_X, g);
+    bq[0][g] = rdB(TW_X, 4 + g);
+  }
+#pragma unroll 1
+  for (int h = 1; h < 11; h += 2) {
+    seg1(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+    tw_barrier();                                     // H half (h - 1) & 1 complete
+    seg2(h - 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
+         std::false_type{});
+    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+    tw_barrier();
+    seg2(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
+         std::false_type{});
+  }
+  seg1(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+  tw_barrier();
+  seg2(10, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::true_type{},
+       std::false_type{});
+  // the epilogue of half-round 11, then its FFN2
+  tw_unroll([&](auto kc) { epi_unit(kc, std::integral_constant<int, 1>{}); }, std::make_integer_sequence<int, 8>{});
+  tw_barrier();
+  seg2(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QF>{}, std::false_type{},
+       std::true_type{});
+  float st1[4], st2[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    st1[g] = sf1[g].x + sf1[g].y;
+    st2[g] = sf2[g].x + sf2[g].y;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the overrun loads have landed
   stamp(4);
@@ -481,6 +671,40 @@ void tailw_kernel(TwArgs p) {
   }
   const uint32_t eb = lds0 + TW_H + 64 * (tw_lane() >> 5);
   {
+#if TW_PACKED_LN
+    // u = hr (acc - hm c1) + b2' = acc hr + (b2' - hm hr c1), in pairs (v_pk_fma_f32)
+    tw_f2 s2v[4], q2v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int T = 3 * wave + t;
+      float b2[16], c1[16];
+      tw_ld16(eb + 4 * (32 * T), b2);
+      tw_ld16(eb + 4 * (D + 32 * T), c1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 xa = rdB(TW_X, (2 * T) * 4 + g), xb = rdB(TW_X, (2 * T + 1) * 4 + g);
+        const float nhh = -hm[g] * hr[g];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const tw_f2 k = tw_f2{c1[2 * e], c1[2 * e + 1]} * nhh + tw_f2{b2[2 * e], b2[2 * e + 1]};
+          const tw_f2 u = tw_lrelu2(tw_f2{acc[t][g][2 * e], acc[t][g][2 * e + 1]} * hr[g] + k);
+          const tw_f2 v = u + tw_bf2((e < 4 ? xa : xb)[e & 3]);
+          acc[t][g][2 * e] = v.x;
+          acc[t][g][2 * e + 1] = v.y;
+          s2v[g] += v;
+          q2v[g] = v * v + q2v[g];
+        }
+      }
+    }
+    float sum[4], sq[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      sum[g] = s2v[g].x + s2v[g].y;
+      sq[g] = q2v[g].x + q2v[g].y;
+    }
+#else
     float sum[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -502,6 +726,7 @@ void tailw_kernel(TwArgs p) {
         }
       }
     }
+#endif
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -542,7 +767,16 @@ void tailw_kernel(TwArgs p) {
         const float nmr = -mean[g] * rstd[g];
         float y[16];
 #pragma unroll
+#if TW_PACKED_LN
+        for (int e = 0; e < 8; ++e) {
+          const tw_f2 z = (tw_f2{acc[t][g][2 * e], acc[t][g][2 * e + 1]} * rstd[g] + nmr) * tw_f2{g2[2 * e], g2[2 * e + 1]} +
+                          tw_f2{be2[2 * e], be2[2 * e + 1]};
+          y[2 * e] = z.x;
+          y[2 * e + 1] = z.y;
+        }
+#else
         for (int i = 0; i < 16; ++i) y[i] = fmaf(fmaf(acc[t][g][i], rstd[g], nmr), g2[i], be2[i]);
+#endif
         if (r < p.M) {
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2)

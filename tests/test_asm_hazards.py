@@ -66,3 +66,47 @@ def test_no_accumulator_read_inside_mfma_latency(tmp_path, src):
                 break
     assert n_mfma > 1000
     assert not bad, bad[:5]
+
+
+def _pending_reads(ins):
+    """Reads of a register whose vector-memory load has not been retired by an s_waitcnt vmcnt yet
+    (the waits counted in issue order, as the hardware does).  An inline-asm load hides its
+    latency from the compiler, which may then copy the destination register (e.g. into an AGPR
+    under register pressure) before the data lands."""
+    pending, bad = [], []
+    for i, t in enumerate(ins):
+        op = t.split(" ")[0]
+        m = re.match(r"s_waitcnt.*vmcnt\((\d+)\)", t)
+        if m:
+            n = int(m.group(1))
+            pending = pending[len(pending) - n:] if len(pending) > n else pending
+            continue
+        if op.startswith(("buffer_load", "global_load", "scratch_load")):
+            pending.append(set() if " lds" in t else _regs(t.split(None, 1)[1].split(",")[0].strip()))
+            continue
+        if op.startswith(("buffer_store", "global_store", "scratch_store")):
+            pending.append(set())
+        if " " in t and op.startswith(("v_", "ds_write")):
+            srcs = _reads(t) if op.startswith("v_") else set().union(*[_regs(o.strip().split()[0])
+                                                                       for o in t.split(None, 1)[1].split(",") if o.strip()])
+            if any(d & srcs for d in pending):
+                bad.append((i, t))
+    return bad
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_wide_tail_no_read_before_load_lands(tmp_path):
+    """csrc/tailw.hip: no instruction reads a register still waiting for its load."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    out = tmp_path / "t.s"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
+                    os.path.join(CSRC, "tailw.hip"), "-o", str(out)], check=True, capture_output=True)
+    text = out.read_text().split("\n")
+    name = "_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:"
+    i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
+    i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
+    ins = [ln.strip() for ln in text[i0:i1]]
+    ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
+    assert sum(t.startswith("v_mfma") for t in ins) > 1000
+    bad = _pending_reads(ins)
+    assert not bad, bad[:5]

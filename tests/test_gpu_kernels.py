@@ -357,14 +357,18 @@ def test_tail_wide_kernel(M):
     with K().option("tail_wide", 1):
         out = K().tail_forward(att, ya, ts, b_o, g1, be1, vec)
     assert out.data_ptr() == ya.data_ptr()
-    K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
+    with K().option("tail_wide", 0):
+        K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
     assert torch.isfinite(ya.float()).all()
     torch.testing.assert_close(ya.double(), ref, rtol=5e-2, atol=5e-2)
     ea, eb = (ya.double() - ref).abs().mean(), (yb.double() - ref).abs().mean()
     assert ea < 1e-2 and ea < 1.25 * eb + 1e-4, (float(ea), float(eb))
-    # vs tail_kernel: a few bf16 steps at most (the hidden is rounded to bf16 in both)
+    # vs tail_kernel: the hidden is rounded to bf16 in both, from differently ordered f32 sums, so
+    # a hidden unit may land one bf16 step apart and move outputs by a few steps; measured at the
+    # bench shape: max 0.031, mean 4e-6, 0.2 % of the outputs differ
     d = (ya.float() - yb.float()).abs()
-    assert bool((d <= 4 * _bf16_step(yb.float().abs().clamp_min(2 ** -6))).all()), float(d.max())
+    assert float(d.max()) <= 0.0625 and float(d.mean()) < 1e-4, (float(d.max()), float(d.mean()))
+    assert int((d > 0).sum()) <= max(16, d.numel() // 50), int((d > 0).sum())
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
@@ -620,11 +624,12 @@ def test_tail_persistent_equals_tail_kernel(M):
     vec = K().ffn_vec(b1, b2g, w2g, g2, be2)
     ts = K().tail_pack(w_o, w1, w2g)
     ya, yb, yc = x.clone(), x.clone(), x.clone()
-    with K().option("tail_persist", 1):
-        K().tail_forward(att, ya, ts, b_o, g1, be1, vec)
-    K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
-    with K().option("tail_variant", 1):                  # tail_kernel with 4 fragments read ahead
-        K().tail_forward(att, yc, ts, b_o, g1, be1, vec)
+    with K().option("tail_wide", 0):                     # (the engine's default is the wide-row tail)
+        with K().option("tail_persist", 1):
+            K().tail_forward(att, ya, ts, b_o, g1, be1, vec)
+        K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
+        with K().option("tail_variant", 1):              # tail_kernel with 4 fragments read ahead
+            K().tail_forward(att, yc, ts, b_o, g1, be1, vec)
     assert torch.equal(yb, yc)
     assert torch.isfinite(ya.float()).all()
     # the same arithmetic; the compilers' f32 contraction choices in the LayerNorm statistics may

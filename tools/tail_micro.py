@@ -11,6 +11,7 @@ from src import kernels as K  # noqa: E402
 
 D = 384
 dev, bf = "cuda", torch.bfloat16
+K.set_option("tail_wide", 0)                         # this tool measures tail_kernel / tailp_kernel
 F = torch.nn.functional
 
 
