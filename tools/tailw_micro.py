@@ -85,8 +85,31 @@ def timeit(wide, reps=10):
 
 
 fl = 18.0 * M * D * D
+flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+
+
+def timeit_cold(wide, reps=8):
+    """each launch after a 512 MB write (weights and activations out of L2 / MALL, as in the
+    encoder where QKV and attention stream GBs between two block tails); events around the tail only"""
+    K.set_option("tail_wide", wide)
+    tot = 0.0
+    for _ in range(reps):
+        flush.fill_(1)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        K.tail_forward(c["att"], xs, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+        b.record()
+        torch.cuda.synchronize()
+        tot += a.elapsed_time(b)
+    K.set_option("tail_wide", 0)
+    return tot / reps
+
+
 for _ in range(30):
     timeit(0, 1)
+for it in range(2):
+    for wide in (0, 1):
+        print(f"cold caches: {'tailw (wide)' if wide else 'tail_kernel '} {timeit_cold(wide):.4f} ms", flush=True)
 res = {0: [], 1: []}
 for it in range(4):
     for wide in (0, 1):
