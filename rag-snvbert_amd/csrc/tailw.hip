@@ -132,22 +132,32 @@ template <typename Body, int... Is>
 __device__ __forceinline__ void tw_unroll(Body&& body, std::integer_sequence<int, Is...>) {
   (body(std::integral_constant<int, Is>{}), ...);
 }
-// (s_nop 1 first: hipcc pads nothing inside an asm string, and it may place a VALU write of an
-// operand — a register copy, an AGPR read — right before it; 2 wait states cover that hazard)
-template <bool AGPR>
+// NOP: s_nop 1 ahead of the MFMA — hipcc pads nothing inside an asm string, and outside the FFN
+// loop (phase A, half-round 0, the last half-rounds) it stashes W fragments in AGPRs and reads one
+// back right before its MFMA (a VALU write of an operand: 2 wait states); the loop body has no such
+// write (tests/test_asm_hazards.py scans for it)
+template <bool AGPR, bool NOP = true>
 __device__ __forceinline__ void tw_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
-  if constexpr (AGPR)
+  if constexpr (AGPR && NOP)
     asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-  else
+  else if constexpr (AGPR)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  else if constexpr (NOP)
     asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
 }
 // zero C operand: the accumulator's first k-step
-template <bool AGPR>
+template <bool AGPR, bool NOP = true>
 __device__ __forceinline__ void tw_mfma0(f32x16& c, const u32x4& a, const u32x4& b) {
-  if constexpr (AGPR)
+  if constexpr (AGPR && NOP)
     asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
-  else
+  else if constexpr (AGPR)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+  else if constexpr (NOP)
     asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
 }
 // a 32x32x16 result is readable 18 wait states after issue
 __device__ __forceinline__ void tw_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
@@ -525,9 +535,9 @@ void tailw_kernel(TwArgs p) {
   };
   // FFN1(h), parity P; Q0 = its first global step (the representative half-round for h >= 1);
   // EPI: with the epilogue of half-round h - 1 (units at steps 2, 5, ..., 23)
-  auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag) {
+  auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag, auto nop_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
-    constexpr bool EPI = decltype(epi_tag)::value;
+    constexpr bool EPI = decltype(epi_tag)::value, NOP = decltype(nop_tag)::value;
     constexpr int F0 = tw_f0(Q0);
     tw_unroll([&](auto ic) {
       constexpr int i = decltype(ic)::value, q = Q0 + i, n = F0 + i;
@@ -535,11 +545,11 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         if constexpr (P == 0) {
-          if constexpr (i == 0) tw_mfma0<false>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
-          else tw_mfma<false>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          if constexpr (i == 0) tw_mfma0<false, NOP>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          else tw_mfma<false, NOP>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
         } else {
-          if constexpr (i == 0) tw_mfma0<true>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
-          else tw_mfma<true>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          if constexpr (i == 0) tw_mfma0<true, NOP>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
+          else tw_mfma<true, NOP>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
         }
         if constexpr (i + 2 < 24) bq[(i + 4) % 3][g] = rdB(TW_X, (i + 2) * 4 + g);
         if (g == 1) {
@@ -558,9 +568,10 @@ void tailw_kernel(TwArgs p) {
   };
   // FFN2(h) from H half h & 1 (P = h & 1); in the loop (Q0 = representative) its iteration is h + 1;
   // LAST: the iteration of h = 10, whose lookahead loads FFN2(11); FINAL: FFN2(11) itself
-  auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag) {
+  auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag, auto nop_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
     constexpr bool LAST = decltype(last_tag)::value, FINAL = decltype(final_tag)::value;
+    constexpr bool NOP = decltype(nop_tag)::value;
     constexpr uint32_t HB = TW_H + P * 32768;
     constexpr int F0 = tw_f0(Q0);
 #pragma unroll
@@ -574,7 +585,7 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
 #pragma unroll
-        for (int t = 0; t < 3; ++t) tw_mfma<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
+        for (int t = 0; t < 3; ++t) tw_mfma<true, NOP>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
         if constexpr (u + 2 < 8) bq[(u + 2) % 3][g] = rdB(HB, (u + 2) * 4 + g);
         else if constexpr (!FINAL && !LAST) bq[(u + 2) % 3][g] = rdB(TW_X, (u - 6) * 4 + g);   // next FFN1 steps 0, 1
         if (g == 1) {
@@ -602,7 +613,7 @@ void tailw_kernel(TwArgs p) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
-  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{});
+  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, std::true_type{});
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     bq[2][g] = rdB(TW_X, g);
@@ -610,24 +621,24 @@ void tailw_kernel(TwArgs p) {
   }
 #pragma unroll 1
   for (int h = 1; h < 11; h += 2) {
-    seg1(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+    seg1(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::false_type{});
     tw_barrier();                                     // H half (h - 1) & 1 complete
     seg2(h - 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{});
-    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+         std::false_type{}, std::false_type{});
+    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::false_type{});
     tw_barrier();
     seg2(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{});
+         std::false_type{}, std::false_type{});
   }
-  seg1(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{});
+  seg1(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::true_type{});
   tw_barrier();
   seg2(10, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::true_type{},
-       std::false_type{});
+       std::false_type{}, std::true_type{});
   // the epilogue of half-round 11, then its FFN2
   tw_unroll([&](auto kc) { epi_unit(kc, std::integral_constant<int, 1>{}); }, std::make_integer_sequence<int, 8>{});
   tw_barrier();
   seg2(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QF>{}, std::false_type{},
-       std::true_type{});
+       std::true_type{}, std::true_type{});
   float st1[4], st2[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {

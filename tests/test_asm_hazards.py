@@ -110,3 +110,44 @@ def test_wide_tail_no_read_before_load_lands(tmp_path):
     assert sum(t.startswith("v_mfma") for t in ins) > 1000
     bad = _pending_reads(ins)
     assert not bad, bad[:5]
+
+
+def _valu_to_mfma(ins):
+    """A VALU write (register copy, AGPR read, ...) of an MFMA source register fewer than 2 wait
+    states before the inline-asm MFMA reading it: hipcc does not pad around asm it does not know is
+    an MFMA, and the MFMA would read the stale value."""
+    bad = []
+    for i, t in enumerate(ins):
+        if not t.startswith("v_mfma"):
+            continue
+        srcs = _reads(t)
+        ws, k = 0, i - 1
+        while k >= 0 and ws < 2:
+            u = ins[k]
+            if u.startswith("s_nop"):
+                ws += int(u.split()[1]) + 1
+            else:
+                if u.startswith("v_") and not u.startswith("v_mfma") and " " in u and \
+                        _regs(u.split(None, 1)[1].split(",")[0].strip()) & srcs:
+                    bad.append((u, t))
+                    break
+                ws += 1
+            k -= 1
+    return bad
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_wide_tail_no_valu_write_before_mfma_operand(tmp_path):
+    """csrc/tailw.hip: its FFN loop MFMAs carry no s_nop, so no VALU write may feed one directly."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    out = tmp_path / "t.s"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
+                    os.path.join(CSRC, "tailw.hip"), "-o", str(out)], check=True, capture_output=True)
+    text = out.read_text().split("\n")
+    for name in ("_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:", "_ZN6snvrag12tailw_kernelILi1EEEvNS_6TwArgsE:"):
+        i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
+        i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
+        ins = [ln.strip() for ln in text[i0:i1]]
+        ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
+        bad = _valu_to_mfma(ins)
+        assert not bad, (name, bad[:5])
