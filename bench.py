@@ -292,7 +292,8 @@ def main():
     peak_f = BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_PEAK_TFLOPS
     # roofline object = the MFMA kernel class with the most time per step
     mf = [("rows_gemm_kernel (encoder QKV/out-proj + fusion/head GEMMs)", gemm, "2*M*N*K averaged over launches"),
-          ("tail_kernel (block tail on 32x32 MFMAs: out-projection + LN1 + FFN + LN2, 12 launches)", ffn, "2*M*D*9D = 18*M*D^2 per launch"),
+          ("tailw_kernel (wide-row block tail on 32x32 MFMAs: out-projection + LN1 + FFN + LN2, 12 launches)", ffn,
+           "2*M*D*9D = 18*M*D^2 per launch"),
           ("attn32_dma (attention)", attn, "4*L^2*dh*H*nseq per launch")]
     name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
     roofline = dict(bound="mfma", kernel=name,
@@ -561,7 +562,7 @@ def pmc_traffic(kernel_name):
     """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes run by tools/pmc.sh
     on this bench, committed as profiles/pmc_traffic.json), launch-weighted over the kernel class."""
     f = REPO / "profiles" / "pmc_traffic.json"
-    cls = {"rows_gemm_kernel": "gemm", "tail_kernel": "ffn", "ffn_kernel": "ffn", "attn32_bf16": "attention",
+    cls = {"rows_gemm_kernel": "gemm", "tailw_kernel": "ffn", "tail_kernel": "ffn", "ffn_kernel": "ffn", "attn32_bf16": "attention",
            "attn32_dma": "attention", "knn_emb_dot_kernel": "knn_emb"}
     key = next((v for k, v in cls.items() if kernel_name.startswith(k)), None)
     if key is None or not f.exists():

@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 CLASSES = {"rows_gemm_kernel": "gemm", "wsg_kernel": "gemm", "sg_kernel": "gemm", "mlp_kernel": "gemm", "ffn_kernel": "ffn",
-           "tail_kernel": "ffn", "attn32_bf16": "attention", "attn32_dma": "attention", "scan2_kernel": "knn_scan", "knn_emb_dot_kernel": "knn_emb"}
+           "tailw_kernel": "ffn", "tail_kernel": "ffn", "attn32_bf16": "attention", "attn32_dma": "attention", "scan2_kernel": "knn_scan", "knn_emb_dot_kernel": "knn_emb"}
 
 
 def load(d, counter):
