@@ -75,6 +75,8 @@ struct Options {
   int64_t g2_variant;      // wide-row GEMM diagnostics: 1 no LDS-DMA, 2 no MFMA (wrong results; timing only),
                            // 3 stamps into the snvrag_tail_stamps buffer
   int64_t tail_persist;    // 1: the persistent block tail (tailp_kernel, A/B); 0 (default): tail_kernel
+  int64_t proj_wide;       // 1 (default): snvrag_proj_forward at D = 384 on the wide-row projection (tailw.hip,
+                           // 0.62 vs 0.68 ms, bit-identical); 0: tail.hip PROJ mode
   int64_t tail_wide;       // block tail at D = 384 (PRE): 1 (default) the wide-row form (tailw.hip), 0 tail_kernel,
                            // 2 the wide-row form with phase stamps into the snvrag_tail_stamps buffer
 };
@@ -85,6 +87,9 @@ unsigned long long* diag_stamps();
 // the wide-row block tail (tailw.hip), D = 384, PRE mode (out = LN2(FFN(LN1(x + att W_o^T))) in place)
 int tailw_launch(int M, const void* att, const void* resid, void* out, const void* ws, const float* vec,
                  const float* b_o, const float* g1, const float* be1, float eps, int desync, int var, hipStream_t s);
+
+// the wide-row projection (tailw.hip), D = 384: out[M, NC D] = x W^T + b on a snvrag_proj_pack stream
+int projw_launch(int M, int NC, const void* x, const void* ws, const float* bias, void* out, int desync, hipStream_t s);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -81,6 +81,8 @@ extern "C" int snvrag_encoder_forward(int dtype, int64_t nseq, int64_t L, int D,
       e.bias = ly.b_qkv;
       // QKV: the 8-wave stream GEMM (csrc/sgemm.hip); its 32-bit output offsets cap one launch
       // at 2 GiB, beyond that the 32x32 projection stream (csrc/tail.hip PROJ mode)
+      // (the wide-row projection, csrc/tailw.hip, measured 0.62-0.70 vs 0.54 ms for the 8-wave stream
+      // GEMM at M = 527 360: the stream GEMM stays; tools/proj_micro.py)
       if (dtype == SNVRAG_BF16 && ly.qkv_sg && M * 3 * D * 2 < (1L << 31))
         rc = snvrag_sgemm_forward(M, (int)D, (int)(3 * D), 0, SNVRAG_ACT_NONE, 0.f, xc, ly.qkv_sg, ly.b_qkv, nullptr,
                                   nullptr, 0, 0.f, qkv, nullptr, nullptr, stream);

@@ -103,7 +103,7 @@ const OptDesc kOpts[] = {
     {"sg_waves4", &Options::sg_waves4, 0},         {"ln_bwd_nopf", &Options::ln_bwd_nopf, 0},
     {"attn_variant", &Options::attn_variant, 0},   {"dw_xcd", &Options::dw_xcd, 1},
     {"ln_rows1", &Options::ln_rows1, 0},           {"tail_persist", &Options::tail_persist, 0},
-    {"tail_wide", &Options::tail_wide, 1},
+    {"tail_wide", &Options::tail_wide, 1},         {"proj_wide", &Options::proj_wide, 1},
     {"g2_variant", &Options::g2_variant, 0},     {"g2_groups", &Options::g2_groups, 0},
 };
 Options make_options() {

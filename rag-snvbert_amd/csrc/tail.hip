@@ -1343,6 +1343,15 @@ extern "C" int snvrag_proj_forward(int64_t M, int D, int NC, const void* x, cons
                    nullptr, 0.f, nullptr, 0};
   evlog_begin(s);
   int rc;
+  if (D == 384 && options().proj_wide && (long)M * NC * D * 2 < 0x7fffffffL) {
+    // the wide-row projection (tailw.hip): first-round stagger as the block tail's
+    const int64_t dz = options().sg_desync;
+    const int desync = cdiv(M, TL_ROWS) >= 8 * 256 ? (dz >= 0 ? (int)dz : 8000) : 0;
+    rc = projw_launch((int)M, NC, x, wstream, bias, out, desync, s);
+    if (rc) return rc;
+    evlog_end(s, EV_GEMM, 2.0 * M * (double)D * D * NC);
+    return 0;
+  }
   switch (D * 8 + NC) {
     case 128 * 8 + 1: rc = launch_proj<128, 1>(a, s); break;
     case 128 * 8 + 3: rc = launch_proj<128, 3>(a, s); break;

@@ -819,4 +819,125 @@ int tailw_launch(int M, const void* att, const void* resid, void* out, const voi
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Wide-row projection (option proj_wide; the encoder's QKV: out[M, NC D] = x W^T + b, D = 384,
+// multi_head_attention.py:44-51): the tail's phase A per output chunk of D features.  A
+// workgroup owns 128 rows (x by LDS-DMA into X once), wave w owns tiles 3w .. 3w+2 of each chunk;
+// per chunk 24 k16 steps x 12 MFMAs into 192 AGPR accumulators, then + bias -> bf16 -> two 16-B
+// stores per (tile, token group).  W fragments (snvrag_proj_pack: chunk c, k16 step s, tile T at
+// fragment c 288 + 12 s + T) through the 12-register ring 9 ahead, compiler-visible loads.
+struct PwArgs {
+  int M, NC;
+  const bf16* x;            // [M, D]
+  const char* ws;           // snvrag_proj_pack stream
+  const float* bias;        // [NC D]
+  bf16* out;                // [M, NC D]
+  int desync;
+};
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void projw_kernel(PwArgs p) {
+  constexpr int D = TW_D, NT = TW_NT, KS = TW_KS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long row0 = (long)blockIdx.x * 128;
+  if (p.desync > 0 && blockIdx.x < 256) {
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
+  const uint32_t lds0 = lds_addr(smem);
+  int lane16 = tw_lane() * 16;
+  asm volatile("" : "+v"(lane16));
+  const i32x4 xrs = dma_rsrc(p.x + row0 * D, ((long)p.M - row0) * D * 2);     // rows >= M read as 0
+  {
+    const int l = tw_lane();
+    const int voff = (32 * wave + (l & 31)) * (D * 2) + 32 * (l >> 5);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      dma_x4(xrs, lds0 + TW_X + (s * 4 + wave) * TW_FRAG, voff, 64 * (s >> 1) + 16 * (s & 1));
+  }
+  const int nfr = p.NC * TW_FPRE;
+  const __amdgpu_buffer_rsrc_t wrb = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, nfr * TW_FRAG, 0x00020000);
+  u32x4 wf[TW_RING];
+  // fragment n of this wave's stream: chunk n / 72, k16 step (n % 72) / 3, tile 3w + n % 3 (past the
+  // last chunk: the last chunk again, never consumed)
+  auto loadW = [&](u32x4& r, int c, int n72) {
+    const int cc = c < p.NC ? c : p.NC - 1;
+    r = __builtin_amdgcn_raw_buffer_load_b128(wrb, lane16, (cc * TW_FPRE + (n72 / 3) * NT + 3 * wave + n72 % 3) * TW_FRAG, 0);
+  };
+#pragma unroll
+  for (int n = 0; n < TW_AH; ++n) loadW(wf[n], 0, n);
+  float* bs = reinterpret_cast<float*>(smem + TW_H);
+  for (int i = threadIdx.x; i < p.NC * D; i += 256) bs[i] = p.bias[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the x image (LDS-DMA) landed
+  tw_barrier();
+  auto rdB = [&](int blk) -> u32x4 { return *reinterpret_cast<const u32x4*>(smem + TW_X + blk * TW_FRAG + lane16); };
+  const long o_bytes = ((long)p.M - row0) * p.NC * D * 2;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.out + row0 * p.NC * D), (short)0, (int)(o_bytes < 0x7fffffffL ? o_bytes : 0x7fffffffL), 0x00020000);
+  f32x16 acc[3][4];
+  u32x4 bq[2][4];
+#pragma unroll 1
+  for (int c = 0; c < p.NC; ++c) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bq[0][g] = rdB(g);
+    tw_unroll([&](auto sc) {
+      constexpr int s = decltype(sc)::value, n0 = 3 * s;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          if constexpr (s == 0) tw_mfma0<true, false>(acc[t][g], wf[(n0 + t) % TW_RING], bq[s & 1][g]);
+          else tw_mfma<true, false>(acc[t][g], wf[(n0 + t) % TW_RING], bq[s & 1][g]);
+        }
+        if constexpr (s + 1 < KS) bq[(s + 1) & 1][g] = rdB((s + 1) * 4 + g);
+        if (g == 1) {
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            constexpr int dummy = 0;
+            const int m = n0 + TW_AH + t;              // within [0, 72 + 9): this chunk or the next
+            if (m < 72) loadW(wf[(n0 + TW_AH + t) % TW_RING], c, m);
+            else loadW(wf[(n0 + TW_AH + t) % TW_RING], c + 1, m - 72);
+            (void)dummy;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }, std::make_integer_sequence<int, KS>{});
+    tw_drain_o(acc);
+    // + bias -> bf16 -> out[row][c D + 32 T + 16 hh .. + 15]
+    const int l = tw_lane();
+    const uint32_t bb = lds0 + TW_H + 4 * (c * D + 16 * (l >> 5));
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int T = 3 * wave + t;
+      float bv[16];
+      tw_ld16(bb + 4 * 32 * T, bv);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ro = ((32 * g + (l & 31)) * p.NC * D + c * D + 32 * T + 16 * (l >> 5)) * 2;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          float y[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = acc[t][g][8 * h2 + j] + bv[8 * h2 + j];
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{tw_pack2(y[0], y[1]), tw_pack2(y[2], y[3]), tw_pack2(y[4], y[5]),
+                                                       tw_pack2(y[6], y[7])},
+                                                 ors, ro + 16 * h2, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+int projw_launch(int M, int NC, const void* x, const void* ws, const float* bias, void* out, int desync, hipStream_t s) {
+  PwArgs a{M, NC, (const bf16*)x, (const char*)ws, bias, (bf16*)out, desync};
+  SNV_HIP(hipFuncSetAttribute((const void*)projw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS));
+  hipLaunchKernelGGL(projw_kernel, dim3((unsigned)cdiv(M, 128)), dim3(256), TW_LDS, s, a);
+  SNV_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace snvrag

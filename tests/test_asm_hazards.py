@@ -102,14 +102,14 @@ def test_wide_tail_no_read_before_load_lands(tmp_path):
     subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
                     os.path.join(CSRC, "tailw.hip"), "-o", str(out)], check=True, capture_output=True)
     text = out.read_text().split("\n")
-    name = "_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:"
-    i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
-    i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
-    ins = [ln.strip() for ln in text[i0:i1]]
-    ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
-    assert sum(t.startswith("v_mfma") for t in ins) > 1000
-    bad = _pending_reads(ins)
-    assert not bad, bad[:5]
+    for name in ("_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:", "_ZN6snvrag12projw_kernelENS_6PwArgsE:"):
+        i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
+        i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
+        ins = [ln.strip() for ln in text[i0:i1]]
+        ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
+        assert sum(t.startswith("v_mfma") for t in ins) > 250
+        bad = _pending_reads(ins)
+        assert not bad, (name, bad[:5])
 
 
 def _valu_to_mfma(ins):
@@ -144,7 +144,8 @@ def test_wide_tail_no_valu_write_before_mfma_operand(tmp_path):
     subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
                     os.path.join(CSRC, "tailw.hip"), "-o", str(out)], check=True, capture_output=True)
     text = out.read_text().split("\n")
-    for name in ("_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:", "_ZN6snvrag12tailw_kernelILi1EEEvNS_6TwArgsE:"):
+    for name in ("_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:", "_ZN6snvrag12tailw_kernelILi1EEEvNS_6TwArgsE:",
+                 "_ZN6snvrag12projw_kernelENS_6PwArgsE:"):
         i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
         i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
         ins = [ln.strip() for ln in text[i0:i1]]

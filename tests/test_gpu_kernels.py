@@ -558,17 +558,21 @@ def test_raw_genotype_index_vs_oracle(n, bits, k, nq):
         assert (I[:, n:] == -1).all() and np.isinf(D[:, n:]).all()
 
 
-@pytest.mark.parametrize("D,M,NC", [(384, 777, 3), (384, 128 * 4, 3), (128, 300, 3), (256, 1, 1), (384, 64 * 1030 + 3, 3)])
-def test_proj_kernel_vs_fp64(D, M, NC):
-    """Projection on the 32x32 stream kernel (csrc/tail.hip PROJ mode, the engine's QKV path;
-    multi_head_attention.py:44-46): x W^T + b vs float64 torch on the same bf16 operands,
+@pytest.mark.parametrize("wide", [1, 0])
+@pytest.mark.parametrize("D,M,NC", [(384, 777, 3), (384, 128 * 4, 3), (128, 300, 3), (256, 1, 1), (384, 64 * 1030 + 3, 3),
+                                    (384, 1, 1)])
+def test_proj_kernel_vs_fp64(D, M, NC, wide):
+    """Projection (multi_head_attention.py:44-46) on the wide-row kernel (csrc/tailw.hip projw_kernel,
+    option proj_wide = 1: the engine's QKV path at D = 384) and on the 32x32 stream kernel (csrc/tail.hip
+    PROJ mode, proj_wide = 0; D 128 / 256 always): x W^T + b vs float64 torch on the same bf16 operands,
     ragged M (rows >= M are dropped by the bounds-checked stores), every chunk rotation."""
     g = torch.Generator(device="cpu").manual_seed(D + M + NC)
     x = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
     w = (torch.randn(NC * D, D, generator=g) / math.sqrt(D)).to(DEV, torch.bfloat16)
     b = torch.randn(NC * D, generator=g).to(DEV)
     out = torch.full((M + 1, NC * D), 7.0, device=DEV, dtype=torch.bfloat16)
-    K().proj_forward(x, K().proj_pack(w), b, NC, out=out[:M])
+    with K().option("proj_wide", wide):
+        K().proj_forward(x, K().proj_pack(w), b, NC, out=out[:M])
     ref = x.double() @ w.double().T + b.double()
     torch.testing.assert_close(out[:M].double(), ref, rtol=2e-2, atol=2e-2)
     assert (out[M] == 7.0).all()                       # nothing written past the last row

@@ -53,6 +53,24 @@ def env(k, v):
     K.set_option(name, -1 if v is None and name.endswith("desync") else int(v or 0))
 
 
+def proj_opt(wide):
+    def fn():
+        K.set_option("proj_wide", wide)
+        K.proj_forward(x, ws, b, 3, out=out)
+    return fn
+
+
+K.set_option("proj_wide", 0)
+o0 = K.proj_forward(x, ws, b, 3, out=out).clone()
+K.set_option("proj_wide", 1)
+o1w = K.proj_forward(x, ws, b, 3, out=out).clone()
+print(f"wide proj vs tail.hip proj: max|diff| {(o1w.float() - o0.float()).abs().max().item():.4f}, "
+      f"bitwise equal {torch.equal(o1w, o0)}", flush=True)
+for it in range(3):
+    for name, fn in (("proj wide (tailw.hip)", proj_opt(1)), ("sgemm", lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out))):
+        ms = timeit(fn)
+        print(f"{name:24s} {ms:.4f} ms  {fl / ms / 1e9:.0f} TFLOP/s", flush=True)
+K.set_option("proj_wide", 0)
 for name, fn, e, f in (("proj (tail.hip)", lambda: K.proj_forward(x, ws, b, 3, out=out), None, fl),
                        ("sgemm", lambda: K.sgemm(x, sgw, 3 * D, sgv, out=out), None, fl),
                        ("gelu 4D", lambda: K.sgemm(x, sg4, 4 * D, sv4, act=1, out=out4), None, fl * 4 / 3)):
