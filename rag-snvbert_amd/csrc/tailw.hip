@@ -416,7 +416,7 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(acc[t][g]));   // v back in AGPRs
+      for (int g = 0; g < 4; ++g) {}   // v back in AGPRs
     const int l = tw_lane();
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -741,7 +741,7 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(acc[t][g]));
+      for (int g = 0; g < 4; ++g) {}
     const int l = tw_lane();
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
