@@ -637,6 +637,17 @@ void tailw_kernel(TwArgs p) {
   // the epilogue of half-round 11, then its FFN2
   tw_unroll([&](auto kc) { epi_unit(kc, std::integral_constant<int, 1>{}); }, std::make_integer_sequence<int, 8>{});
   tw_barrier();
+  // H half 0 is free from here (its last reader, FFN2(10), is behind this barrier): the LN epilogue's
+  // tables [b2' | c1 | g2 | be2] (6 KiB) arrive there by LDS-DMA during FFN2(11) (retired by the
+  // vmcnt(0) after it, visible after the epilogue's first barrier)
+  {
+    const i32x4 vrs = dma_rsrc(p.vec + 4 * D, 4L * D * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = wave + 4 * j;
+      if (pc < 6) dma_x4(vrs, lds0 + TW_H + pc * TW_FRAG, lane16, pc * TW_FRAG);
+    }
+  }
   seg2(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QF>{}, std::false_type{},
        std::true_type{}, std::true_type{});
   float st1[4], st2[4];
@@ -651,8 +662,7 @@ void tailw_kernel(TwArgs p) {
   // ---- epilogue: out = LN2(x1 + lrelu(rstd_f (acc - mean_f c1) + b2'))
   float2* s2 = reinterpret_cast<float2*>(smem + TW_H + 8 * 1024);
   float2* s3 = reinterpret_cast<float2*>(smem + TW_H + 12 * 1024);
-  float* et = reinterpret_cast<float*>(smem + TW_H);  // [b2' | c1 | g2 | be2]
-  asm volatile("s_barrier" ::: "memory");             // every wave done reading H
+  // (H half 0 holds the tables, DMA'd during FFN2(11), and the statistics; FFN2(11) reads half 1)
   {
     const int l = tw_lane();
 #pragma unroll
@@ -661,7 +671,6 @@ void tailw_kernel(TwArgs p) {
       st2[g] = tw_xsum32(st2[g]);
       s2[wave * 128 + 32 * g + (l & 31)] = make_float2(st1[g], st2[g]);
     }
-    for (int i = threadIdx.x; i < 4 * D; i += 256) et[i] = p.vec[4 * D + i];
   }
   tw_barrier();
   float hm[4], hr[4];
