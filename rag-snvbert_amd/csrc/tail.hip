@@ -1192,7 +1192,9 @@ static int launch_tail(TailArgs a, hipStream_t s) {
     if (var == 0 && options().tail_wide) {
       const long nwg = cdiv(a.M, TL_ROWS);
       const int64_t dz = options().tail_desync;
-      const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 25000) : 0;
+      // (first-round stagger 10 k cycles: tools/tailw_desync.py, two boxes: 1.409 / 1.403 ms vs
+      // 1.454 / 1.399 at tail_kernel's 25 k and 1.444 without)
+      const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 10000) : 0;
       return tailw_launch(a.M, a.act, a.resid, a.out, a.ws, a.vec, a.b_o, a.g1, a.be1, a.eps, desync,
                           (int)options().tail_wide == 2 ? 1 : 0, s);
     }
