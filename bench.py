@@ -296,9 +296,12 @@ def main():
            "2*M*D*9D = 18*M*D^2 per launch"),
           ("attn32_dma (attention)", attn, "4*L^2*dh*H*nseq per launch")]
     name, dom, per = max((m for m in mf if m[1]), key=lambda m: m[1]["total_ms_per_step"])
+    tr = pmc_traffic(name)
     roofline = dict(bound="mfma", kernel=name,
                     achieved=round(dom["rate"] / 1e12, 2), peak=peak_f, unit="TFLOP/s",
-                    frac=round(dom["rate"] / 1e12 / peak_f, 4), traffic=pmc_traffic(name),
+                    frac=round(dom["rate"] / 1e12 / peak_f, 4),
+                    traffic=tr["bytes_per_launch"] if tr else None, traffic_unit="HBM bytes per launch",
+                    traffic_detail=tr,
                     avg_launch_ms=round(dom["avg_ms"], 4),
                     algorithmic_per_launch=f"{dom['work_per_launch']:.4g} FLOP ({per})")
     extra = {
