@@ -9,8 +9,11 @@ Metric (BASELINE.json): masked SNVs imputed/s (2 * sum(mask) per sample-window),
 with kNN queries/s reported beside it.  Workload = configs[2] of BASELINE.json:
 window 1024 sites, k = 32, 1M-haplotype panel resident in HBM, d384/L12/H12.
 
-Launch: python bench.py --gpus 1 --steps K --warmup W   (N>1: torch.distributed.run,
-one rank per GPU; each rank imputes its own B samples -> weak scaling).  With N>1 the
+Launch: python bench.py --gpus N --steps K --warmup W.  N>1 runs one rank per GPU: under
+torch.distributed.run (WORLD_SIZE set) this process is one rank and checks WORLD_SIZE == N;
+started directly, it first checks that N devices are visible (exit 2 otherwise) and then
+starts ``torch.distributed.run --nproc-per-node N`` on itself as a child process before any
+GPU call, exiting with the child's status.  Each rank imputes its own B samples -> weak scaling.  With N>1 the
 default ``--panel sharded`` gives every rank a contiguous 1/N of the panel: the search
 all-gathers the ranks' query tokens, scans the local shard, all-gathers and merges the
 partial top-k keys and all-reduces the neighbours' alt-allele counts over RCCL
@@ -39,9 +42,10 @@ BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (no sparsity)
 F32_PEAK_TFLOPS = 157.3
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks = GPUs (default: WORLD_SIZE under a launcher, else 1)")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=256,
@@ -67,24 +71,91 @@ def parse():
     p.add_argument("--train-steps", type=int, default=3,
                    help="timed DDP training steps at configs[1] (B=24/GPU, window 512, k=8, 10k-haplotype panel); 0 = skip")
     p.add_argument("--train-window", type=int, default=512, help="configs[1] window (sites) of the training leg")
-    return p.parse_args()
+    p.add_argument("--one-device-rehearsal", action="store_true",
+                   help="N>1 rehearsal on a one-GPU box: every rank on cuda:0 over gloo (host-staged "
+                        "collectives); the numbers are not a measurement")
+    return p.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(args, argv, port):
+    """The torch.distributed.run command that starts ``args.gpus`` ranks of this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+
+
+def check_devices(n_ranks: int, n_devices: int, rehearsal: bool) -> None:
+    """Exit (status 2, message on stderr) instead of measuring fewer GPUs than asked for."""
+    if not rehearsal and n_devices < n_ranks:
+        sys.stderr.write(f"bench.py: --gpus {n_ranks} needs {n_ranks} visible GPUs, found {n_devices}; "
+                         "not measuring (no n_gpus line is printed)\n")
+        sys.exit(2)
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 without a launcher: start N ranks (one per GPU) as a CHILD process — this
+    process has not touched the GPU (torch.cuda.device_count() does not initialise it) and
+    does not exec; its exit status is the launcher's."""
+    import subprocess
+    check_devices(args.gpus, torch.cuda.device_count(), args.one_device_rehearsal)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(launch_command(args, argv, _free_port()), env=env)
 
 
 def setup_dist(args):
+    """This rank's (world, rank, local device).  The world must be the --gpus asked for, and
+    every rank needs its own visible GPU (RCCL: one process per GPU); the rehearsal puts every
+    rank on cuda:0 over gloo."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if args.gpus is not None and args.gpus != world:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks\n")
+        sys.exit(2)
+    args.gpus = world
+    check_devices(world, torch.cuda.device_count(), args.one_device_rehearsal)
+    dev_i = 0 if args.one_device_rehearsal else local
+    torch.cuda.set_device(dev_i)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    return world, rank, local
+        if args.one_device_rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_i}"))
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    return world, rank, dev_i
 
 
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def dist_info(world):
+    """The collective backend this run measured on (the bench line's ``distributed``)."""
+    if world <= 1:
+        return {"backend": None, "world_size": 1}
+    import torch.distributed as dist
+    be = dist.get_backend()
+    return {"backend": "rccl" if be == "nccl" else be, "world_size": dist.get_world_size(),
+            "rehearsal_one_device": be == "gloo"}
+
+
+def max_over_ranks(v: float, world: int, dev) -> float:
+    """MAX of a host float over the ranks (gloo: through a host tensor)."""
+    if world <= 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device=dev if dist.get_backend() != "gloo" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def make_queries(args, af_np, seed, rank):
@@ -172,8 +243,11 @@ def make_step(wl, eng, k):
     return step
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
     from src import native as N
@@ -260,11 +334,7 @@ def main():
     # precision leg: the same batch through the exact-f32 path, whose logits
     # carry the 1e-3 parity bar; report how often the bf16 run's imputed calls agree with it
     precision = precision_leg(args, wl, eng, k, out) if (args.f32_leg and dtype == torch.bfloat16) else None
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world, dev)
 
     def agg(kind):
         sel = kinds == kind
@@ -288,6 +358,9 @@ def main():
     torch.cuda.empty_cache()
     train = train_bench(args, world, rank, dev) if args.train_steps > 0 else None
     if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
         return
     peak_f = BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else F32_PEAK_TFLOPS
     # roofline object = the MFMA kernel class with the most time per step
@@ -333,7 +406,7 @@ def main():
     }
     from src.dataset import utils as U
     cpu = None
-    if args.cpu_baseline:
+    if args.cpu_baseline and world == 1:             # rank 0 at N = 1 only (the other ranks would idle)
         cpu = cpu_baseline(args, model, vocab, af_np, ref_af, raw_mask, x, dev)
     line = {
         "metric": "masked SNVs imputed/sec (+ kNN queries/sec), window=1024 k=32",
@@ -347,8 +420,12 @@ def main():
                    "global_batch": B * world, "seq_len": L, "parallelism": (f"dp{world} + panel sharded {world}-way" if shard is not None
                                                   else f"dp{world} (panel replicated)")},
         "roofline": roofline, "cpu_baseline": cpu, **extra, "precision_parity": precision, "train": train,
+        "distributed": dist_info(world),
     }
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def call_agreement(o_lo, o_hi, raw_mask):
@@ -429,21 +506,35 @@ def train_bench(args, world, rank, dev):
     sites (configs[1]; the encoder still runs L = 1030 tokens), k=8 neighbours from a
     10k-haplotype panel, d384/L12/H12, bf16 + f32 master weights.
     One step = retrieval + forward + focal losses + backward + bucketed all-reduce (RCCL when
-    world > 1) + clipped fused Adam.  Timed like the main metric (barrier + sync around)."""
+    world > 1) + clipped fused Adam.  Timed like the main metric (barrier + sync around).
+    With world > 1 every rank builds the SAME panel and global batch and trains on its own 24
+    samples; ``--panel sharded`` (configs[3]) gives each rank a contiguous 1/world of the panel
+    and the retrieval runs the collective search (src/retrieval/shards.py)."""
     from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
     from src.dataset.synthetic import make_rag_dataset
     from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from src.model import build_model
     Bt, S, nref = 24, args.train_window, 5000
-    ds, vocab = make_rag_dataset(n_samples=Bt, n_sites=S, n_windows=1, n_ref_samples=nref, seed=7 + rank,
+    ds, vocab = make_rag_dataset(n_samples=Bt * world, n_sites=S, n_windows=1, n_ref_samples=nref, seed=7,
                                  name="train")
-    batch = embedding_rag_collate_fn([ds[i] for i in range(Bt)])
+    shard = None
+    if world > 1 and args.panel == "sharded":
+        from src.retrieval.shards import PanelShard
+        shard = PanelShard.current()
+        ds.set_panel_shard(shard)
+    batch = embedding_rag_collate_fn([ds[i] for i in range(rank * Bt, (rank + 1) * Bt)])
     torch.manual_seed(0)
     model = build_model(len(vocab), args.dims, args.layers, args.heads).to(dev)
     if world > 1:
         import torch.distributed as dist
+        gloo = dist.get_backend() == "gloo"
         for t in list(model.parameters()) + list(model.buffers()):
-            dist.broadcast(t.data, 0)
+            if gloo:
+                h = t.data.cpu()
+                dist.broadcast(h, 0)
+                t.data.copy_(h)
+            else:
+                dist.broadcast(t.data, 0)
     tr = BERTTrainerWithValidationOptimized(model, None, None, vocab, lr=7.5e-5, warmup_steps=100,
                                             grad_accum_steps=1, log_freq=0)
     tr.rag_train_dataset = ds
@@ -459,12 +550,7 @@ def train_bench(args, world, rank, dev):
         loss = tr.train_step(dict(batch))
     torch.cuda.synchronize()
     barrier(world)
-    el = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([el], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
     masked = 2 * int(batch["mask"].sum())
     ms = el / args.train_steps * 1e3
     tflops = fl.flops / (ms * 1e-3) / 1e12
@@ -473,6 +559,7 @@ def train_bench(args, world, rank, dev):
             "frac_bf16_peak": round(tflops / BF16_PEAK_TFLOPS, 4), "flop_count": fl.RULE,
             "masked_snvs_per_s": round(masked * world * args.train_steps / el, 1),
             "batch_per_gpu": Bt, "window_sites": S, "k": 8, "panel_haplotypes": 2 * nref,
+            "panel": (f"sharded {world}-way" if shard is not None else "replicated"),
             "n_gpus": world, "loss": round(float(loss), 3),
             "note": "DDP: bucketed async all-reduce of the flat f32 gradient buffer over RCCL; "
                     "reference banner: 115 ms/batch at B=24 on an unstated GPU (BASELINE.md)"}

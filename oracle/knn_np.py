@@ -25,6 +25,10 @@ golden tests check that tie-equivalence on the reference's own outputs.
 
 from __future__ import annotations
 
+import ctypes
+import subprocess
+from pathlib import Path
+
 import numpy as np
 
 TOK0, TOK1, MASK_TOK = 5, 6, 4
@@ -48,16 +52,64 @@ def lut_delta(W, tok_q, dA, site_mask, tok0=TOK0, tok1=TOK1):
     return delta
 
 
+_LIB = None
+
+
+def _oracle_lib():
+    """oracle/build/liboracle.so (oracle/lut_f32.c), built on first use if absent."""
+    global _LIB
+    if _LIB is None:
+        here = Path(__file__).resolve().parent
+        so = here / "build" / "liboracle.so"
+        if not so.exists() or so.stat().st_mtime < (here / "lut_f32.c").stat().st_mtime:
+            subprocess.run(["make", "-s", "-C", str(here)], check=True)
+        lib = ctypes.CDLL(str(so))
+        lib.oracle_lut_delta_f32.restype = ctypes.c_int
+        lib.oracle_lut_delta_f32.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_void_p] * 4 + [ctypes.c_int64] + \
+            [ctypes.c_void_p] * 2 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        _LIB = lib
+    return _LIB
+
+
+def lut_delta_f32(W, tok_q, site_mask, Aq=None, aq_period=0, Ar=None, Wp=None, tok0=TOK0, tok1=TOK1):
+    """Delta_q[s] (f32 [Bq, S]) in the DEVICE's f32 arithmetic and order (oracle/lut_f32.c restates
+    csrc/knn.hip lut_kernel / lut_delta_kernel), the input of the canonical quantised order.
+
+    W [V, D] query-side token table, Wp the panel side's (default W: snvrag_knn_lut_panel);
+    Aq [P, L, D] query AF-embedding offsets (row q uses Aq[q % aq_period] when aq_period > 0),
+    Ar [L, D] the panel's; either may be None (the device then takes the no-offset path)."""
+    c = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)
+    W = c(W, np.float32)
+    Wp = W if Wp is None else c(Wp, np.float32)
+    tok = c(tok_q, np.int64)
+    Aq, Ar = c(Aq, np.float32), c(Ar, np.float32)
+    sm = c(site_mask, np.uint8)
+    nq, L = tok.shape
+    S = sm.shape[0]
+    out = np.zeros((nq, S), np.float32)
+    ptr = lambda a: None if a is None else a.ctypes.data
+    rc = _oracle_lib().oracle_lut_delta_f32(nq, L, W.shape[1], ptr(tok), ptr(W), ptr(Wp), ptr(Aq), int(aq_period),
+                                            ptr(Ar), ptr(sm), S, tok0, tok1, ptr(out))
+    if rc:
+        raise ValueError("lut_delta_f32: D must be a multiple of 4 and the window must fit L")
+    return out
+
+
 def quantize_lut(delta, limbs=2):
     """Per-query power-of-two scale and rint quantisation (mirrors knn.hip ``lut_kernel``).
 
+    The exponent is the largest e with max|Delta| * 2^e <= 2**(7*limbs) - 1 (exact
+    power-of-two comparisons; the device takes floor(log2(qmax / m)) and corrects it down).
     Returns (Dq int32 [Bq, S], exp2 int32 [Bq]).  |Dq| <= 2**(7*limbs) - 1.
     """
     qmax = float((1 << (7 * limbs)) - 1)
-    m = np.abs(delta).max(-1)
+    m = np.abs(np.asarray(delta, np.float64)).max(-1)
     e = np.where(m > 0, np.floor(np.log2(qmax / np.where(m > 0, m, 1.0))), 0).astype(np.int32)
-    # guard rounding of log2: make sure m * 2^e <= qmax
-    e = np.where(m * np.exp2(e) > qmax, e - 1, e).astype(np.int32)
+    pos = m > 0
+    for _ in range(2):                     # exact: m * 2^e <= qmax < m * 2^(e+1)
+        e = np.where(pos & (m * np.exp2(e + 1.0) <= qmax), e + 1, e)
+        e = np.where(pos & (m * np.exp2(e * 1.0) > qmax), e - 1, e)
+    e = e.astype(np.int32)
     dq = np.rint(delta * np.exp2(e)[:, None]).astype(np.int64)
     return np.clip(dq, -qmax, qmax).astype(np.int32), e
 

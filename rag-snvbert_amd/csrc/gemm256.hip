@@ -576,7 +576,9 @@ extern "C" int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, in
   SNV_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wpacked % 16) == 0 &&
                     ((uintptr_t)resid % 16) == 0,
                 "16-byte aligned operands");
-  SNV_CHECK_ARG(257L * lda * 2 < (1L << 31) && 257L * ldo * 2 < (1L << 31), "row offsets must fit 31 bits");
+  SNV_CHECK_ARG(257L * lda * 2 < (1L << 31) && 257L * ldo * 2 < (1L << 31) &&
+                    (!resid || 257L * ld_resid * 2 < (1L << 31)),
+                "row offsets must fit 31 bits");
   if (M == 0) return 0;
   const G2Args a{(int)M, K, (const bf16*)A, (long)lda, (const char*)wpacked, bias, (const bf16*)resid,
                  (long)ld_resid, (bf16*)out, (long)ldo, nullptr};

@@ -31,7 +31,8 @@ namespace snvrag {
 constexpr int TL_FRAG = 1024;               // one A fragment: 32 rows x 16 k bf16
 constexpr int TL_SLAB = 16 * TL_FRAG;
 constexpr int TL_NSLOT = 9;                 // ring slots (144 KiB)
-constexpr int TL_PF_DEFAULT = 4;            // A fragments read ahead (r3: 4: 1.634 ms, 8: 1.659; r5: 8 faster, launch_tail)
+constexpr int TL_PF4 = 4;                   // A fragments read ahead: the template default and tail_variant 1
+constexpr int TL_PF_DEFAULT = 8;             // launch_tail's default (r3: 4: 1.634 ms, 8: 1.659 spilling; r5: 8 faster)
 constexpr int TL_ROWS = 128;
 constexpr int TL_VEC_LDS = 11 * 1024;       // b1 [4D] + g1, be1, b_o [D] (f32, D <= 384)
 
@@ -154,7 +155,7 @@ enum { TS_REAL0 = 0, TS_START, TS_PROLOGUE, TS_PROJ, TS_LN1, TS_FFN, TS_EPI, TS_
 // (stamps), 5 = VAR 3.
 // NC > 0: projection mode (snvrag_proj_forward): out[M, NC*D] = act W^T + b over NC output
 // chunks of D features (the QKV projection: NC = 3), the same stream / ring / read machinery.
-template <int D, bool PRE, int TL_PF = TL_PF_DEFAULT, int VAR = 0, bool TL_SGB = true, int NC = 0>
+template <int D, bool PRE, int TL_PF = TL_PF4, int VAR = 0, bool TL_SGB = true, int NC = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void tail_kernel(TailArgs p) {
   using S = TailShape<D>;
@@ -811,7 +812,7 @@ void tailp_kernel(TailArgs p) {
     rd_slot = rd_slot >= RING ? rd_slot - RING : rd_slot;
   };
 
-  constexpr int PF = TL_PF_DEFAULT;
+  constexpr int PF = TL_PF4;
   u32x4 a[PF];
   // consume a part of NF fragments (whole slabs) starting at tile slab G0 (compile-time), or, with
   // G0 < 0, the loop part at block offset P of the iteration whose issue base is mloop
@@ -1141,7 +1142,7 @@ __global__ void proj_pack_kernel(int D, long n_pieces, const bf16* __restrict__ 
 
 template <int D, int NC>
 static int launch_proj(const TailArgs& a, hipStream_t s) {
-  auto kern = tail_kernel<D, false, TL_PF_DEFAULT, 0, true, NC>;
+  auto kern = tail_kernel<D, false, TL_PF4, 0, true, NC>;
   constexpr size_t lds = (size_t)TL_NSLOT * TL_SLAB + NC * D * 4;
   static_assert(NC * D * 4 <= TL_VEC_LDS && lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1204,11 +1205,11 @@ static int launch_tail(TailArgs a, hipStream_t s) {
     if ((var == 0 || var == 7) && options().tail_persist && (long)a.M * D * 2 < 0x7fffffffL) return launch_tailp<D>(a, s);
   // default: 8 fragments read ahead (r5: 1.530 vs 1.553 ms at PF 4, mean of 5 sessions of
   // tools/tail_micro.py at M = 527 360; variant 1 = PF 4, the r4 default)
-  auto kern = var == 1 ? tail_kernel<D, PRE, TL_PF_DEFAULT> : var == 2 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 1>
-              : var == 3 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 0, false>
-              : var == 5 ? tail_kernel<D, PRE, TL_PF_DEFAULT, 3> : tail_kernel<D, PRE, 8>;
+  auto kern = var == 1 ? tail_kernel<D, PRE, TL_PF4> : var == 2 ? tail_kernel<D, PRE, TL_PF4, 1>
+              : var == 3 ? tail_kernel<D, PRE, TL_PF4, 0, false>
+              : var == 5 ? tail_kernel<D, PRE, TL_PF4, 3> : tail_kernel<D, PRE, TL_PF_DEFAULT>;
   if (var == 4 && D == 384 && g_tail_stamps) {           // phase stamps (tools/tail_micro.py)
-    kern = tail_kernel<D, PRE, TL_PF_DEFAULT, 2>;
+    kern = tail_kernel<D, PRE, TL_PF4, 2>;
     a.stamps = g_tail_stamps;
   }
   // first-round phase step: only when every CU runs several rounds (the delay is paid once).

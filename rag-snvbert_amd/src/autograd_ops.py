@@ -97,7 +97,14 @@ def clear_weight_cache() -> None:
 
 def weights_updated() -> None:
     """Called after a parameter update done outside torch's version tracking (HIP kernels):
-    every derived weight tensor is refreshed from the new master weights in one launch."""
+    every derived weight tensor is refreshed from the new master weights in one launch.
+
+    Every call also counts as a weight change for the train-mode retrieval's panel snapshot
+    (``embedding_rag_dataset._weights_token``): after it the window's stale-snapshot search takes
+    the exact LUT form even if the values did not change (an lr = 0 step, ``sync_mirror``) — the
+    same neighbours, a slower LUT.  On a sharded panel that decision selects collectives
+    (``any_rank``), so every rank must make the same calls in the same order: the trainer calls it
+    once per optimizer step and once per ``load`` / ``sync_mirror``, on every rank alike."""
     _EPOCH[0] += 1
     _BF16.clear()
     _refresh_derived()
@@ -522,7 +529,9 @@ class _HipLinear(torch.autograd.Function):
                 else:
                     r2 = res.reshape(-1, n_in).to(torch.bfloat16)
                     if r2.stride(1) != 1 or r2.stride(0) % 8 or r2.data_ptr() % 16:
-                        r2 = r2.contiguous()
+                        # a fresh, 16-byte aligned copy (contiguous() returns a contiguous but
+                        # misaligned view unchanged, which the C side would reject)
+                        r2 = r2.clone(memory_format=torch.contiguous_format)
                     gx = K.gemm256(g2, wsp, n_in, resid=r2)
             elif _BLAS_LARGE_K[0] and g2.shape[1] >= 1024 and n_in == 384:
                 # A/B: hipBLASLt, the handed-off gradient as addmm's C operand

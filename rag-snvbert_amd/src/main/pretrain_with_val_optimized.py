@@ -332,12 +332,18 @@ class BERTTrainerWithValidationOptimized:
         weights and the optimizer / schedule / early-stopping / sampler state; the reference's
         formats (a pickled BERTFoundationModel, a state_dict or {'state_dict': ...}, optional
         ``module.`` prefixes) restore the weights, read by ``model.checkpoint`` without
-        executing any pickled class."""
+        executing any pickled class.
+
+        Returns the checkpoint's epoch; ``self.loaded_own_checkpoint`` says whether the file was
+        this trainer's own (``save``: weights + optimizer state + epoch) — a reference-format file
+        carries no epoch the resume may trust (the reference starts at --resume_epoch whatever the
+        file holds, train_embedding_rag.py:155-191)."""
         from ..model.checkpoint import load_state_dict_any
         if torch.serialization.get_unsafe_globals_in_checkpoint(path):
             ck = {"model": load_state_dict_any(path)}
         else:
             ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.loaded_own_checkpoint = isinstance(ck, dict) and "model" in ck and "optim" in ck and "epoch" in ck
         sd = ck["model"] if "model" in ck else ck.get("state_dict", ck)
         sd = {k[7:] if k.startswith("module.") else k: v for k, v in sd.items()}
         self.model.load_state_dict(sd)

@@ -43,7 +43,9 @@ def parse_args(argv=None):
     p.add_argument("--cuda_devices", type=int, default=0)
     p.add_argument("--num_workers", type=int, default=0)
     p.add_argument("--resume_path", type=str, default=None)
-    p.add_argument("--resume_epoch", type=int, default=0)
+    p.add_argument("--resume_epoch", type=int, default=None,
+                   help="epoch to resume at (reference: default 0); unset = after a checkpoint of this "
+                        "trainer's own epoch, 0 for a reference-format file")
     p.add_argument("--output_path", type=str, default="output/rag_bert.model")
     p.add_argument("--log_freq", type=int, default=500)
     p.add_argument("--rare_threshold", type=float, default=0.05)
@@ -144,8 +146,12 @@ def main(argv=None):
     start = 0
     if args.resume_path:
         # train_embedding_rag.py:155-191 (weights; here also optimizer / schedule / early-stopping /
-        # sampler state); start at --resume_epoch, or after the checkpoint's epoch
-        start = trainer.load(args.resume_path) + 1 if not args.resume_epoch else args.resume_epoch
+        # sampler state).  An explicit --resume_epoch (0 included) wins, as in the reference; unset,
+        # a checkpoint of this trainer resumes after its epoch and a reference-format file (pickled
+        # module, state_dict, {'state_dict': ...}: no trustworthy epoch) at the reference's default 0
+        ep = trainer.load(args.resume_path)
+        start = args.resume_epoch if args.resume_epoch is not None else \
+            (ep + 1 if trainer.loaded_own_checkpoint else 0)
     ds, val_ds = train_loader.dataset, val_loader.dataset
     if start > 0 and hasattr(ds, "add_level"):
         # :326-336 — the curriculum level of the resumed epoch, min(start // 2, 7)

@@ -137,15 +137,16 @@ def test_knn_bit_exact_vs_oracle(n_ref, n_sites, nq, k, limbs, tie):
     smask = torch.from_numpy(site_mask).to(DEV)
     idx, dist, keys, lut, exps = idx_t.search(torch.from_numpy(tok).to(DEV), Wt, smask, k, limbs=limbs,
                                               return_keys=True)
-    # LUT vs oracle quantisation of the fp64 Delta (<= 1 quantum, identical exponents)
-    delta = knn_np.lut_delta(W, tok, None, site_mask)
-    dq_o, e_o = knn_np.quantize_lut(delta, limbs)
+    # LUT == the oracle's quantisation of Delta computed in the device's f32 arithmetic
+    # (oracle/lut_f32.c), bit for bit; within one quantum of the fp64 Delta's
+    dq_o, e_o = knn_np.quantize_lut(knn_np.lut_delta_f32(W, tok, site_mask), limbs)
     dq_g = decode_lut(lut, nq, idx_t.n_sites_pad, limbs)
     np.testing.assert_array_equal(exps.cpu().numpy(), e_o)
-    assert np.abs(dq_g[:, :n_sites] - dq_o).max() <= 1
+    np.testing.assert_array_equal(dq_g[:, :n_sites], dq_o)
+    assert np.abs(knn_np.quantize_lut(knn_np.lut_delta(W, tok, None, site_mask), limbs)[0] - dq_o).max() <= 1
     assert (dq_g[:, n_sites:] == 0).all()
-    # scan + merge bit-exact against the oracle on the SAME integer LUT
-    oi, od = knn_np.knn(panel, dq_g[:, :n_sites], k)
+    # scan + merge bit-exact against the oracle's own LUT -> top-k
+    oi, od = knn_np.knn(panel, dq_o, k)
     np.testing.assert_array_equal(idx.cpu().numpy(), oi)
     kk = keys.cpu().numpy().view(np.uint64)
     valid = oi >= 0

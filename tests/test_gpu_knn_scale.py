@@ -4,9 +4,10 @@ The bench (configs[2]) searches 512 query haplotypes against a 1,000,000-haploty
 1024-site panel: 32 query tiles -> G = 4 co-scheduled query groups sharing each panel
 range (csrc/knn.hip scan2_kernel slot/group/part mapping), the n_parts >= 256 branch of
 ``scan_parts`` and the threshold pre-pass over a 1/64 panel prefix.  Every case here
-compares the device top-k keys with the ORACLE (``oracle/knn_np.knn``, float64-exact
-(distance, index) order) run on the host copy of the same panel and the same integer LUT
-the device quantised; sampled queries cover every query group.
+compares the device top-k keys with the ORACLE run end to end on the host copy of the same
+panel: Delta in the device's f32 arithmetic (``knn_np.lut_delta_f32``, oracle/lut_f32.c) ->
+``quantize_lut`` (asserted equal to the device's LUT bit for bit) -> ``knn_np.knn``
+(float64-exact (distance, index) order); sampled queries cover every query group.
 
 Cases:
   * bench shape:   N = 1,000,000, 1024 sites, 512 queries (G = 4), aligned masks (the
@@ -43,13 +44,21 @@ def _sample_queries(nq, per_group=8, seed=0):
     return np.array(sorted(set(out)))
 
 
-def _check_sampled(index, lut, nq, limbs, keys, idx, sample, k):
-    """Device keys/indices of the sampled queries == oracle top-k on the host panel copy, using
-    the integer LUT the device itself quantised."""
-    n_sites = index.n_sites
-    codes = index.codes.cpu().numpy()[:, :n_sites]
-    dq = decode_lut(lut, nq, index.n_sites_pad, limbs)[sample, :n_sites]
-    oi, od = knn_np.knn(codes, dq, k)
+def _oracle_lut(tok, W, site_mask, exps, lut, nq, n_sites_pad, sample, limbs=2, **offsets):
+    """The oracle's LUT of the sampled queries (f32 Delta in the device's order -> quantised),
+    asserted equal to the device's LUT and exponents."""
+    n_sites = site_mask.shape[0]
+    dq_o, e_o = knn_np.quantize_lut(knn_np.lut_delta_f32(W, tok[sample], site_mask, **offsets), limbs)
+    np.testing.assert_array_equal(exps.cpu().numpy()[sample], e_o)
+    np.testing.assert_array_equal(decode_lut(lut, nq, n_sites_pad, limbs)[sample, :n_sites], dq_o)
+    return dq_o
+
+
+def _check_sampled(index, dq_o, keys, idx, sample, k):
+    """Device keys/indices of the sampled queries == the oracle's top-k (from the oracle's own
+    LUT ``dq_o``) on the host panel copy."""
+    codes = index.codes.cpu().numpy()[:, :index.n_sites]
+    oi, od = knn_np.knn(codes, dq_o, k)
     np.testing.assert_array_equal(idx.cpu().numpy()[sample], oi)
     kk = keys.cpu().numpy().view(np.uint64)[sample]
     np.testing.assert_array_equal(kk, knn_np.pack_key(od, oi))
@@ -75,7 +84,9 @@ def test_knn_bench_launch_shape_1m_512q():
     assert lut_wide_flag(lut, nq, wl.index.n_sites_pad) == 0
     sample = _sample_queries(nq)
     assert len(sample) >= 32 and len({q // 128 for q in sample}) == 4
-    oi, od = _check_sampled(wl.index, lut, nq, 2, keys, idx, sample, k)
+    dq_o = _oracle_lut(wl.tok.cpu().numpy(), P.W.cpu().numpy(), wl.raw_mask.astype(np.uint8), exps, lut, nq,
+                       wl.index.n_sites_pad, sample)
+    oi, od = _check_sampled(wl.index, dq_o, keys, idx, sample, k)
     # each query's own source haplotype (2 % flips) is among its nearest neighbours
     src = np.concatenate([wl.src[:, 0], wl.src[:, 1]])[sample]
     assert np.mean([s in row for s, row in zip(src, oi)]) > 0.9
@@ -103,15 +114,15 @@ def test_knn_ragged_600k_200q_two_limb():
     smask = torch.from_numpy(site_mask).to(DEV)
     idx, dist, keys, lut, exps = index.search(torch.from_numpy(tok).to(DEV), W, smask, k, return_keys=True)
     assert ((nq + 15) // 16 + 7) // 8 == 2 and nq % 16 == 8
-    # the device LUT equals the oracle's quantisation of the fp64 Delta (<= 1 quantum)
-    delta = knn_np.lut_delta(W.cpu().numpy(), tok, None, site_mask)
-    dq_o, e_o = knn_np.quantize_lut(delta, 2)
-    np.testing.assert_array_equal(exps.cpu().numpy(), e_o)
-    dq_g = decode_lut(lut, nq, index.n_sites_pad, 2)
-    assert np.abs(dq_g[:, :n_sites] - dq_o).max() <= 1
+    # the device LUT equals the oracle's (f32 Delta in the device's order) for EVERY query, and
+    # is within one quantum of the fp64 Delta's quantisation
+    allq = np.arange(nq)
+    dq_o = _oracle_lut(tok, W.cpu().numpy(), site_mask, exps, lut, nq, index.n_sites_pad, allq)
+    dq_64, _ = knn_np.quantize_lut(knn_np.lut_delta(W.cpu().numpy(), tok, None, site_mask), 2)
+    assert np.abs(dq_64 - dq_o).max() <= 1
     sample = _sample_queries(nq, per_group=12, seed=1)
     assert {q // 128 for q in sample} == {0, 1} and nq - 1 in sample
-    _check_sampled(index, lut, nq, 2, keys, idx, sample, k)
+    _check_sampled(index, dq_o[sample], keys, idx, sample, k)
 
 
 def test_knn_aq_ne_ar_exact_lut():
@@ -134,15 +145,15 @@ def test_knn_aq_ne_ar_exact_lut():
     T = lambda a: torch.from_numpy(a).to(DEV)
     idx, dist, keys, lut, exps = index.search(T(tok), T(W), T(site_mask), k, Aq=T(Aq), aq_period=period, Ar=T(Ar),
                                               return_keys=True)
-    dA = Aq[np.arange(nq) % period] - Ar[None]
-    delta = knn_np.lut_delta(W, tok, dA, site_mask)
-    dq_o, e_o = knn_np.quantize_lut(delta, 2)
-    np.testing.assert_array_equal(exps.cpu().numpy(), e_o)
-    dq_g = decode_lut(lut, nq, index.n_sites_pad, 2)
-    assert np.abs(dq_g[:, :n_sites] - dq_o).max() <= 1
-    assert lut_wide_flag(lut, nq, index.n_sites_pad) == 1           # real-valued Delta: two limbs
     sample = np.arange(nq)
-    _check_sampled(index, lut, nq, 2, keys, idx, sample, k)
+    # real-valued Delta: the oracle's f32 restatement of lut_delta_kernel (u = (W + A_q) - A_r)
+    # gives the device's LUT bit for bit, and its top-k the device's indices
+    dq_o = _oracle_lut(tok, W, site_mask, exps, lut, nq, index.n_sites_pad, sample, Aq=Aq, aq_period=period, Ar=Ar)
+    dA = Aq[np.arange(nq) % period] - Ar[None]
+    dq_64, _ = knn_np.quantize_lut(knn_np.lut_delta(W, tok, dA, site_mask), 2)
+    assert np.abs(dq_64 - dq_o).max() <= 1
+    assert lut_wide_flag(lut, nq, index.n_sites_pad) == 1           # real-valued Delta: two limbs
+    _check_sampled(index, dq_o, keys, idx, sample, k)
 
 
 def test_knn_quantised_lut_vs_exact_fp64_l2_reorder_bound():

@@ -153,3 +153,91 @@ def test_sharded_retrieval_two_ranks_matches_single_process():
         np.testing.assert_array_equal(got[r]["bench_idx"], idx.cpu().numpy())
         codes = wl.index.codes.cpu().numpy()
         np.testing.assert_array_equal(got[r]["bench_counts"], codes[idx.cpu().numpy()].sum(1))
+
+
+# ------------------------------------------------------------------ 8 ranks on the one GPU
+W8_ITEMS = [[0, 1, 2], [5], [3, 9, 11, 4], [15], [7, 8], [10], [6, 12, 13], [14]]   # ragged, both windows
+
+
+def _batches8(ds, rank):
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    return embedding_rag_collate_fn([ds[i] for i in W8_ITEMS[rank]])
+
+
+def _reference_run8():
+    from src.dataset.synthetic import make_rag_dataset
+    from src.engine import engine_for
+    from src.model import build_model
+    torch.manual_seed(0)
+    np.random.seed(0)
+    ds, vocab = make_rag_dataset(n_samples=16, n_sites=200, n_windows=2, n_ref_samples=45, seed=4)
+    m = build_model(len(vocab), 64, 1, 4).to(DEV).eval()
+    engine_for(m).set_dtype(torch.float32)
+    return ds, m
+
+
+def _rank_worker8(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        root = os.path.join(os.path.dirname(__file__), "..")
+        sys.path[:0] = [root, os.path.join(root, "rag-snvbert_amd")]
+        from src.retrieval.shards import PanelShard
+        from src.engine import engine_for
+        ds, m = _reference_run8()
+        ds.set_panel_shard(PanelShard.current())
+        b = ds.process_batch_retrieval(_batches8(ds, rank), m.bert.embedding, DEV, k_retrieve=5)
+        res = dict(idx1=b["rag_idx_h1"].cpu().numpy(), idx2=b["rag_idx_h2"].cpu().numpy(),
+                   mean=b["rag_mean"].float().cpu().numpy())
+        import bench
+        from src.dataset.vocab import WordVocab
+        from src.dataset import synthetic
+        args = SimpleNamespace(batch=1 + rank % 3, n_ref=2500, window=192, level=4)
+        wl = bench.build_workload(args, torch.device(DEV), WordVocab(synthetic.POPS), rank,
+                                  shard=PanelShard.current())
+        idx, counts = bench.make_search(wl, engine_for(m), 8)()
+        res.update(bench_idx=idx.cpu().numpy(), bench_counts=counts.cpu().numpy())
+        q.put((rank, res))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_sharded_retrieval_eight_ranks_one_gpu_matches_single_process():
+    """configs[3]'s 8-way panel shard at tiny size: 8 gloo ranks on the one GPU run the HIP
+    shard kernels (local scan with global indices, 8-list topk_merge, neighbour counts
+    all-reduce) under the product path — ragged batches over two windows — and every rank's
+    neighbours and means equal one process on the whole panel."""
+    import bench
+    from src.dataset.vocab import WordVocab
+    from src.dataset import synthetic
+    from src.engine import engine_for
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_worker8, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=380) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert isinstance(got[r], dict), got[r]
+    ds, m = _reference_run8()
+    for r in range(world):
+        b = ds.process_batch_retrieval(_batches8(ds, r), m.bert.embedding, DEV, k_retrieve=5)
+        np.testing.assert_array_equal(got[r]["idx1"], b["rag_idx_h1"].cpu().numpy())
+        np.testing.assert_array_equal(got[r]["idx2"], b["rag_idx_h2"].cpu().numpy())
+        np.testing.assert_array_equal(got[r]["mean"], b["rag_mean"].float().cpu().numpy())
+        args = SimpleNamespace(batch=1 + r % 3, n_ref=2500, window=192, level=4)
+        wl = bench.build_workload(args, torch.device(DEV), WordVocab(synthetic.POPS), r)
+        idx, _ = bench.make_search(wl, engine_for(m), 8)()
+        np.testing.assert_array_equal(got[r]["bench_idx"], idx.cpu().numpy())
+        codes = wl.index.codes.cpu().numpy()
+        np.testing.assert_array_equal(got[r]["bench_counts"], codes[idx.cpu().numpy()].sum(1))

@@ -865,6 +865,60 @@ def test_train_mode_retrieval_query_dropout():
     assert same >= 0.5
 
 
+def test_train_mode_retrieval_lut_and_topk_bit_exact_vs_oracle(monkeypatch):
+    """Train-mode retrieval ranks DROPPED-OUT query embeddings (embedding_rag_dataset.py:385-386:
+    per-query offsets A_q != A_r, real-valued Delta) and, after a weight update inside the window,
+    against the panel snapshot (Wp != W, :334-377).  Every LUT the device quantises equals the
+    oracle's (Delta in the device's f32 arithmetic, oracle/lut_f32.c, then ``quantize_lut``) bit
+    for bit, and the oracle's exact top-k from its OWN LUT equals the device's neighbours."""
+    from oracle import knn_np
+    from knn_helpers import decode_lut
+    from src import kernels as Km
+    from src.dataset.synthetic import make_rag_dataset
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.model import build_model
+    ds, vocab = make_rag_dataset(n_samples=6, n_sites=300, n_windows=1, n_ref_samples=50, seed=12, name="train")
+    torch.manual_seed(3)
+    m = build_model(len(vocab), 64, 1, 4).to(DEV).train()
+    emb = m.bert.embedding
+    emb.dropout.p = 0.1
+    calls = []
+    orig = Km.knn_lut
+
+    def rec(tok_q, W, site_mask, n_sites, n_sites_pad, limbs=2, Aq=None, aq_period=0, Ar=None, tok0=5, tok1=6,
+            mask_tok=4, Wp=None):
+        out = orig(tok_q, W, site_mask, n_sites, n_sites_pad, limbs, Aq, aq_period, Ar, tok0, tok1, mask_tok, Wp=Wp)
+        h = lambda t: None if t is None else t.detach().float().cpu().numpy()
+        calls.append(dict(tok=tok_q.cpu().numpy(), W=h(W), Wp=h(Wp), Aq=h(Aq), aq_period=aq_period, Ar=h(Ar),
+                          sm=site_mask.cpu().numpy()[:n_sites], limbs=limbs, pad=n_sites_pad,
+                          lut=out[0].clone(), exps=out[1].cpu().numpy()))
+        return out
+    monkeypatch.setattr(Km, "knn_lut", rec)
+    k, B = 5, 6
+    batch = lambda: embedding_rag_collate_fn([ds[i] for i in range(B)])
+    codes = ds.panel_index(0, DEV).codes.cpu().numpy()
+    for step in range(2):
+        calls.clear()
+        b = ds.process_batch_retrieval(batch(), emb, DEV, k_retrieve=k)
+        assert len(calls) == 1, len(calls)
+        c = calls[0]
+        assert c["Aq"] is not None                                   # the dropped-out query offsets
+        if step == 1:
+            assert c["Wp"] is not None and not np.array_equal(c["Wp"], c["W"])   # stale panel snapshot
+        nq, S = c["tok"].shape[0], c["sm"].shape[0]
+        delta = knn_np.lut_delta_f32(c["W"], c["tok"], c["sm"], Aq=c["Aq"], aq_period=c["aq_period"], Ar=c["Ar"],
+                                     Wp=c["Wp"])
+        dq_o, e_o = knn_np.quantize_lut(delta, c["limbs"])
+        np.testing.assert_array_equal(c["exps"], e_o)
+        np.testing.assert_array_equal(decode_lut(c["lut"], nq, c["pad"], c["limbs"])[:, :S], dq_o)
+        oi, _ = knn_np.knn(codes[:, :S], dq_o, k)
+        got = torch.cat([b["rag_idx_h1"], b["rag_idx_h2"]]).cpu().numpy()
+        np.testing.assert_array_equal(got, oi)
+        with torch.no_grad():                                        # a training step's update
+            for p_ in emb.parameters():
+                p_.add_(torch.randn_like(p_) * 0.2 * (p_.std() if p_.numel() > 1 else 1.0))
+
+
 def test_train_panel_cache_window_snapshot_semantics():
     """panel_cache="window" (default): train-mode retrieval searches the panel embedded under the
     weights of the window's FIRST batch (the reference's JIT cache, embedding_rag_dataset.py:
@@ -1065,6 +1119,42 @@ def test_train_entry_point_save_best_and_resume(tmp_path, capsys):
     with open(mcsv) as f:
         rows2 = list(csv.DictReader(f))
     assert [(r["epoch"], r["mode"]) for r in rows2[4:]] == [("2", "train"), ("2", "val")]
+
+
+def test_train_entry_point_resume_from_reference_checkpoint(tmp_path):
+    """Resume from the reference trainer's own checkpoint object (a pickled BERTFoundationModel,
+    tests/golden/ref_module_tiny.pth) and from a plain state_dict: the weights load, and the run
+    starts at --resume_epoch as the reference does (train_embedding_rag.py:155-191, default 0) —
+    an explicit 0 included, and not after an epoch the file does not hold; a checkpoint of this
+    trainer without --resume_epoch continues after its saved epoch."""
+    import csv
+    import os
+    from src import train_embedding_rag as T
+    from src.model.checkpoint import load_state_dict_any
+    pth = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_module_tiny.pth")
+    torch.save({"state_dict": load_state_dict_any(pth), "epoch": 5}, tmp_path / "sd_epoch5.pt")
+    out = tmp_path / "m.model"
+    mcsv = tmp_path / "metrics.csv"
+    common = ["--synthetic", "4", "--synthetic_sites", "120", "--synthetic_windows", "1", "--synthetic_ref", "12",
+              "--dims", "64", "--layers", "2", "--attn_heads", "2", "--train_batch_size", "2",
+              "--val_batch_size", "2", "--max_steps", "1", "--log_freq", "1", "--warmup_steps", "3",
+              "--rag_k", "3", "--output_path", str(out), "--metrics_csv", str(mcsv), "--epochs", "1"]
+
+    def epochs_run():
+        with open(mcsv) as f:
+            rows = list(csv.DictReader(f))
+        os.remove(mcsv)
+        return sorted({int(r["epoch"]) for r in rows})
+    for path, extra in ((pth, []), (pth, ["--resume_epoch", "0"]), (str(tmp_path / "sd_epoch5.pt"), [])):
+        tr = T.main(common + ["--resume_path", path] + extra)
+        assert tr.loaded_own_checkpoint is False
+        assert epochs_run() == [1]                               # epoch 0 ran (CSV epochs are 1-based)
+    # the run above saved <out>.ep0, a checkpoint of this trainer: unset --resume_epoch continues after it
+    tr = T.main(common[:-1] + ["2", "--resume_path", str(out) + ".ep0"])
+    assert tr.loaded_own_checkpoint is True
+    assert epochs_run() == [2]
+    tr = T.main(common[:-1] + ["2", "--resume_path", str(out) + ".ep0", "--resume_epoch", "0"])
+    assert epochs_run() == [1, 2]
 
 
 def test_direct_weight_grads_match_autograd_accumulation():

@@ -68,15 +68,50 @@ def test_oracle_knn_canonical_and_tie_equivalent(case):
     for h in ("h1", "h2"):
         tok = g["hap_1" if h == "h1" else "hap_2"]
         delta = knn_np.lut_delta(W, tok, None, site_mask)
+        # the device-arithmetic restatement (f32, csrc/knn.hip order) agrees with the fp64 Delta
+        d32 = knn_np.lut_delta_f32(W, tok, site_mask)
+        np.testing.assert_allclose(d32, delta, rtol=1e-5, atol=1e-5 * np.abs(delta).max())
         for limbs in (1, 2):
             dq, e = knn_np.quantize_lut(delta, limbs)
             idx, d = knn_np.knn(codes, dq, k)
             np.testing.assert_array_equal(idx, g[f"Ican_{h}"])
+            idx32, _ = knn_np.knn(codes, knn_np.quantize_lut(d32, limbs)[0], k)
+            np.testing.assert_array_equal(idx32, g[f"Ican_{h}"])
         # tie-equivalence of the reference's own choice (exact fp64 distances)
         full = knn_np.distances(codes, np.rint(delta * 1.0).astype(np.int64))  # any linear map of delta
         ref_sorted = np.sort(np.take_along_axis(full, g[f"Iref_{h}"], 1), 1)
         can_sorted = np.sort(np.take_along_axis(full, g[f"Ican_{h}"], 1), 1)
         np.testing.assert_array_equal(ref_sorted, can_sorted)
+
+
+def test_oracle_lut_f32_restatement_offsets_and_exponent():
+    """oracle/lut_f32.c with query / panel AF offsets (the device's 16-lane lut_delta_kernel
+    order) and a separate panel token table stays within f32 rounding of the fp64 Delta, and
+    quantize_lut's exponent is the largest e with max|Delta| 2^e <= qmax (also at exact powers
+    of two, where floor(log2) alone is on the edge)."""
+    rng = np.random.default_rng(8)
+    nq, L, S, D = 6, 1030, 257, 48
+    W = rng.standard_normal((12, D)).astype(np.float32)
+    Wp = (W + 0.1 * rng.standard_normal(W.shape)).astype(np.float32)
+    tok = np.zeros((nq, L), np.int64)
+    tok[:, 0], tok[:, S + 1] = 2, 3
+    tok[:, 1:S + 1] = 5 + (rng.random((nq, S)) < 0.3)
+    sm = (rng.random(S) < 0.25).astype(np.uint8)
+    Aq = (0.3 * rng.standard_normal((3, L, D))).astype(np.float32)
+    Ar = (0.3 * rng.standard_normal((L, D))).astype(np.float32)
+    d32 = knn_np.lut_delta_f32(W, tok, sm, Aq=Aq, aq_period=3, Ar=Ar, Wp=Wp)
+    u = W.astype(np.float64)[tok[:, 1:S + 1]] + (Aq[np.arange(nq) % 3] - Ar[None])[:, 1:S + 1]
+    d64 = ((u - Wp[6].astype(np.float64)) ** 2).sum(-1) - ((u - Wp[5].astype(np.float64)) ** 2).sum(-1)
+    d64[:, sm.astype(bool)] = 0
+    np.testing.assert_allclose(d32, d64, rtol=1e-5, atol=1e-5 * np.abs(d64).max())
+    assert (d32[:, sm.astype(bool)] == 0).all()
+    for limbs in (1, 2):
+        qmax = (1 << (7 * limbs)) - 1
+        for m in (1.0, 0.5, 3.0, float(qmax), qmax / 1024.0, np.nextafter(np.float32(2.0), np.float32(0))):
+            dl = np.array([[m, -m / 3, 0.0]])
+            dq, e = knn_np.quantize_lut(dl, limbs)
+            assert m * 2.0 ** e[0] <= qmax < m * 2.0 ** (e[0] + 1)
+            assert abs(dq[0, 0]) <= qmax
 
 
 def test_oracle_knn_tie_break_and_small_panels():

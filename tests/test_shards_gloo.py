@@ -1,4 +1,4 @@
-"""World-size-2 gloo tests of the sharded retrieval (src/retrieval/shards.py):
+"""World-size-2 and -8 gloo tests of the sharded retrieval (src/retrieval/shards.py):
 each rank owns a contiguous range of the panel, computes its exact local top-k with GLOBAL
 indices, the partial key lists are all-gathered and merged, and the neighbours' per-site
 alt-allele counts are all-reduced — results must equal the single-shard canonical top-k
@@ -61,34 +61,41 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(120)
-def test_sharded_topk_equals_single_shard_world2():
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_topk_equals_single_shard(world):
     codes, dq, k = _case()
     want = _local_keys(codes, dq, k, 0).view(np.int64)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    got = dict(q.get(timeout=100) for _ in ps)
+    got = dict(q.get(timeout=200) for _ in ps)
     for p in ps:
         p.join(30)
         assert p.exitcode == 0
-    for r in range(2):
+    for r in range(world):
         np.testing.assert_array_equal(got[r], want)
 
 
 # ---------------------------------------------------------------------------- product plumbing
-def _plumbing_case(seed=5, n_ref=203, n_sites=80, k=6):
+# ragged per-rank query counts (world 8: one rank without queries)
+QUERIES = {2: (5, 3), 8: (5, 3, 1, 4, 0, 2, 6, 3)}
+WINDOWS = {2: ([3, 1], [1, 4]), 8: ([3, 1], [1, 4], [1], [], [7], [3], [1, 3], [0])}
+
+
+def _plumbing_case(world=2, seed=5, n_ref=203, n_sites=80, k=6):
     rng = np.random.default_rng(seed)
     codes = (rng.random((n_ref, n_sites)) < 0.25).astype(np.uint8)
     codes[:10] = codes[50:60]                          # ties across the shard boundary
+    codes[120:130] = codes[20:30]                      # (world 8: ties across several shards)
     W = rng.standard_normal((11, 16)).astype(np.float32)
     site_mask = (rng.random(n_sites) < 0.3).astype(np.uint8)
     L = n_sites + 2
     toks = []
-    for nq in (5, 3):                                  # ragged: rank 0 has 5 queries, rank 1 has 3
+    for nq in QUERIES[world]:
         t = np.zeros((nq, L), np.int64)
         t[:, 0], t[:, -1] = 2, 3
         src = codes[rng.integers(0, n_ref, nq)] ^ (rng.random((nq, n_sites)) < 0.05)
@@ -134,37 +141,42 @@ def _plumbing_worker(rank, world, port, q):
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "rag-snvbert_amd"))
         from src.retrieval.shards import PanelShard, batch_windows, sharded_neighbours
-        codes, W, site_mask, toks, k = _plumbing_case()
+        codes, W, site_mask, toks, k = _plumbing_case(world)
         shard = PanelShard.current()
         r0, r1 = shard.bounds(codes.shape[0])
         ops = _oracle_ops(codes[r0:r1], r0, W, site_mask, k)
         idx, d, cnt = sharded_neighbours(torch.from_numpy(toks[rank]), k, ops, None, shard.group)
-        wins = batch_windows([3, 1] if rank == 0 else [1, 4], shard.group)
+        wins = batch_windows(WINDOWS[world][rank], shard.group)
         q.put((rank, idx.numpy().copy(), cnt.numpy().copy(), wins))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(120)
-def test_sharded_neighbours_product_plumbing_world2():
-    codes, W, site_mask, toks, k = _plumbing_case()
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_neighbours_product_plumbing(world):
+    codes, W, site_mask, toks, k = _plumbing_case(world)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_plumbing_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_plumbing_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
     for _ in ps:
-        r, idx, cnt, wins = q.get(timeout=100)
+        r, idx, cnt, wins = q.get(timeout=200)
         got[r] = (idx, cnt, wins)
     for p in ps:
         p.join(30)
         assert p.exitcode == 0
-    for r in range(2):
+    want_w = sorted({w for ws in WINDOWS[world] for w in ws})
+    for r in range(world):
+        idx, cnt, wins = got[r]
+        assert wins == want_w
+        assert idx.shape == (QUERIES[world][r], k)
+        if QUERIES[world][r] == 0:
+            continue
         dq, _ = knn_np.quantize_lut(knn_np.lut_delta(W, toks[r], None, site_mask), 2)
         want_i, _ = knn_np.knn(codes, dq, k)
-        idx, cnt, wins = got[r]
         np.testing.assert_array_equal(idx, want_i)
         np.testing.assert_array_equal(cnt, codes[want_i].sum(1).astype(np.uint8))
-        assert wins == [1, 3, 4]

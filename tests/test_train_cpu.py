@@ -100,17 +100,18 @@ def _bucket_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_grad_bucketer_gloo_world2():
+@pytest.mark.parametrize("world", [2, 8])
+def test_grad_bucketer_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    res = dict(q.get(timeout=200) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    assert res == {r: True for r in range(world)}
 
 
 class _DirectLinear(torch.autograd.Function):
@@ -161,7 +162,7 @@ def _shared_use_worker(rank, world, port, q):
             h = torch.tanh(lin(h, body))
             return shared(torch.tanh(head(h)).repeat(1, 4)).pow(2).sum()   # one autograd use too
 
-        n_uses = 3 if rank == 0 else 1
+        n_uses = _uses(rank)
         x = torch.randn(5, 8, generator=torch.Generator().manual_seed(rank))
         fwd(x, n_uses, True).backward()
         assert bk.finish() == 1.0
@@ -179,7 +180,7 @@ def _shared_use_worker(rank, world, port, q):
                 m.weight, m.bias = w, b
             xr = torch.randn(5, 8, generator=torch.Generator().manual_seed(r))
             shared_, body_, head_ = s2, b2, h2
-            h = sum(shared_(xr * (u + 1)) for u in range(3 if r == 0 else 1))
+            h = sum(shared_(xr * (u + 1)) for u in range(_uses(r)))
             h = torch.tanh(body_(h))
             shared_(torch.tanh(head_(h)).repeat(1, 4)).pow(2).sum().backward()
             for j, p in enumerate(ps):
@@ -197,17 +198,24 @@ def _index_of(fp, p):
     return next(i for i, t in enumerate(fp.params) if t is p)
 
 
-def test_grad_bucketer_launches_after_last_use_in_rank_order():
+def _uses(rank):
+    """Rank-dependent use count of the shared layer (1..4): its bucket finishes at a different
+    point of every rank's backward."""
+    return (3, 1, 4, 2, 1, 3, 2, 4)[rank % 8]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_grad_bucketer_launches_after_last_use_in_rank_order(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shared_use_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_shared_use_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    res = dict(q.get(timeout=200) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res[0] == res[1] and res[0][0] is True, res
+    assert all(res[r] == res[0] for r in range(world)) and res[0][0] is True, res
 
 
 def test_trainer_metric_rows_and_early_stopping_match_reference(tmp_path):
