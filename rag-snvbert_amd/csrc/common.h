@@ -75,6 +75,7 @@ struct Options {
   int64_t g2_variant;      // wide-row GEMM diagnostics: 1 no LDS-DMA, 2 no MFMA (wrong results; timing only),
                            // 3 stamps into the snvrag_tail_stamps buffer
   int64_t tail_persist;    // 1: the persistent block tail (tailp_kernel, A/B); 0 (default): tail_kernel
+  int64_t tail_split;      // wide-row tail: split a last partial round of <= this many 128-row tiles into 32-row tiles (0: off)
   int64_t proj_wide;       // 1 (default): snvrag_proj_forward at D = 384 on the wide-row projection (tailw.hip,
                            // 0.62 vs 0.68 ms, bit-identical); 0: tail.hip PROJ mode
   int64_t tail_wide;       // block tail at D = 384 (PRE): 1 (default) the wide-row form (tailw.hip), 0 tail_kernel,

@@ -105,6 +105,7 @@ const OptDesc kOpts[] = {
     {"ln_rows1", &Options::ln_rows1, 0},           {"tail_persist", &Options::tail_persist, 0},
     {"tail_wide", &Options::tail_wide, 1},         {"proj_wide", &Options::proj_wide, 1},
     {"g2_variant", &Options::g2_variant, 0},     {"g2_groups", &Options::g2_groups, 0},
+    {"tail_split", &Options::tail_split, 64},
 };
 Options make_options() {
   Options o{};

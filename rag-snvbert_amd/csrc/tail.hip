@@ -1197,7 +1197,7 @@ static int launch_tail(TailArgs a, hipStream_t s) {
       // 1.454 / 1.399 at tail_kernel's 25 k and 1.444 without)
       const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 10000) : 0;
       return tailw_launch(a.M, a.act, a.resid, a.out, a.ws, a.vec, a.b_o, a.g1, a.be1, a.eps, desync,
-                          (int)options().tail_wide == 2 ? 1 : 0, s);
+                          (int)options().tail_wide >= 2 ? (int)options().tail_wide - 1 : 0, s);
     }
   // the persistent kernel (option tail_persist; measured no faster, see tailp_kernel): 32-bit
   // byte offsets of the in-place rows

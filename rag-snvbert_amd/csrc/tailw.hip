@@ -246,18 +246,20 @@ struct TwArgs {
   float eps;
   int desync;
   unsigned long long* stamps;   // VAR 1: [workgroup][wave][8] s_memtime stamps
+  int n_full;                   // workgroups of 128 rows (the rest: 32 rows)
 };
 
-template <int VAR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void tailw_kernel(TwArgs p) {
-  constexpr int D = TW_D, NT = TW_NT;
+// G token groups of 32 rows (G = 4: a 128-row tile; G = 1: the 32-row tiles that spread the last
+// partial round of 128-row tiles over more CUs, tailw_kernel below).  GI: the group after whose
+// MFMAs a step issues its W loads
+template <int VAR, int G>
+__device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
+  constexpr int D = TW_D, NT = TW_NT, GI = G > 1 ? 1 : 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long row0 = (long)blockIdx.x * 128;
   unsigned long long st[8];
   auto stamp = [&](int i) {
-    if constexpr (VAR == 1) st[i] = __builtin_amdgcn_s_memtime();
+    if constexpr (VAR & 1) st[i] = __builtin_amdgcn_s_memtime();
   };
   // first-round stagger (tail.hip): later rounds' prologue bursts overlap other CUs' MFMAs
   if (p.desync > 0 && blockIdx.x < 256) {
@@ -279,16 +281,21 @@ void tailw_kernel(TwArgs p) {
   {
     const int l = tw_lane();
     const int voff = (32 * wave + (l & 31)) * (D * 2) + 32 * (l >> 5);
+    if (wave < G) {
 #pragma unroll
-    for (int s = 0; s < TW_KS; ++s)
-      dma_x4(ars, lds0 + TW_X + (s * 4 + wave) * TW_FRAG, voff, 64 * (s >> 1) + 16 * (s & 1));
+      for (int s = 0; s < TW_KS; ++s)
+        dma_x4(ars, lds0 + TW_X + (s * 4 + wave) * TW_FRAG, voff, 64 * (s >> 1) + 16 * (s & 1));
+    }
   }
   u32x4 wf[TW_RING];                                 // W fragment ring
   // W fragment F of the stream into register r (soffset: scalar)
   // (compiler-visible loads: its waitcnt pass places the waits before every read of the register —
   // hand-counted asm loads were seen copied into AGPRs by the register allocator before they landed)
   const __amdgpu_buffer_rsrc_t wrb = __builtin_amdgcn_make_buffer_rsrc((void*)p.ws, (short)0, TW_NFRAG * TW_FRAG, 0x00020000);
-  auto loadW = [&](u32x4& r, int F) { r = __builtin_amdgcn_raw_buffer_load_b128(wrb, lane16, F * TW_FRAG, 0); };
+  // (diagnostic VAR bit 1: every load reads fragment F % 12 — a cache-resident 12 KiB, results wrong)
+  auto loadW = [&](u32x4& r, int F) {
+    r = __builtin_amdgcn_raw_buffer_load_b128(wrb, lane16, ((VAR & 2) ? F % 12 : F) * TW_FRAG, 0);
+  };
   // stream offsets: FFN1(h) step i = wave w's tile of chunk 4 (h >> 1) + w, half h & 1;
   // FFN2(h) step u, tile t = chunk 4 (h >> 1) + u / 2, k16 step 2 (h & 1) + u % 2, tile 3w + t
   auto f_ffn1 = [&](int h, int i) { return TW_FPRE + (4 * (h >> 1) + wave) * TW_FPC + 2 * i + (h & 1); };
@@ -308,7 +315,7 @@ void tailw_kernel(TwArgs p) {
   {
     const int l = tw_lane();
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       long r = row0 + 32 * g + (l & 31);
       r = r < p.M ? r : (long)p.M - 1;
 #pragma unroll
@@ -330,7 +337,7 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) asm volatile("" : "+v"(rr[t][g][0]), "+v"(rr[t][g][1]));
+    for (int g = 0; g < G; ++g) asm volatile("" : "+v"(rr[t][g][0]), "+v"(rr[t][g][1]));
   tw_barrier();
   stamp(1);
 
@@ -344,19 +351,19 @@ void tailw_kernel(TwArgs p) {
   // a third buffer beside the residual rows pushed the W fragments into AGPR copies taken before
   // their loads had landed)
 #pragma unroll
-  for (int g = 0; g < 4; ++g) bq[0][g] = rdB(TW_X, g);
+  for (int g = 0; g < G; ++g) bq[0][g] = rdB(TW_X, g);
   tw_unroll([&](auto qc) {
     constexpr int q = decltype(qc)::value, n0 = 3 * q;
     tw_wait3<tw_younger(q)>(wf[n0 % TW_RING], wf[(n0 + 1) % TW_RING], wf[(n0 + 2) % TW_RING]);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
         if constexpr (q == 0) tw_mfma0<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
         else tw_mfma<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
       }
       if constexpr (q + 1 < TW_KS) bq[(q + 1) & 1][g] = rdB(TW_X, (q + 1) * 4 + g);
-      if (g == 1)
+      if (g == GI)
         tw_unroll([&](auto tc) { issue_a(std::integral_constant<int, n0 + TW_AH + decltype(tc)::value>{}); },
                   std::make_integer_sequence<int, 3>{});
     }
@@ -373,13 +380,13 @@ void tailw_kernel(TwArgs p) {
     // (packed f32 math: pairs of features per v_pk_* instruction)
     tw_f2 s2v[4], q2v[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
+    for (int g = 0; g < G; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       float bo[16];
       tw_ld16(tb + 4 * 32 * (3 * wave + t), bo);
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const tw_f2 v = tw_f2{acc[t][g][2 * e], acc[t][g][2 * e + 1]} + tw_f2{bo[2 * e], bo[2 * e + 1]} +
@@ -392,7 +399,7 @@ void tailw_kernel(TwArgs p) {
     }
     float sum[4], sq[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       sum[g] = s2v[g].x + s2v[g].y;
       sq[g] = q2v[g].x + q2v[g].y;
     }
@@ -403,7 +410,7 @@ void tailw_kernel(TwArgs p) {
       float bo[16];
       tw_ld16(tb + 4 * 32 * (3 * wave + t), bo);
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float v = acc[t][g][i] + bo[i] + tw_bf(rr[t][g][i >> 3], i & 7);
@@ -416,10 +423,10 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {}   // v back in AGPRs
+      for (int g = 0; g < G; ++g) {}   // v back in AGPRs
     const int l = tw_lane();
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       sum[g] = tw_xsum32(sum[g]);
       sq[g] = tw_xsum32(sq[g]);
       s1[wave * 128 + 32 * g + (l & 31)] = make_float2(sum[g], sq[g]);
@@ -431,7 +438,7 @@ void tailw_kernel(TwArgs p) {
     const uint32_t tb = lds0 + TW_H + 64 * (l >> 5);
     float mean[4], rstd[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < 4; ++w2) {
@@ -449,7 +456,7 @@ void tailw_kernel(TwArgs p) {
       tw_ld16(tb + 4 * (2 * D + 32 * (3 * wave + t)), bb);
       const int T = 3 * wave + t;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G; ++g) {
         float y[16];
 #if TW_PACKED_LN
         const float nmr = -mean[g] * rstd[g];
@@ -488,15 +495,15 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[t][g] = f32x16{};
+    for (int g = 0; g < G; ++g) acc[t][g] = f32x16{};
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(acc[t][g]));
+    for (int g = 0; g < G; ++g) asm volatile("" : "+a"(acc[t][g]));
   typedef float f2 __attribute__((ext_vector_type(2)));
-  f2 sf1[4], sf2[4];                                  // LN_f partial sums (pairs of hidden units)
+  float sa1[4], sa2[4];                               // LN_f partial sums of this lane's hidden units
 #pragma unroll
-  for (int g = 0; g < 4; ++g) sf1[g] = sf2[g] = f2{0.f, 0.f};
+  for (int g = 0; g < G; ++g) sa1[g] = sa2[g] = 0.f;
   u32x4 b1v[4];                                       // b1 of the tile whose epilogue runs next
   const __amdgpu_buffer_rsrc_t b1b = __builtin_amdgcn_make_buffer_rsrc((void*)p.vec, (short)0, 4 * D * 4, 0x00020000);
   auto b1_load = [&](int h) {                         // b1[64 c' + 32 (h & 1) + 8 r + 4 hh .. + 3]
@@ -506,23 +513,42 @@ void tailw_kernel(TwArgs p) {
     for (int r = 0; r < 4; ++r) b1v[r] = __builtin_amdgcn_raw_buffer_load_b128(b1b, vo + 32 * r, so, 0);
   };
   // epilogue unit k (0 .. 7: group k / 2, k16 step j = k % 2 of the tile) of the half-round with
-  // parity Q: 8 hidden units of this lane's token -> its 16-B slot of an FFN2 B fragment in H half Q
-  auto epi_unit = [&](auto k_tag, auto q_tag) {
-    constexpr int k = decltype(k_tag)::value, Q = decltype(q_tag)::value, g = k >> 1, j = k & 1;
-    const f32x16& a = Q ? ha[g] : hv[g];
-    uint32_t pk[4];
+  // parity Q: 8 hidden units of this lane's token -> its 16-B slot of an FFN2 B fragment in H half Q.
+  // A unit runs as TW_EP pieces spread over the MFMA gaps of three FFN1 steps (piece p after MFMA
+  // g of step 3k + p / G): values v at piece v (TW_EP - 2) / 8 (b1, LeakyReLU, the LN_f sums: five
+  // scalar VALU each), the four bf16 packs at piece TW_EP - 2, the LDS write at TW_EP - 1 — at most
+  // ~5 VALU per 32x32x16 gap, which the MFMA hides; one ~40-instruction block per unit (packed f32)
+  // stalled the matrix pipe for ~130 cycles after every third step.
+  constexpr int TW_EP = 3 * G;
+  float ex[8];                                        // the unit's values between its pieces
+  uint32_t epk[4];
+  auto epi_piece = [&](auto k_tag, auto q_tag, auto p_tag) {
+    constexpr int k = decltype(k_tag)::value, Q = decltype(q_tag)::value, pc = decltype(p_tag)::value;
+    constexpr int g = k >> 1, j = k & 1;
+    if constexpr (g < G) {
+      const f32x16& a = Q ? ha[g] : hv[g];
+      tw_unroll([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        if constexpr (v * (TW_EP - 2) / 8 == pc) {
+          // (LeakyReLU as plain code: the inline-asm form made hipcc pad an s_nop after every one)
+          const float u = a[8 * j + v] + __uint_as_float(b1v[(8 * j + v) >> 2][(8 * j + v) & 3]);
+          const float x = fmaxf(u, 0.1f * u);
+          ex[v] = x;
+          sa1[g] += x;
+          sa2[g] = fmaf(x, x, sa2[g]);
+        }
+      }, std::make_integer_sequence<int, 8>{});
+      if constexpr (pc == TW_EP - 2) {
 #pragma unroll
-    for (int e2 = 0; e2 < 4; ++e2) {
-      const int i0 = 8 * j + 2 * e2;
-      f2 x = f2{a[i0], a[i0 + 1]} +
-             f2{__uint_as_float(b1v[i0 >> 2][i0 & 3]), __uint_as_float(b1v[(i0 + 1) >> 2][(i0 + 1) & 3])};
-      x = f2{tw_lrelu(x.x), tw_lrelu(x.y)};
-      sf1[g] += x;
-      sf2[g] = x * x + sf2[g];
-      pk[e2] = tw_pack2(x.x, x.y);
+        for (int e2 = 0; e2 < 4; ++e2) epk[e2] = tw_pack2(ex[2 * e2], ex[2 * e2 + 1]);
+      }
+      if constexpr (pc == TW_EP - 1)
+        *reinterpret_cast<u32x4*>(smem + TW_H + Q * 32768 + ((wave * 2 + j) * 4 + g) * TW_FRAG + lane16) =
+            u32x4{epk[0], epk[1], epk[2], epk[3]};
     }
-    *reinterpret_cast<u32x4*>(smem + TW_H + Q * 32768 + ((wave * 2 + j) * 4 + g) * TW_FRAG + lane16) =
-        u32x4{pk[0], pk[1], pk[2], pk[3]};
+  };
+  auto epi_unit = [&](auto k_tag, auto q_tag) {       // a whole unit at once (half-round 11's epilogue)
+    tw_unroll([&](auto pc) { epi_piece(k_tag, q_tag, pc); }, std::make_integer_sequence<int, TW_EP>{});
   };
   // fragment r of an iteration (r relative to its first fragment; h = the iteration's half-round):
   // [0, 24) FFN1(h), [24, 48) FFN2(h - 1), then the next iteration's FFN1(h + 1) (LAST: FFN2(11))
@@ -534,7 +560,7 @@ void tailw_kernel(TwArgs p) {
     else loadW(wf[n % TW_RING], f_ffn1(h + 1, r - 48));
   };
   // FFN1(h), parity P; Q0 = its first global step (the representative half-round for h >= 1);
-  // EPI: with the epilogue of half-round h - 1 (units at steps 2, 5, ..., 23)
+  // EPI: with the epilogue of half-round h - 1 (unit k over steps 3k .. 3k + 2, one piece per MFMA gap)
   auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag, auto nop_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
     constexpr bool EPI = decltype(epi_tag)::value, NOP = decltype(nop_tag)::value;
@@ -542,8 +568,8 @@ void tailw_kernel(TwArgs p) {
     tw_unroll([&](auto ic) {
       constexpr int i = decltype(ic)::value, q = Q0 + i, n = F0 + i;
       tw_wait1<tw_wait_of(q)>(wf[n % TW_RING]);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      tw_unroll([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
         if constexpr (P == 0) {
           if constexpr (i == 0) tw_mfma0<false, NOP>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
           else tw_mfma<false, NOP>(hv[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
@@ -551,16 +577,19 @@ void tailw_kernel(TwArgs p) {
           if constexpr (i == 0) tw_mfma0<true, NOP>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
           else tw_mfma<true, NOP>(ha[g], wf[n % TW_RING], bq[(i + 2) % 3][g]);
         }
-        if constexpr (i + 2 < 24) bq[(i + 4) % 3][g] = rdB(TW_X, (i + 2) * 4 + g);
-        if (g == 1) {
+        // (diagnostic VAR bit 2: FFN1 reads no B fragments — stale operands, no LDS traffic)
+        if constexpr (i + 2 < 24 && !(VAR & 4)) bq[(i + 4) % 3][g] = rdB(TW_X, (i + 2) * 4 + g);
+        if constexpr (g == GI) {
           if constexpr (Q0 == TW_QA) issue_a(std::integral_constant<int, n + TW_AH>{});
           else issue_it(std::integral_constant<int, i + TW_AH>{}, h, std::false_type{});
         }
-      }
+        if constexpr (EPI) {                          // piece (i % 3) G + g of unit i / 3, in this gap
+          epi_piece(std::integral_constant<int, i / 3>{}, std::integral_constant<int, 1 - P>{},
+                    std::integral_constant<int, (i % 3) * G + g>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }, std::make_integer_sequence<int, G>{});
       if constexpr (Q0 == TW_QA && i == 16) b1_load(0);
-      if constexpr (EPI && i >= 2 && (i - 2) % 3 == 0) {
-        epi_unit(std::integral_constant<int, (i - 2) / 3>{}, std::integral_constant<int, 1 - P>{});
-      }
       __builtin_amdgcn_sched_barrier(0);
     }, std::make_integer_sequence<int, 24>{});
     if constexpr (P == 0) tw_drain_h4<false>(hv);
@@ -575,7 +604,7 @@ void tailw_kernel(TwArgs p) {
     constexpr uint32_t HB = TW_H + P * 32768;
     constexpr int F0 = tw_f0(Q0);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       bq[0][g] = rdB(HB, g);
       bq[1][g] = rdB(HB, 4 + g);
     }
@@ -583,12 +612,12 @@ void tailw_kernel(TwArgs p) {
       constexpr int u = decltype(uc)::value, q = Q0 + u, n0 = F0 + 3 * u;
       tw_wait3<tw_wait_of(q)>(wf[n0 % TW_RING], wf[(n0 + 1) % TW_RING], wf[(n0 + 2) % TW_RING]);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G; ++g) {
 #pragma unroll
         for (int t = 0; t < 3; ++t) tw_mfma<true, NOP>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
         if constexpr (u + 2 < 8) bq[(u + 2) % 3][g] = rdB(HB, (u + 2) * 4 + g);
         else if constexpr (!FINAL && !LAST) bq[(u + 2) % 3][g] = rdB(TW_X, (u - 6) * 4 + g);   // next FFN1 steps 0, 1
-        if (g == 1) {
+        if (g == GI) {
           if constexpr (FINAL) {
             if constexpr (n0 + TW_AH < TW_NFRAGW)
               tw_unroll([&](auto tc) {
@@ -609,13 +638,13 @@ void tailw_kernel(TwArgs p) {
     tw_drain_o(acc);
   };
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < G; ++g) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
   seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, std::true_type{});
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < G; ++g) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
@@ -652,9 +681,9 @@ void tailw_kernel(TwArgs p) {
        std::true_type{}, std::true_type{});
   float st1[4], st2[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    st1[g] = sf1[g].x + sf1[g].y;
-    st2[g] = sf2[g].x + sf2[g].y;
+  for (int g = 0; g < G; ++g) {
+    st1[g] = sa1[g];
+    st2[g] = sa2[g];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the overrun loads have landed
   stamp(4);
@@ -666,7 +695,7 @@ void tailw_kernel(TwArgs p) {
   {
     const int l = tw_lane();
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       st1[g] = tw_xsum32(st1[g]);
       st2[g] = tw_xsum32(st2[g]);
       s2[wave * 128 + 32 * g + (l & 31)] = make_float2(st1[g], st2[g]);
@@ -677,7 +706,7 @@ void tailw_kernel(TwArgs p) {
   {
     const int l = tw_lane();
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < 4; ++w2) {
@@ -695,7 +724,7 @@ void tailw_kernel(TwArgs p) {
     // u = hr (acc - hm c1) + b2' = acc hr + (b2' - hm hr c1), in pairs (v_pk_fma_f32)
     tw_f2 s2v[4], q2v[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
+    for (int g = 0; g < G; ++g) s2v[g] = q2v[g] = tw_f2{0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int T = 3 * wave + t;
@@ -703,7 +732,7 @@ void tailw_kernel(TwArgs p) {
       tw_ld16(eb + 4 * (32 * T), b2);
       tw_ld16(eb + 4 * (D + 32 * T), c1);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G; ++g) {
         const u32x4 xa = rdB(TW_X, (2 * T) * 4 + g), xb = rdB(TW_X, (2 * T + 1) * 4 + g);
         const float nhh = -hm[g] * hr[g];
 #pragma unroll
@@ -720,7 +749,7 @@ void tailw_kernel(TwArgs p) {
     }
     float sum[4], sq[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       sum[g] = s2v[g].x + s2v[g].y;
       sq[g] = q2v[g].x + q2v[g].y;
     }
@@ -733,7 +762,7 @@ void tailw_kernel(TwArgs p) {
       tw_ld16(eb + 4 * (32 * T), b2);
       tw_ld16(eb + 4 * (D + 32 * T), c1);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G; ++g) {
         const u32x4 xa = rdB(TW_X, (2 * T) * 4 + g), xb = rdB(TW_X, (2 * T + 1) * 4 + g);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -750,10 +779,10 @@ void tailw_kernel(TwArgs p) {
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {}
+      for (int g = 0; g < G; ++g) {}
     const int l = tw_lane();
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       sum[g] = tw_xsum32(sum[g]);
       sq[g] = tw_xsum32(sq[g]);
       s3[wave * 128 + 32 * g + (l & 31)] = make_float2(sum[g], sq[g]);
@@ -764,7 +793,7 @@ void tailw_kernel(TwArgs p) {
     const int l = tw_lane();
     float mean[4], rstd[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < G; ++g) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < 4; ++w2) {
@@ -782,7 +811,7 @@ void tailw_kernel(TwArgs p) {
       tw_ld16(eb + 4 * (2 * D + 32 * T), g2);
       tw_ld16(eb + 4 * (3 * D + 32 * T), be2);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < G; ++g) {
         const long r = row0 + 32 * g + (l & 31);
         const float nmr = -mean[g] * rstd[g];
         float y[16];
@@ -807,7 +836,7 @@ void tailw_kernel(TwArgs p) {
       }
     }
   }
-  if constexpr (VAR == 1) {
+  if constexpr (VAR & 1) {
     stamp(5);
     if ((threadIdx.x & 63) == 0 && p.stamps) {
 #pragma unroll
@@ -816,14 +845,34 @@ void tailw_kernel(TwArgs p) {
   }
 }
 
+// workgroups [0, n_full): 128-row tiles; the rest: 32-row tiles after row 128 n_full (the launch's
+// last partial round of 128-row tiles spread over 4x the CUs, dispatched last)
+template <int VAR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void tailw_kernel(TwArgs p) {
+  if ((int)blockIdx.x < p.n_full) tailw_body<VAR, 4>(p, (long)blockIdx.x * 128);
+  else tailw_body<VAR, 1>(p, (long)p.n_full * 128 + (long)(blockIdx.x - p.n_full) * 32);
+}
+
 int tailw_launch(int M, const void* att, const void* resid, void* out, const void* ws, const float* vec,
                  const float* b_o, const float* g1, const float* be1, float eps, int desync, int var,
                  hipStream_t s) {
+  // the last partial round of 128-row tiles (rem of 256 CUs) as 4 rem workgroups of 32 rows, when
+  // they fit one round of 32-row tiles (option tail_split = the largest rem split; 0: off)
+  const long T = cdiv(M, 128), rem = T % 256;
+  const long split = options().tail_split;
+  const long n_full = (T > 256 && rem > 0 && rem <= split) ? T - rem : T;
+  const long nwg = n_full + cdiv((long)M - n_full * 128, 32);
   TwArgs a{M, (const bf16*)att, (const bf16*)resid, (bf16*)out, (const char*)ws, vec, b_o, g1, be1, eps, desync,
-           diag_stamps()};
-  auto kern = (var == 1 && a.stamps) ? tailw_kernel<1> : tailw_kernel<0>;
+           diag_stamps(), (int)n_full};
+  // var (option tail_wide - 1): bit 0 phase stamps, bit 1 / bit 2 the W-latency / FFN1-LDS
+  // diagnostics (wrong results: tools/tailw_micro.py timing only)
+  if ((var & 1) && !a.stamps) var &= ~1;
+  auto kern = var == 1 ? tailw_kernel<1> : var == 2 ? tailw_kernel<2> : var == 3 ? tailw_kernel<3>
+              : var == 4 ? tailw_kernel<4> : var == 5 ? tailw_kernel<5> : var == 6 ? tailw_kernel<6>
+              : var == 7 ? tailw_kernel<7> : tailw_kernel<0>;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS));
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, 128)), dim3(256), TW_LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), TW_LDS, s, a);
   SNV_LAUNCH_CHECK();
   return 0;
 }

@@ -325,14 +325,15 @@ def test_tail32_kernel(D, M):
     assert (out.double() - ref).abs().mean() < 1e-2
 
 
-@pytest.mark.parametrize("M", [777, 128 * 3, 1, 4 * 1030 + 5, 64 * 1030])
+@pytest.mark.parametrize("M", [777, 128 * 3, 1, 4 * 1030 + 5, 64 * 1030, 294 * 128 - 51])
 def test_tail_wide_kernel(M):
     """Wide-row block tail (csrc/tailw.hip, option tail_wide: wave w owns features 96w..96w+95 and
     hidden chunks 4c + w, its weight fragments loaded straight into its registers; att / x1 and the
     hidden of a round are the LDS-resident operands) vs float64 torch with test_tail32_kernel's bar,
     in place; and close to tail_kernel on the same operands (the same function; the accumulation
     order of the bias and of the cross-wave row statistics differs).  Ragged M: 777, one row, a
-    partial last tile, 515 workgroups."""
+    partial last tile, 515 and 294 tiles (the last partial round split into 32-row workgroups:
+    bit-identical to the unsplit launch)."""
     D = 384
     g = torch.Generator(device="cpu").manual_seed(11 * M + 3)
     bf, F = torch.bfloat16, torch.nn.functional
@@ -362,6 +363,13 @@ def test_tail_wide_kernel(M):
         K().tail_forward(att, yb, ts, b_o, g1, be1, vec)
     assert torch.isfinite(ya.float()).all()
     torch.testing.assert_close(ya.double(), ref, rtol=5e-2, atol=5e-2)
+    if M > 256 * 128:
+        # the last partial round as 32-row workgroups (option tail_split; 64 x 1030: 12 of them,
+        # 294 x 128 - 51: 151, the last ragged) computes every row exactly as a 128-row tile does
+        yc = x.clone()
+        with K().option("tail_wide", 1), K().option("tail_split", 0):
+            K().tail_forward(att, yc, ts, b_o, g1, be1, vec)
+        torch.testing.assert_close(yc, ya, rtol=0, atol=0)
     ea, eb = (ya.double() - ref).abs().mean(), (yb.double() - ref).abs().mean()
     assert ea < 1e-2 and ea < 1.25 * eb + 1e-4, (float(ea), float(eb))
     # vs tail_kernel: the hidden is rounded to bf16 in both, from differently ordered f32 sums, so
