@@ -547,9 +547,6 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
             u32x4{epk[0], epk[1], epk[2], epk[3]};
     }
   };
-  auto epi_unit = [&](auto k_tag, auto q_tag) {       // a whole unit at once (half-round 11's epilogue)
-    tw_unroll([&](auto pc) { epi_piece(k_tag, q_tag, pc); }, std::make_integer_sequence<int, TW_EP>{});
-  };
   // fragment r of an iteration (r relative to its first fragment; h = the iteration's half-round):
   // [0, 24) FFN1(h), [24, 48) FFN2(h - 1), then the next iteration's FFN1(h + 1) (LAST: FFN2(11))
   auto issue_it = [&](auto r_tag, int h, auto last_tag) {
@@ -561,9 +558,9 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   };
   // FFN1(h), parity P; Q0 = its first global step (the representative half-round for h >= 1);
   // EPI: with the epilogue of half-round h - 1 (unit k over steps 3k .. 3k + 2, one piece per MFMA gap)
-  auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag, auto nop_tag) {
+  auto seg1 = [&](int h, auto p_tag, auto q0_tag, auto epi_tag, auto nop_tag, auto b1_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
-    constexpr bool EPI = decltype(epi_tag)::value, NOP = decltype(nop_tag)::value;
+    constexpr bool EPI = decltype(epi_tag)::value, NOP = decltype(nop_tag)::value, B1 = decltype(b1_tag)::value;
     constexpr int F0 = tw_f0(Q0);
     tw_unroll([&](auto ic) {
       constexpr int i = decltype(ic)::value, q = Q0 + i, n = F0 + i;
@@ -590,6 +587,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
         }
       }, std::make_integer_sequence<int, G>{});
       if constexpr (Q0 == TW_QA && i == 16) b1_load(0);
+      if constexpr (B1 && i == 8) b1_load(h);        // for this half-round's epilogue in the next FFN2
       __builtin_amdgcn_sched_barrier(0);
     }, std::make_integer_sequence<int, 24>{});
     if constexpr (P == 0) tw_drain_h4<false>(hv);
@@ -597,10 +595,12 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   };
   // FFN2(h) from H half h & 1 (P = h & 1); in the loop (Q0 = representative) its iteration is h + 1;
   // LAST: the iteration of h = 10, whose lookahead loads FFN2(11); FINAL: FFN2(11) itself
-  auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag, auto nop_tag) {
+  // EPI: with the epilogue of half-round h + 1 (whose FFN1 ran just before; parity 1 - P), one piece
+  // after each of the 24 G MFMAs (unit k over gaps 3 G k .. 3 G k + 3 G - 1)
+  auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag, auto nop_tag, auto epi_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
     constexpr bool LAST = decltype(last_tag)::value, FINAL = decltype(final_tag)::value;
-    constexpr bool NOP = decltype(nop_tag)::value;
+    constexpr bool NOP = decltype(nop_tag)::value, EPI = decltype(epi_tag)::value;
     constexpr uint32_t HB = TW_H + P * 32768;
     constexpr int F0 = tw_f0(Q0);
 #pragma unroll
@@ -611,13 +611,20 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     tw_unroll([&](auto uc) {
       constexpr int u = decltype(uc)::value, q = Q0 + u, n0 = F0 + 3 * u;
       tw_wait3<tw_wait_of(q)>(wf[n0 % TW_RING], wf[(n0 + 1) % TW_RING], wf[(n0 + 2) % TW_RING]);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int t = 0; t < 3; ++t) tw_mfma<true, NOP>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
+      tw_unroll([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        tw_unroll([&](auto tc) {
+          constexpr int t = decltype(tc)::value, x = 3 * G * u + 3 * g + t;
+          tw_mfma<true, NOP>(acc[t][g], wf[(n0 + t) % TW_RING], bq[u % 3][g]);
+          if constexpr (EPI) {
+            epi_piece(std::integral_constant<int, x / (3 * G)>{}, std::integral_constant<int, 1 - P>{},
+                      std::integral_constant<int, x % (3 * G)>{});
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }, std::make_integer_sequence<int, 3>{});
         if constexpr (u + 2 < 8) bq[(u + 2) % 3][g] = rdB(HB, (u + 2) * 4 + g);
         else if constexpr (!FINAL && !LAST) bq[(u + 2) % 3][g] = rdB(TW_X, (u - 6) * 4 + g);   // next FFN1 steps 0, 1
-        if (g == GI) {
+        if constexpr (g == GI) {
           if constexpr (FINAL) {
             if constexpr (n0 + TW_AH < TW_NFRAGW)
               tw_unroll([&](auto tc) {
@@ -630,9 +637,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
             }, std::make_integer_sequence<int, 3>{});
           }
         }
-      }
-      // b1 of the FFN1 tile just computed (half-round h + 1), after this step's W loads (tw_extra)
-      if constexpr (u == 0 && !FINAL) b1_load(h + 1);
+      }, std::make_integer_sequence<int, G>{});
       __builtin_amdgcn_sched_barrier(0);
     }, std::make_integer_sequence<int, 8>{});
     tw_drain_o(acc);
@@ -642,29 +647,39 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
-  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, std::true_type{});
+  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, std::true_type{},
+       std::false_type{});
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
+  // FFN1(1) with the epilogue of half-round 0 in its MFMA gaps (no FFN2 to carry it yet); then b1 of
+  // half-round 1 (after the epilogue's last read of b1v)
+  seg1(1, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_Q0>{}, std::true_type{}, std::true_type{},
+       std::false_type{});
+  b1_load(1);
+  tw_barrier();                                       // H half 0 complete
+  // steady state: FFN2(h - 1) with the epilogue of half-round h in its MFMA gaps, FFN1(h + 1) (pure
+  // MFMA + B-fragment reads), one barrier (H half h & 1 complete).  The W fragments are consumed in
+  // the same global order as [FFN1(h) FFN2(h - 1)] iterations; only the epilogue moved from FFN1's
+  // gaps (~5 VALU beside every MFMA, at the issue limit) to FFN2's, which carry no other VALU.
 #pragma unroll 1
   for (int h = 1; h < 11; h += 2) {
-    seg1(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::false_type{});
-    tw_barrier();                                     // H half (h - 1) & 1 complete
     seg2(h - 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{}, std::false_type{});
-    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::false_type{});
+         std::false_type{}, std::false_type{}, std::true_type{});
+    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::false_type{},
+         std::false_type{}, std::true_type{});
     tw_barrier();
     seg2(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{}, std::false_type{});
+         std::false_type{}, std::false_type{}, std::true_type{});
+    seg1(h + 2, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::false_type{},
+         std::false_type{}, std::true_type{});
+    tw_barrier();
   }
-  seg1(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::true_type{}, std::true_type{});
-  tw_barrier();
+  // FFN2(10) with the epilogue of half-round 11, then FFN2(11)
   seg2(10, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::true_type{},
-       std::false_type{}, std::true_type{});
-  // the epilogue of half-round 11, then its FFN2
-  tw_unroll([&](auto kc) { epi_unit(kc, std::integral_constant<int, 1>{}); }, std::make_integer_sequence<int, 8>{});
+       std::false_type{}, std::true_type{}, std::true_type{});
   tw_barrier();
   // H half 0 is free from here (its last reader, FFN2(10), is behind this barrier): the LN epilogue's
   // tables [b2' | c1 | g2 | be2] (6 KiB) arrive there by LDS-DMA during FFN2(11) (retired by the
@@ -678,7 +693,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     }
   }
   seg2(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QF>{}, std::false_type{},
-       std::true_type{}, std::true_type{});
+       std::true_type{}, std::true_type{}, std::false_type{});
   float st1[4], st2[4];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -862,7 +877,7 @@ int tailw_launch(int M, const void* att, const void* resid, void* out, const voi
   const long T = cdiv(M, 128), rem = T % 256;
   const long split = options().tail_split;
   const long n_full = (T > 256 && rem > 0 && rem <= split) ? T - rem : T;
-  const long nwg = n_full + cdiv((long)M - n_full * 128, 32);
+  const long nwg = n_full < T ? n_full + cdiv((long)M - n_full * 128, 32) : T;
   TwArgs a{M, (const bf16*)att, (const bf16*)resid, (bf16*)out, (const char*)ws, vec, b_o, g1, be1, eps, desync,
            diag_stamps(), (int)n_full};
   // var (option tail_wide - 1): bit 0 phase stamps, bit 1 / bit 2 the W-latency / FFN1-LDS
