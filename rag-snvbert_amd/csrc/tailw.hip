@@ -136,6 +136,13 @@ __device__ __forceinline__ void tw_unroll(Body&& body, std::integer_sequence<int
 // loop (phase A, half-round 0, the last half-rounds) it stashes W fragments in AGPRs and reads one
 // back right before its MFMA (a VALU write of an operand: 2 wait states); the loop body has no such
 // write (tests/test_asm_hazards.py scans for it)
+// TW_NOPMASK: which MFMA segments outside the FFN loop carry the s_nop (bit 0 phase A, bit 1 FFN1(0),
+// bit 2 the last FFN1 / FFN2 of the loop's tail, bit 3 FFN2(11)); the 32-row (G = 1) body always.
+// r6: only FFN1(0) gets a VALU write of an MFMA operand within 2 wait states without it (a scan of
+// each segment with its s_nop removed: tests/test_asm_hazards.py keeps checking the build)
+#ifndef TW_NOPMASK
+#define TW_NOPMASK 2
+#endif
 template <bool AGPR, bool NOP = true>
 __device__ __forceinline__ void tw_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
   if constexpr (AGPR && NOP)
@@ -255,9 +262,17 @@ struct TwArgs {
 template <int VAR, int G>
 __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   constexpr int D = TW_D, NT = TW_NT, GI = G > 1 ? 1 : 0;
+  // VAR bit 3: the FFN epilogue in FFN2's MFMA gaps instead of FFN1's (A/B)
+  constexpr bool EPI_FFN2 = (VAR & 8) != 0;
+  // s_nop ahead of the inline-asm MFMAs of a segment (TW_NOPMASK bit b, or the 32-row body)
+  constexpr bool NOPA = G == 1 || (TW_NOPMASK & 1), NOP0 = G == 1 || (TW_NOPMASK & 2);
+  constexpr bool NOPT = G == 1 || (TW_NOPMASK & 4), NOPF = G == 1 || (TW_NOPMASK & 8);
+  using TNA = std::integral_constant<bool, NOP0>;
+  using TNT = std::integral_constant<bool, NOPT>;
+  using TNF = std::integral_constant<bool, NOPF>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  unsigned long long st[8];
+  unsigned long long st[8] = {};
   auto stamp = [&](int i) {
     if constexpr (VAR & 1) st[i] = __builtin_amdgcn_s_memtime();
   };
@@ -359,8 +374,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        if constexpr (q == 0) tw_mfma0<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
-        else tw_mfma<true>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
+        if constexpr (q == 0) tw_mfma0<true, NOPA>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
+        else tw_mfma<true, NOPA>(acc[t][g], wf[(n0 + t) % TW_RING], bq[q & 1][g]);
       }
       if constexpr (q + 1 < TW_KS) bq[(q + 1) & 1][g] = rdB(TW_X, (q + 1) * 4 + g);
       if (g == GI)
@@ -597,10 +612,12 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   // LAST: the iteration of h = 10, whose lookahead loads FFN2(11); FINAL: FFN2(11) itself
   // EPI: with the epilogue of half-round h + 1 (whose FFN1 ran just before; parity 1 - P), one piece
   // after each of the 24 G MFMAs (unit k over gaps 3 G k .. 3 G k + 3 G - 1)
+  // (FFN1-gap schedule: b1 of half-round h + 1 loaded at step 0, for its epilogue in FFN1(h + 2))
   auto seg2 = [&](int h, auto p_tag, auto q0_tag, auto last_tag, auto final_tag, auto nop_tag, auto epi_tag) {
     constexpr int P = decltype(p_tag)::value, Q0 = decltype(q0_tag)::value;
     constexpr bool LAST = decltype(last_tag)::value, FINAL = decltype(final_tag)::value;
     constexpr bool NOP = decltype(nop_tag)::value, EPI = decltype(epi_tag)::value;
+    constexpr bool B1N = !EPI && !FINAL && !EPI_FFN2;
     constexpr uint32_t HB = TW_H + P * 32768;
     constexpr int F0 = tw_f0(Q0);
 #pragma unroll
@@ -638,6 +655,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
           }
         }
       }, std::make_integer_sequence<int, G>{});
+      if constexpr (B1N && u == 0) b1_load(h + 1);
       __builtin_amdgcn_sched_barrier(0);
     }, std::make_integer_sequence<int, 8>{});
     tw_drain_o(acc);
@@ -647,40 +665,70 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
-  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, std::true_type{},
+  seg1(0, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QA>{}, std::false_type{}, TNA{},
        std::false_type{});
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     bq[2][g] = rdB(TW_X, g);
     bq[0][g] = rdB(TW_X, 4 + g);
   }
-  // FFN1(1) with the epilogue of half-round 0 in its MFMA gaps (no FFN2 to carry it yet); then b1 of
-  // half-round 1 (after the epilogue's last read of b1v)
-  seg1(1, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_Q0>{}, std::true_type{}, std::true_type{},
-       std::false_type{});
-  b1_load(1);
-  tw_barrier();                                       // H half 0 complete
-  // steady state: FFN2(h - 1) with the epilogue of half-round h in its MFMA gaps, FFN1(h + 1) (pure
-  // MFMA + B-fragment reads), one barrier (H half h & 1 complete).  The W fragments are consumed in
-  // the same global order as [FFN1(h) FFN2(h - 1)] iterations; only the epilogue moved from FFN1's
-  // gaps (~5 VALU beside every MFMA, at the issue limit) to FFN2's, which carry no other VALU.
+  using T0 = std::false_type;
+  using T1 = std::true_type;
+  using IQR = std::integral_constant<int, TW_QREP>;
+  using IQ2 = std::integral_constant<int, TW_QREP + 24>;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  // a barrier of the FFN (stamped variants: cycles parked in the FFN's barriers into stamp slot 6)
+  auto ffn_barrier = [&]() {
+    if constexpr (VAR & 1) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      tw_barrier();
+      st[6] += __builtin_amdgcn_s_memtime() - t0;
+    } else {
+      tw_barrier();
+    }
+  };
+  if constexpr (!EPI_FFN2) {
+    // FFN1(h) with the epilogue of half-round h - 1 in its MFMA gaps (b1(h - 1) loaded at FFN2(h - 2)
+    // step 0), barrier, FFN2(h - 1)
 #pragma unroll 1
-  for (int h = 1; h < 11; h += 2) {
-    seg2(h - 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{}, std::false_type{}, std::true_type{});
-    seg1(h + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP>{}, std::false_type{},
-         std::false_type{}, std::true_type{});
-    tw_barrier();
-    seg2(h, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP + 24>{}, std::false_type{},
-         std::false_type{}, std::false_type{}, std::true_type{});
-    seg1(h + 2, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QREP>{}, std::false_type{},
-         std::false_type{}, std::true_type{});
-    tw_barrier();
+    for (int h = 1; h < 11; h += 2) {
+      seg1(h, P1{}, IQR{}, T1{}, T0{}, T0{});
+      ffn_barrier();                                  // H half (h - 1) & 1 complete
+      seg2(h - 1, P0{}, IQ2{}, T0{}, T0{}, T0{}, T0{});
+      seg1(h + 1, P0{}, IQR{}, T1{}, T0{}, T0{});
+      ffn_barrier();
+      seg2(h, P1{}, IQ2{}, T0{}, T0{}, T0{}, T0{});
+    }
+    seg1(11, P1{}, IQR{}, T1{}, TNT{}, T0{});
+    ffn_barrier();
+    seg2(10, P0{}, IQ2{}, T1{}, T0{}, TNT{}, T0{});
+    // the epilogue of half-round 11, then its FFN2
+    tw_unroll([&](auto kc) {                          // (unit by unit: a unit's pieces share ex / epk)
+      tw_unroll([&](auto pc) { epi_piece(kc, P1{}, pc); }, std::make_integer_sequence<int, TW_EP>{});
+    }, std::make_integer_sequence<int, 8>{});
+    ffn_barrier();
+  } else {
+    // FFN1(1) with the epilogue of half-round 0 in its MFMA gaps (no FFN2 to carry it yet); then b1
+    // of half-round 1 (after the epilogue's last read of b1v)
+    seg1(1, P1{}, std::integral_constant<int, TW_Q0>{}, T1{}, TNT{}, T0{});
+    b1_load(1);
+    ffn_barrier();                                    // H half 0 complete
+    // FFN2(h - 1) with the epilogue of half-round h in its MFMA gaps, FFN1(h + 1) (pure MFMA +
+    // B-fragment reads), one barrier (H half h & 1 complete): the same W consumption order
+#pragma unroll 1
+    for (int h = 1; h < 11; h += 2) {
+      seg2(h - 1, P0{}, IQ2{}, T0{}, T0{}, T0{}, T1{});
+      seg1(h + 1, P0{}, IQR{}, T0{}, T0{}, T1{});
+      ffn_barrier();
+      seg2(h, P1{}, IQ2{}, T0{}, T0{}, T0{}, T1{});
+      seg1(h + 2, P1{}, IQR{}, T0{}, T0{}, T1{});
+      ffn_barrier();
+    }
+    // FFN2(10) with the epilogue of half-round 11, then FFN2(11)
+    seg2(10, P0{}, IQ2{}, T1{}, T0{}, TNT{}, T1{});
+    ffn_barrier();
   }
-  // FFN2(10) with the epilogue of half-round 11, then FFN2(11)
-  seg2(10, std::integral_constant<int, 0>{}, std::integral_constant<int, TW_QREP + 24>{}, std::true_type{},
-       std::false_type{}, std::true_type{}, std::true_type{});
-  tw_barrier();
   // H half 0 is free from here (its last reader, FFN2(10), is behind this barrier): the LN epilogue's
   // tables [b2' | c1 | g2 | be2] (6 KiB) arrive there by LDS-DMA during FFN2(11) (retired by the
   // vmcnt(0) after it, visible after the epilogue's first barrier)
@@ -693,7 +741,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     }
   }
   seg2(11, std::integral_constant<int, 1>{}, std::integral_constant<int, TW_QF>{}, std::false_type{},
-       std::true_type{}, std::true_type{}, std::false_type{});
+       std::true_type{}, TNF{}, std::false_type{});
   float st1[4], st2[4];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -855,7 +903,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     stamp(5);
     if ((threadIdx.x & 63) == 0 && p.stamps) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) p.stamps[((long)blockIdx.x * 4 + wave) * 8 + i] = st[i];
+      for (int i = 0; i < 7; ++i) p.stamps[((long)blockIdx.x * 4 + wave) * 8 + i] = st[i];
     }
   }
 }
@@ -881,11 +929,11 @@ int tailw_launch(int M, const void* att, const void* resid, void* out, const voi
   TwArgs a{M, (const bf16*)att, (const bf16*)resid, (bf16*)out, (const char*)ws, vec, b_o, g1, be1, eps, desync,
            diag_stamps(), (int)n_full};
   // var (option tail_wide - 1): bit 0 phase stamps, bit 1 / bit 2 the W-latency / FFN1-LDS
-  // diagnostics (wrong results: tools/tailw_micro.py timing only)
+  // diagnostics (wrong results: tools/tailw_diag.py timing only; r6: W-cached no faster, no-FFN1-LDS
+  // 2 %), bit 3 the FFN epilogue in FFN2's gaps (A/B)
   if ((var & 1) && !a.stamps) var &= ~1;
-  auto kern = var == 1 ? tailw_kernel<1> : var == 2 ? tailw_kernel<2> : var == 3 ? tailw_kernel<3>
-              : var == 4 ? tailw_kernel<4> : var == 5 ? tailw_kernel<5> : var == 6 ? tailw_kernel<6>
-              : var == 7 ? tailw_kernel<7> : tailw_kernel<0>;
+  auto kern = var == 1 ? tailw_kernel<1> : var == 2 ? tailw_kernel<2> : var == 4 ? tailw_kernel<4>
+              : var == 8 ? tailw_kernel<8> : var == 9 ? tailw_kernel<9> : tailw_kernel<0>;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS));
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), TW_LDS, s, a);
   SNV_LAUNCH_CHECK();

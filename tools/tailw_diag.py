@@ -22,9 +22,9 @@ D = 384
 M = int(os.environ.get("GM_M", 512 * 1030))
 c = case(M, 1)
 ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
-VARS = {"base": (1, 64), "no-split": (1, 0)}
+VARS = {"base": (1, 64), "epi-in-FFN2": (9, 64), "no-split": (1, 0)}
 if os.environ.get("DIAG_ALL"):
-    VARS.update({"W-cached": (3, 64), "no-FFN1-LDS": (5, 64), "both": (7, 64)})
+    VARS.update({"W-cached": (3, 64), "no-FFN1-LDS": (5, 64)})
 
 
 def timeit(optv, reps=10):
@@ -74,4 +74,4 @@ for name, (opt, split) in VARS.items():
     tot = s[:, 5] - s[:, 0]
     parts = [np.median(s[:, i + 1] - s[:, i]) for i in range(5)]
     print(f"{name:12s} stamps: " + ", ".join(f"{n} {p:.0f}" for n, p in zip(names, parts)) +
-          f", total {np.median(tot):.0f} cyc", flush=True)
+          f", total {np.median(tot):.0f} cyc; in FFN barriers {np.median(s[:, 6]):.0f}", flush=True)
