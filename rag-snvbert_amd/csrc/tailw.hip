@@ -225,6 +225,16 @@ __device__ __forceinline__ void tw_ld16(uint32_t addr, float (&v)[16]) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = __uint_as_float(r[i >> 2][i & 3]);
 }
+// the same by plain LDS reads (LN phases: no LDS-DMA is in flight there, so the compiler's waits
+// count only these reads and it may issue the next tile's reads under this tile's math)
+__device__ __forceinline__ void tw_ld16p(const char* p, float (&v)[16]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(p + 16 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * i + j] = q[j];
+  }
+}
 // wait until at most Y younger vector-memory ops are in flight; the fragments' uses are ordered after it
 #ifndef TW_ASM_WAITS
 #define TW_ASM_WAITS 0                                 // 1: hand-counted waits on asm loads (diagnostics)
@@ -399,7 +409,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       float bo[16];
-      tw_ld16(tb + 4 * 32 * (3 * wave + t), bo);
+      tw_ld16p(smem + (tb - lds0) + 4 * 32 * (3 * wave + t), bo);
 #pragma unroll
       for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -423,7 +433,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       float bo[16];
-      tw_ld16(tb + 4 * 32 * (3 * wave + t), bo);
+      tw_ld16p(smem + (tb - lds0) + 4 * 32 * (3 * wave + t), bo);
 #pragma unroll
       for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -467,8 +477,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       float gg[16], bb[16];
-      tw_ld16(tb + 4 * (D + 32 * (3 * wave + t)), gg);
-      tw_ld16(tb + 4 * (2 * D + 32 * (3 * wave + t)), bb);
+      tw_ld16p(smem + (tb - lds0) + 4 * (D + 32 * (3 * wave + t)), gg);
+      tw_ld16p(smem + (tb - lds0) + 4 * (2 * D + 32 * (3 * wave + t)), bb);
       const int T = 3 * wave + t;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -792,8 +802,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     for (int t = 0; t < 3; ++t) {
       const int T = 3 * wave + t;
       float b2[16], c1[16];
-      tw_ld16(eb + 4 * (32 * T), b2);
-      tw_ld16(eb + 4 * (D + 32 * T), c1);
+      tw_ld16p(smem + (eb - lds0) + 4 * (32 * T), b2);
+      tw_ld16p(smem + (eb - lds0) + 4 * (D + 32 * T), c1);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const u32x4 xa = rdB(TW_X, (2 * T) * 4 + g), xb = rdB(TW_X, (2 * T + 1) * 4 + g);
@@ -822,8 +832,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     for (int t = 0; t < 3; ++t) {
       const int T = 3 * wave + t;
       float b2[16], c1[16];
-      tw_ld16(eb + 4 * (32 * T), b2);
-      tw_ld16(eb + 4 * (D + 32 * T), c1);
+      tw_ld16p(smem + (eb - lds0) + 4 * (32 * T), b2);
+      tw_ld16p(smem + (eb - lds0) + 4 * (D + 32 * T), c1);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const u32x4 xa = rdB(TW_X, (2 * T) * 4 + g), xb = rdB(TW_X, (2 * T + 1) * 4 + g);
@@ -871,8 +881,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
     for (int t = 0; t < 3; ++t) {
       const int T = 3 * wave + t;
       float g2[16], be2[16];
-      tw_ld16(eb + 4 * (2 * D + 32 * T), g2);
-      tw_ld16(eb + 4 * (3 * D + 32 * T), be2);
+      tw_ld16p(smem + (eb - lds0) + 4 * (2 * D + 32 * T), g2);
+      tw_ld16p(smem + (eb - lds0) + 4 * (3 * D + 32 * T), be2);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const long r = row0 + 32 * g + (l & 31);
