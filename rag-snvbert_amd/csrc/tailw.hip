@@ -274,6 +274,10 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   constexpr int D = TW_D, NT = TW_NT, GI = G > 1 ? 1 : 0;
   // VAR bit 3: the FFN epilogue in FFN2's MFMA gaps instead of FFN1's (A/B)
   constexpr bool EPI_FFN2 = (VAR & 8) != 0;
+  // the residual rows loaded during phase A (after step TW_RES_STEP's W loads: the prologue's HBM
+  // burst halves, -2 k cycles per wave net, r6 tools/tailw_diag.py); VAR bit 4: in the prologue (A/B)
+  constexpr bool LATE_RES = (VAR & 16) == 0;
+  constexpr int TW_RES_STEP = 21;
   // s_nop ahead of the inline-asm MFMAs of a segment (TW_NOPMASK bit b, or the 32-row body)
   constexpr bool NOPA = G == 1 || (TW_NOPMASK & 1), NOP0 = G == 1 || (TW_NOPMASK & 2);
   constexpr bool NOPT = G == 1 || (TW_NOPMASK & 4), NOPF = G == 1 || (TW_NOPMASK & 8);
@@ -337,7 +341,9 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   };
   tw_unroll([&](auto nc) { issue_a(nc); }, std::make_integer_sequence<int, TW_AH>{});
   u32x4 rr[3][4][2];                                 // residual x: tile t, group g, half h2
-  {
+  // (LATE_RES: issued after phase A step TW_RES_STEP's W loads instead of here — the prologue's HBM
+  // burst halves; the W waits after it then also wait for these rows, in-order vmcnt)
+  auto load_res = [&]() {
     const int l = tw_lane();
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -349,7 +355,8 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
         for (int h2 = 0; h2 < 2; ++h2)
           rr[t][g][h2] = *reinterpret_cast<const u32x4*>(p.resid + r * D + 32 * (3 * wave + t) + 16 * (l >> 5) + 8 * h2);
     }
-  }
+  };
+  if constexpr (!LATE_RES) load_res();
   float* tab = reinterpret_cast<float*>(smem + TW_H);                        // [b_o | g1 | be1]
   for (int i = threadIdx.x; i < D; i += 256) {
     tab[i] = p.b_o[i];
@@ -359,10 +366,12 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // the residual rows retired here (else the compiler's wait for them lands at LN1, behind the
   // in-flight W loads of the first FFN steps)
+  if constexpr (!LATE_RES) {
 #pragma unroll
-  for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int g = 0; g < G; ++g) asm volatile("" : "+v"(rr[t][g][0]), "+v"(rr[t][g][1]));
+      for (int g = 0; g < G; ++g) asm volatile("" : "+v"(rr[t][g][0]), "+v"(rr[t][g][1]));
+  }
   tw_barrier();
   stamp(1);
 
@@ -392,6 +401,7 @@ __device__ __forceinline__ void tailw_body(const TwArgs& p, const long row0) {
         tw_unroll([&](auto tc) { issue_a(std::integral_constant<int, n0 + TW_AH + decltype(tc)::value>{}); },
                   std::make_integer_sequence<int, 3>{});
     }
+    if constexpr (LATE_RES && q == TW_RES_STEP) load_res();
     __builtin_amdgcn_sched_barrier(0);
   }, std::make_integer_sequence<int, TW_QA>{});
   tw_drain_o(acc);
@@ -943,7 +953,8 @@ int tailw_launch(int M, const void* att, const void* resid, void* out, const voi
   // 2 %), bit 3 the FFN epilogue in FFN2's gaps (A/B)
   if ((var & 1) && !a.stamps) var &= ~1;
   auto kern = var == 1 ? tailw_kernel<1> : var == 2 ? tailw_kernel<2> : var == 4 ? tailw_kernel<4>
-              : var == 8 ? tailw_kernel<8> : var == 9 ? tailw_kernel<9> : tailw_kernel<0>;
+              : var == 8 ? tailw_kernel<8> : var == 9 ? tailw_kernel<9> : var == 16 ? tailw_kernel<16>
+              : var == 17 ? tailw_kernel<17> : tailw_kernel<0>;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TW_LDS));
   hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), TW_LDS, s, a);
   SNV_LAUNCH_CHECK();

@@ -149,7 +149,7 @@ def test_wide_tail_no_valu_write_before_mfma_operand(tmp_path):
                    capture_output=True)
     text = out.read_text().split("\n")
     for name in ("_ZN6snvrag12tailw_kernelILi0EEEvNS_6TwArgsE:", "_ZN6snvrag12tailw_kernelILi1EEEvNS_6TwArgsE:",
-                 "_ZN6snvrag12tailw_kernelILi8EEEvNS_6TwArgsE:",
+                 "_ZN6snvrag12tailw_kernelILi8EEEvNS_6TwArgsE:", "_ZN6snvrag12tailw_kernelILi16EEEvNS_6TwArgsE:",
                  "_ZN6snvrag12projw_kernelENS_6PwArgsE:"):
         i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
         i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))

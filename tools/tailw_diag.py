@@ -22,7 +22,7 @@ D = 384
 M = int(os.environ.get("GM_M", 512 * 1030))
 c = case(M, 1)
 ts = K.tail_pack(c["w_o"], c["w1"], c["w2g"])
-VARS = {"base": (1, 64), "epi-in-FFN2": (9, 64), "no-split": (1, 0)}
+VARS = {"base": (1, 64), "early-resid": (17, 64), "no-split": (1, 0)}
 if os.environ.get("DIAG_ALL"):
     VARS.update({"W-cached": (3, 64), "no-FFN1-LDS": (5, 64)})
 
@@ -47,6 +47,18 @@ def timeit(optv, reps=10):
 
 for _ in range(20):
     timeit((1, 64), 1)
+# correctness of the A/B arms (same arithmetic: bitwise equal outputs)
+outs = {}
+for name, (opt, split) in VARS.items():
+    xs = c["x"].clone()
+    K.set_option("tail_split", split)
+    K.set_option("tail_wide", opt)
+    K.tail_forward(c["att"], xs, ts, c["b_o"], c["g1"], c["be1"], c["vec"])
+    outs[name] = xs
+K.set_option("tail_wide", 1)
+K.set_option("tail_split", 64)
+print("bitwise equal to base: " + ", ".join(f"{n} {bool(torch.equal(o, outs['base']))}" for n, o in outs.items()),
+      flush=True)
 res = {k: [] for k in VARS}
 for it in range(4):
     for name, opt in VARS.items():
