@@ -407,6 +407,16 @@ size_t snvrag_gemm256_pack_bytes(int N, int K);
 int snvrag_gemm256_pack(int N, int K, const void* w, int64_t ldw, void* out, void* stream);
 int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, int64_t lda, const void* wpacked, const float* bias,
                            const void* resid, int64_t ld_resid, void* out, int64_t ldo, void* stream);
+/* The same GEMM with the rag fusion's tail as its epilogue (fusion.py:152-162: fusion[3] Linear(4D, D)
+ * -> fusion[4] LayerNorm -> MAF weighting -> residual, replacing the row-panel GEMM's LN/post epilogue
+ * of snvrag_linear for this call): y = A W^T + bias (f32); v = LN(y) * ln_g + ln_b over the N = 384
+ * outputs of a row (two-pass mean / variance, eps); out = base + post_scale * v * w(af[m % period])
+ * with w(a) = min(log1p(1 / (min(a, 1 - a) + 1e-6)), 3) (post_af null: w = 1; base null: out = v).
+ * Inference / eval only (no saved statistics). */
+int snvrag_gemm256_ln_forward(int64_t M, int N, int K, const void* A, int64_t lda, const void* wpacked,
+                              const float* bias, const float* ln_g, const float* ln_b, float eps, const void* base,
+                              int64_t ld_base, float post_scale, const float* post_af, int64_t post_af_period,
+                              void* out, int64_t ldo, void* stream);
 
 /* The hap head's Linear(K, 2) (foundation_model.py:25-33 net[2]) in training: x bf16 [M, K],
  * w f32 [2, K], b f32 [2] -> out f32 [M, 2] = x w^T + b.  Backward: dx bf16 [M, K] = g w (optional),

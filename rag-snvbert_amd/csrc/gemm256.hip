@@ -84,7 +84,22 @@ struct G2Args {
   bf16* out;                 // [M, N] (ldo)
   long ldo;
   unsigned long long* stamps;  // VAR 3 (diagnostics): [workgroup][wave][8] s_memtime stamps
+  // EPI 1 (g3 only): row LayerNorm over the N outputs, then out = base + post_scale * LN(y) * w(af):
+  // fusion.py:152-162 (the rag fusion's Linear(4D, D) -> LayerNorm, MAF weighting, residual)
+  const float* ln_g;
+  const float* ln_b;
+  float ln_eps;
+  const bf16* base;          // [M, N] (ld_base) or null
+  long ld_base;
+  float post_scale;
+  const float* post_af;      // [period] or null: w = min(log1p(1 / (min(af, 1 - af) + 1e-6)), 3)
+  long post_af_period;
 };
+
+__device__ __forceinline__ float g2_maf_w(float af) {   // fusion.py:155-160
+  const float maf = fminf(af, 1.0f - af);
+  return fminf(log1pf(1.0f / (maf + 1e-6f)), 3.0f);
+}
 
 template <int NT, int VAR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -330,7 +345,7 @@ constexpr int G3_PF = 3;                              // B-fragment reads ahead
 __host__ __device__ constexpr int g3_img(int G) { return 32 * G * 128; }   // one A image: 32 G rows x 128 B
 __host__ __device__ constexpr int g3_pieces_in_phase(int G, int s) { return G / 4 + (s < G % 4 ? 1 : 0); }
 
-template <int G, int VAR>
+template <int G, int VAR, int EPI = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void g3_kernel(G2Args p) {
   constexpr int N = 384, TW = 3, G3_IMG = g3_img(G);
@@ -348,6 +363,11 @@ void g3_kernel(G2Args p) {
   stamp(1, __builtin_amdgcn_s_memrealtime());
   const long row0 = (long)blockIdx.x * (32 * G);
   for (int i = threadIdx.x; i < N; i += 256) sb[i] = p.bias ? p.bias[i] : 0.f;
+  if constexpr (EPI == 1)
+    for (int i = threadIdx.x; i < N; i += 256) {
+      sb[N + i] = p.ln_g[i];
+      sb[2 * N + i] = p.ln_b[i];
+    }
 
   const i32x4 ars = dma_rsrc(p.A + row0 * p.lda, ((long)M - row0) * p.lda * 2);   // rows >= M read as 0
   const i32x4 wrs = dma_rsrc(p.ws, (long)nk * 4 * 12 * G2_FRAG);
@@ -444,18 +464,136 @@ void g3_kernel(G2Args p) {
     slot_wr = slot_wr + G3_IMG == G3_NS * G3_IMG ? 0 : slot_wr + G3_IMG;
     // the last K-step's MFMA results: the drain sits INSIDE the loop body, so that the register
     // moves the compiler places on the loop exit (re-homing accumulators for the epilogue) come
-    // after it — after the loop they were seen reading an AGPR before its last MFMA had written it
-    if (k == nk - 1) g2_drain();
+    // after it — after the loop they were seen reading an AGPR before its last MFMA had written it.
+    // Likewise the last K-step's overrun W loads (asm: the compiler takes their registers as written
+    // at issue and dead after the loop): they must land before the loop exit, whose moves were seen
+    // reusing a W register (v_accvgpr_read into v[120:121] while its buffer_load was in flight —
+    // a rare wrong accumulator, tests/test_gpu_kernels.py in-place check)
+    if (k == nk - 1) {
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[0][2]), "+v"(w[1][0]), "+v"(w[1][1]), "+v"(w[1][2]),
+                     "+v"(w[2][0]), "+v"(w[2][1]), "+v"(w[2][2]), "+v"(w[3][0]), "+v"(w[3][1]), "+v"(w[3][2])
+                   :: "memory");
+      g2_drain();
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the overrun loads have landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the A overrun DMA has landed
   stamp(3, __builtin_amdgcn_s_memtime());
   stamp(6, st_wait);
 
-  // ---- epilogue: + bias (+ resid) -> bf16, two 16-B stores per (token group, feature tile)
   const long rows_left = (long)M - row0;
   const long o_bytes = rows_left * p.ldo * 2;
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.out + row0 * p.ldo), (short)0, (int)(o_bytes < 0x7fffffffL ? o_bytes : 0x7fffffffL), 0x00020000);
+  if constexpr (EPI == 1) {
+    // ---- epilogue: y = acc + bias; two-pass row LayerNorm over the 384 outputs (a row's features
+    // are spread over the 4 waves: per-wave partial sums through LDS, summed in wave order); then
+    // out = base + post_scale * (LN(y) g + be) * w(af[row % period]) -> bf16
+    float* red = sb + 3 * N;                          // [4 waves][G][32]
+    const int n = g2_lane() & 31, hh = g2_lane() >> 5;
+    auto tile_vec = [&](const float* tab, int t, u32x4 (&v)[4]) {
+      const uint32_t ba = lds_addr(tab) + 4 * (96 * wave + 32 * t + 16 * hh);
+      asm volatile(
+          "ds_read_b128 %0, %4 offset:0\n ds_read_b128 %1, %4 offset:16\n ds_read_b128 %2, %4 offset:32\n"
+          " ds_read_b128 %3, %4 offset:48\n s_waitcnt lgkmcnt(0)"
+          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+          : "v"(ba));
+    };
+    // sum over the workgroup's 4 waves of the per-(wave, group, row) partials s[g]
+    auto row_sum = [&](float (&s)[G]) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        s[g] += __shfl_xor(s[g], 32, 64);
+        if (hh == 0) red[(wave * G + g) * 32 + n] = s[g];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        s[g] = ((red[g * 32 + n] + red[(G + g) * 32 + n]) + red[(2 * G + g) * 32 + n]) + red[(3 * G + g) * 32 + n];
+      __syncthreads();                                // red is rewritten by the next pass
+    };
+    float mean[G], rstd[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) mean[g] = 0.f;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      u32x4 bv[4];
+      tile_vec(sb, t, bv);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mean[g] += acc[g][t][i] + __uint_as_float(bv[i >> 2][i & 3]);
+    }
+    row_sum(mean);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      mean[g] *= 1.0f / N;
+      rstd[g] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      u32x4 bv[4];
+      tile_vec(sb, t, bv);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float d = acc[g][t][i] + __uint_as_float(bv[i >> 2][i & 3]) - mean[g];
+          rstd[g] = fmaf(d, d, rstd[g]);
+        }
+    }
+    row_sum(rstd);
+    float w[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      rstd[g] = 1.0f / sqrtf(rstd[g] * (1.0f / N) + p.ln_eps);
+      long m = row0 + 32 * g + n;
+      m = m < M ? m : M - 1;
+      w[g] = p.post_af ? g2_maf_w(p.post_af[p.post_af_period > 0 ? m % p.post_af_period : m]) : 1.0f;
+    }
+    const long b_bytes = p.base ? rows_left * p.ld_base * 2 : 0;
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.base ? p.base + row0 * p.ld_base : p.out), (short)0,
+        (int)(b_bytes < 0x7fffffffL ? b_bytes : 0x7fffffffL), 0x00020000);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int f0 = 96 * wave + 32 * t + 16 * hh;
+      u32x4 bv[4], gv[4], ev[4];
+      tile_vec(sb, t, bv);
+      tile_vec(sb + N, t, gv);
+      tile_vec(sb + 2 * N, t, ev);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int rl = 32 * g + n;
+        float y[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          y[i] = fmaf((acc[g][t][i] + __uint_as_float(bv[i >> 2][i & 3]) - mean[g]) * rstd[g],
+                      __uint_as_float(gv[i >> 2][i & 3]), __uint_as_float(ev[i >> 2][i & 3]));
+        if (p.base) {
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(brs, (int)(rl * p.ld_base + f0 + 8 * h2) * 2, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              y[8 * h2 + 2 * e] = __uint_as_float(r[e] << 16) + p.post_scale * (y[8 * h2 + 2 * e] * w[g]);
+              y[8 * h2 + 2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u) + p.post_scale * (y[8 * h2 + 2 * e + 1] * w[g]);
+            }
+          }
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{g2_pack2(y[8 * h2], y[8 * h2 + 1]), g2_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
+                    g2_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), g2_pack2(y[8 * h2 + 6], y[8 * h2 + 7])},
+              ors, (int)(rl * p.ldo + f0 + 8 * h2) * 2, 0, 0);
+      }
+    }
+    stamp(4, __builtin_amdgcn_s_memtime());
+    stamp(5, __builtin_amdgcn_s_memrealtime());
+    return;
+  }
+  // ---- epilogue: + bias (+ resid) -> bf16, two 16-B stores per (token group, feature tile)
   const long r_bytes = p.resid ? rows_left * p.ld_resid * 2 : 0;
   const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.resid ? p.resid + row0 * p.ld_resid : p.out), (short)0,
@@ -500,10 +638,11 @@ void g3_kernel(G2Args p) {
   stamp(5, __builtin_amdgcn_s_memrealtime());
 }
 
-template <int G, int VAR>
+template <int G, int VAR, int EPI = 0>
 static int g3_launch(const G2Args& a, hipStream_t s) {
-  auto kern = g3_kernel<G, VAR>;
-  constexpr size_t lds = (size_t)G3_NS * g3_img(G) + 384 * 4;
+  auto kern = g3_kernel<G, VAR, EPI>;
+  // + bias table (+ EPI 1: LN g, be tables and the [4][G][32] row-sum exchange)
+  constexpr size_t lds = (size_t)G3_NS * g3_img(G) + 384 * 4 + (EPI == 1 ? 2 * 384 * 4 + 4 * G * 32 * 4 : 0);
   static_assert(lds <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 32 * G)), dim3(256), lds, s, a);
@@ -511,15 +650,38 @@ static int g3_launch(const G2Args& a, hipStream_t s) {
   return 0;
 }
 
-template <int VAR>
+template <int VAR, int EPI = 0>
 static int g3_dispatch(int G, const G2Args& a, hipStream_t s) {
   switch (G) {
-    case 4: return g3_launch<4, VAR>(a, s);
-    case 5: return g3_launch<5, VAR>(a, s);
-    case 6: return g3_launch<6, VAR>(a, s);
-    case 7: return g3_launch<7, VAR>(a, s);
-    default: return g3_launch<8, VAR>(a, s);
+    case 4: return g3_launch<4, VAR, EPI>(a, s);
+    case 5: return g3_launch<5, VAR, EPI>(a, s);
+    case 6: return g3_launch<6, VAR, EPI>(a, s);
+    case 7: return g3_launch<7, VAR, EPI>(a, s);
+    default: return g3_launch<8, VAR, EPI>(a, s);
   }
+}
+
+// token groups per workgroup: the fewest rows that still fit one round of the CUs (4 .. 8 groups
+// of 32); past one round of 8-group workgroups, the G whose rounds x (G + 1) (a workgroup's time
+// ~ G plus a fixed prologue / epilogue share) is least; option g2_groups overrides
+static int g3_groups(long M) {
+  static int n_cu = 0;
+  if (n_cu <= 0) {
+    int dev = 0, v = 0;
+    n_cu = hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0
+               ? v : 256;
+  }
+  int G = (int)std::min<long>(8, std::max<long>(4, (M + 32L * n_cu - 1) / (32L * n_cu)));
+  if (M > 8L * 32 * n_cu) {
+    long best = -1;
+    for (int g = 8; g >= 4; --g) {
+      const long rounds = (cdiv(M, 32L * g) + n_cu - 1) / n_cu, cost = rounds * (g + 1);
+      if (best < 0 || cost < best) best = cost, G = g;
+    }
+  }
+  if (options().g2_groups >= 4 && options().g2_groups <= 8) G = (int)options().g2_groups;
+  return G;
 }
 
 // One thread per 16-byte piece: fragment F = k16 NT + T, lane l = (m = l % 32, kh = l / 32) holds
@@ -587,17 +749,7 @@ extern "C" int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, in
   const int64_t var = options().g2_variant;
   G2Args b = a;
   b.stamps = diag_stamps();
-  // token groups per workgroup: the fewest rows that still fit one round of the CUs (4 .. 8
-  // groups of 32; option g2_groups overrides)
-  static int n_cu = 0;
-  if (n_cu <= 0) {
-    int dev = 0, v = 0;
-    n_cu = hipGetDevice(&dev) == hipSuccess &&
-                   hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0
-               ? v : 256;
-  }
-  int G = (int)std::min<long>(8, std::max<long>(4, (M + 32L * n_cu - 1) / (32L * n_cu)));
-  if (options().g2_groups >= 4 && options().g2_groups <= 8) G = (int)options().g2_groups;
+  const int G = g3_groups(M);
   // g2_variant: 0 v2 (default); 1 / 2 / 3: v2 without A loads / without MFMA / with stamps;
   // 4: v1 (W through LDS); 5 / 6 / 7: v1 without loads / without MFMA / with stamps
   int rc;
@@ -611,6 +763,41 @@ extern "C" int snvrag_gemm256_forward(int64_t M, int N, int K, const void* A, in
     case 7: rc = b.stamps ? g2_launch<12, 3>(b, s) : g2_launch<12, 0>(a, s); break;
     default: rc = g3_dispatch<0>(G, a, s);
   }
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)N * K);
+  return 0;
+}
+
+extern "C" int snvrag_gemm256_ln_forward(int64_t M, int N, int K, const void* A, int64_t lda, const void* wpacked,
+                                         const float* bias, const float* ln_g, const float* ln_b, float eps,
+                                         const void* base, int64_t ld_base, float post_scale, const float* post_af,
+                                         int64_t post_af_period, void* out, int64_t ldo, void* stream) {
+  SNV_CHECK_ARG(N == 384, "gemm256: N = 384");
+  SNV_CHECK_ARG(K >= 64 && K % 64 == 0, "gemm256: K % 64 == 0");
+  SNV_CHECK_ARG(A && wpacked && out && ln_g && ln_b, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && lda >= K && ldo >= N && (!base || ld_base >= N), "bad shape / leading dims");
+  SNV_CHECK_ARG(post_af_period >= 0, "bad af period");
+  SNV_CHECK_ARG(lda % 8 == 0 && ldo % 8 == 0 && (!base || ld_base % 8 == 0), "16-byte rows");
+  SNV_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)wpacked % 16) == 0 &&
+                    ((uintptr_t)base % 16) == 0,
+                "16-byte aligned operands");
+  SNV_CHECK_ARG(257L * lda * 2 < (1L << 31) && 257L * ldo * 2 < (1L << 31) &&
+                    (!base || 257L * ld_base * 2 < (1L << 31)),
+                "row offsets must fit 31 bits");
+  if (M == 0) return 0;
+  G2Args a{(int)M, K, (const bf16*)A, (long)lda, (const char*)wpacked, bias, nullptr, 0, (bf16*)out, (long)ldo,
+           nullptr};
+  a.ln_g = ln_g;
+  a.ln_b = ln_b;
+  a.ln_eps = eps;
+  a.base = (const bf16*)base;
+  a.ld_base = (long)ld_base;
+  a.post_scale = post_scale;
+  a.post_af = post_af;
+  a.post_af_period = (long)post_af_period;
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  const int rc = g3_dispatch<0, 1>(g3_groups(M), a, s);
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)N * K);
   return 0;

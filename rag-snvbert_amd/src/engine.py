@@ -61,6 +61,10 @@ class _Packed:
 
 
 class Engine:
+    # bf16 at D = 384: the rag fusion's fusion[3] -> LN -> MAF tail on the wide-row GEMM (gemm256
+    # EPI 1) instead of the row-panel GEMM's LN epilogue (class-level A/B switch; repack on change)
+    rag_tail_wide = True
+
     def __init__(self, root: nn.Module):
         self.root = root
         self.dtype = torch.float32
@@ -175,6 +179,9 @@ class Engine:
                     rs=float(rf.res_scale.detach().float().item()))
         if sg_ok and D == 384 and P.rf["f0"].shape == (4 * D, 2 * D):
             P.rf["f0_sg"], P.rf["f0_v"] = K.sgemm_pack(P.rf["f0"]), K.sgemm_vec(P.rf["f0b"])
+        if sg_ok and D == 384 and P.rf["f3"].shape == (D, 4 * D) and self.rag_tail_wide:
+            # fusion[3] + LayerNorm + MAF weighting + residual on the wide-row GEMM (csrc/gemm256.hip EPI 1)
+            P.rf["f3_g2"] = K.gemm256_pack(P.rf["f3"])
         mlp_ok = sg_ok and D == 384
         if mlp_ok and P.rf["a0"].shape == (4 * D, D) and P.rf["a3"].shape == (D, 4 * D):
             # af_adapter: Linear -> GELU -> Linear -> Sigmoid in one launch, hidden on chip
@@ -345,8 +352,13 @@ class Engine:
             else:
                 cat = K.rag_concat(fused[:2 * B], fused[2 * B:], aw, BL)   # [2B, L, 2D]
                 h = K.linear(cat, rf["f0"], rf["f0b"], act=N.ACT_GELU)
-            xx = K.linear(h, rf["f3"], rf["f3b"], ln=(rf["g"], rf["bb"]), post_base=fused[:2 * B],
-                          post_scale=rf["rs"], post_af=af, post_af_period=BL, post_maf=True)
+            if "f3_g2" in rf:
+                xx = K.gemm256_ln(h.view(-1, h.shape[-1]), rf["f3_g2"], rf["f3b"], (rf["g"], rf["bb"]),
+                                  base=fused[:2 * B].view(-1, D), post_scale=rf["rs"], post_af=af.view(-1),
+                                  post_af_period=BL).view(2 * B, L, D)
+            else:
+                xx = K.linear(h, rf["f3"], rf["f3b"], ln=(rf["g"], rf["bb"]), post_base=fused[:2 * B],
+                              post_scale=rf["rs"], post_af=af, post_af_period=BL, post_maf=True)
         else:
             xx = fused[:2 * B].clone()
         ws_bytes = K.encoder_ws_bytes(T, 2 * B, L, D, P.heads)

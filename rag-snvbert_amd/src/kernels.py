@@ -787,6 +787,37 @@ def gemm256(a: torch.Tensor, wpacked: torch.Tensor, n_out: int, bias: Optional[t
     return out
 
 
+def gemm256_ln(a: torch.Tensor, wpacked: torch.Tensor, bias: Optional[torch.Tensor], ln: Tuple[torch.Tensor, torch.Tensor],
+               base: Optional[torch.Tensor] = None, post_scale: float = 1.0, post_af: Optional[torch.Tensor] = None,
+               post_af_period: int = 0, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 [M, 384] = base + post_scale * LN(a W^T + bias) * w(post_af[m % period]) on the wide-row
+    GEMM (csrc/gemm256.hip EPI 1): the rag fusion's fusion[3] -> fusion[4] -> MAF -> residual
+    (fusion.py:152-162), the same arithmetic as :func:`linear` with ``ln=``, ``post_base=``,
+    ``post_maf=True``."""
+    N.require_gpu(a)
+    assert a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(1) == 1
+    M, Kk = a.shape
+    n_out = 384
+    assert wpacked.numel() * wpacked.element_size() == int(N.lib().snvrag_gemm256_pack_bytes(n_out, Kk))
+    if out is None:
+        out = torch.empty(M, n_out, device=a.device, dtype=torch.bfloat16)
+    assert out.dtype == torch.bfloat16 and out.shape == (M, n_out) and out.stride(1) == 1
+    for t in (bias, ln[0], ln[1]) if bias is not None else ln:
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n_out
+    if base is not None:
+        assert base.dtype == torch.bfloat16 and base.shape == (M, n_out) and base.stride(1) == 1
+    if post_af is not None:
+        assert post_af.dtype == torch.float32 and post_af.is_contiguous()
+        assert post_af.numel() >= (post_af_period if post_af_period > 0 else M)
+    check(N.lib().snvrag_gemm256_ln_forward(M, n_out, Kk, ptr(a), a.stride(0), ptr(wpacked),
+                                            ptr(bias) if bias is not None else None, ptr(ln[0]), ptr(ln[1]), eps,
+                                            ptr(base) if base is not None else None,
+                                            base.stride(0) if base is not None else 0, post_scale,
+                                            ptr(post_af) if post_af is not None else None, post_af_period,
+                                            ptr(out), out.stride(0), stream_ptr()), "gemm256_ln")
+    return out
+
+
 DERIVE_F32, DERIVE_BF16, DERIVE_SGPACK, DERIVE_G2PACK = 0, 1, 2, 3
 
 

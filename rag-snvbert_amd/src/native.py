@@ -157,6 +157,8 @@ _SIGS = {
     "snvrag_gemm256_pack_bytes": ([C.c_int, C.c_int], sz),
     "snvrag_gemm256_pack": ([C.c_int, C.c_int, vp, i64, vp, vp], C.c_int),
     "snvrag_gemm256_forward": ([i64, C.c_int, C.c_int, vp, i64, vp, vp, vp, i64, vp, i64, vp], C.c_int),
+    "snvrag_gemm256_ln_forward": ([i64, C.c_int, C.c_int, vp, i64, vp, vp, vp, vp, C.c_float, vp, i64, C.c_float,
+                                   vp, i64, vp, i64, vp], C.c_int),
     "snvrag_head2_fwd": ([i64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
     "snvrag_head2_ws_bytes": ([i64, C.c_int], sz),
     "snvrag_tokgrad_ws_bytes": ([i64, C.c_int, C.c_int], sz),

@@ -157,3 +157,53 @@ def test_wide_tail_no_valu_write_before_mfma_operand(tmp_path):
         ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
         bad = _valu_to_mfma(ins)
         assert not bad, (name, bad[:5])
+
+
+def _pending_writes(ins):
+    """Writes to a register whose inline-asm vector-memory load has not been retired by an
+    s_waitcnt vmcnt yet (the waits counted in issue order): the load lands later and overwrites
+    the new value.  The compiler takes an asm load's destination as written at issue, so once the
+    loaded value is dead (the K loop's last overrun loads) it may reuse the register at once."""
+    pending, bad = [], []
+    for i, t in enumerate(ins):
+        op = t.split(" ")[0]
+        m = re.match(r"s_waitcnt.*vmcnt\((\d+)\)", t)
+        if m:
+            n = int(m.group(1))
+            pending = pending[len(pending) - n:] if len(pending) > n else pending
+            continue
+        if op.startswith(("buffer_load", "global_load", "scratch_load")):
+            pending.append(set() if " lds" in t else _regs(t.split(None, 1)[1].split(",")[0].strip()))
+            continue
+        if op.startswith(("buffer_store", "global_store", "scratch_store")):
+            pending.append(set())
+            continue
+        if " " in t and (op.startswith(("v_", "ds_read")) and not op.startswith("v_accvgpr_write")):
+            dst = _regs(t.split(None, 1)[1].split(",")[0].strip())
+            if any(d & dst for d in pending):
+                bad.append((i, t))
+    return bad
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_gemm256_no_write_or_read_before_asm_load_lands(tmp_path):
+    """csrc/gemm256.hip (the v2 kernel, every token-group count, plain and LayerNorm epilogues): from
+    the K loop on (after the prologue's barrier), no instruction reads a register still waiting for
+    its inline-asm W load, and none writes one — the r6 fault: the loop exit re-homed an accumulator
+    into v[120:121] while the last K-step's overrun W load into v[120:123] was in flight."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    out = tmp_path / "g.s"
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
+                    os.path.join(CSRC, "gemm256.hip"), "-o", str(out)], check=True, capture_output=True)
+    text = out.read_text().split("\n")
+    names = [f"_ZN6snvrag9g3_kernelILi{g}ELi0ELi{e}EEEvNS_6G2ArgsE:" for g in range(4, 9) for e in (0, 1)]
+    for name in names:
+        i0 = next(i for i, ln in enumerate(text) if ln.startswith(name))
+        i1 = next(i for i in range(i0, len(text)) if text[i].strip().startswith(".Lfunc_end"))
+        ins = [ln.strip() for ln in text[i0:i1]]
+        ins = [ln for ln in ins if ln and not ln.startswith((";", ".", "_")) and not ln.endswith(":")]
+        ins = ins[next(i for i, t in enumerate(ins) if t.startswith("s_barrier")):]
+        assert sum(t.startswith("v_mfma") for t in ins) >= 48
+        bad = _pending_writes(ins) + _pending_reads(ins)
+        assert not bad, (name, bad[:5])
+

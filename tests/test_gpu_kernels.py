@@ -694,6 +694,44 @@ def test_gemm256_vs_fp32(M, Kd, lda_pad, bias, res):
         assert torch.equal(r2, out)
 
 
+@pytest.mark.parametrize("M,base,af_period", [(777, True, 259), (1, True, 0), (70001, True, 35000),
+                                              (513, False, 0)])
+def test_gemm256_ln_vs_fp32(M, base, af_period):
+    """snvrag_gemm256_ln_forward (gemm256 EPI 1: the rag fusion's fusion[3] -> LayerNorm -> MAF
+    weighting -> residual, fusion.py:152-162) vs torch fp32 on the same bf16 operands: two-pass row
+    LayerNorm across the 4 waves' feature slices, base + scale * LN * w(af[m % period]); ragged M
+    (M = 70 001 takes the multi-round workgroup-height choice).  Every workgroup height gives the
+    same bits (the row sums are combined in wave order whatever the height)."""
+    kk = K()
+    g = torch.Generator(device="cpu").manual_seed(M + 11)
+    Kd = 1536
+    a = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(384, Kd, generator=g) / math.sqrt(Kd)).to(DEV, torch.bfloat16)
+    b = torch.randn(384, generator=g).to(DEV)
+    gm, be = (1 + 0.2 * torch.randn(384, generator=g)).to(DEV), (0.1 * torch.randn(384, generator=g)).to(DEV)
+    bs = torch.randn(M, 384, generator=g).to(DEV, torch.bfloat16) if base else None
+    af = torch.rand(af_period if af_period else M, generator=g).to(DEV)
+    af[:3] = torch.tensor([0.0, 1.0, 0.5])[:af.numel()]                     # the clamp, both MAF branches
+    wp = kk.gemm256_pack(w)
+    out = kk.gemm256_ln(a, wp, b, (gm, be), base=bs, post_scale=0.37, post_af=af, post_af_period=af_period)
+    y = torch.nn.functional.layer_norm(a.float() @ w.float().t() + b, (384,), gm, be, 1e-5)
+    ai = af[torch.arange(M, device=DEV) % af.numel()]
+    mw = torch.log1p(1.0 / (torch.minimum(ai, 1 - ai) + 1e-6)).clamp(max=3.0)
+    # (no base: the LayerNorm output alone, as the row-panel GEMM's post epilogue)
+    ref = bs.float() + 0.37 * y * mw[:, None] if bs is not None else y
+    tol = _bf16_step(ref) + 1e-3 * (1 + ref.abs())
+    bad = (out.float() - ref).abs() > tol
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} of {bad.numel()} outside tolerance, first at " \
+                                f"{bad.nonzero()[:4].tolist()}"
+    try:
+        for groups in (4, 8):
+            kk.set_option("g2_groups", groups)
+            y2 = kk.gemm256_ln(a, wp, b, (gm, be), base=bs, post_scale=0.37, post_af=af, post_af_period=af_period)
+            assert torch.equal(y2, out), groups
+    finally:
+        kk.set_option("g2_groups", 0)
+
+
 def test_gemm256_derive_pack_matches_pack():
     """snvrag_derive kind 3 from f32 masters (plain, two stacked parts, and the transposed view a
     dX GEMM packs) == snvrag_gemm256_pack of the bf16-rounded matrix, byte for byte."""
