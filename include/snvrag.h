@@ -373,6 +373,18 @@ size_t snvrag_mlp_pack_bytes(int D);
 int snvrag_mlp_pack(int D, const void* w1, const void* w2, void* out, void* stream);
 int snvrag_mlp_forward(int64_t M, int D, int epi2, const void* x, const void* wstream, const float* vec,
                        const float* r1, const float* r2, int64_t period, float eps, void* out, void* stream);
+/* The af_adapter chain with its input computed in the prologue (fusion.py:135-138: fused_af =
+ * CrossAFInteraction(af, af_p), then af_adapter = Linear(D, 4D) -> GELU -> Linear(4D, D) -> Sigmoid):
+ * out bf16 [M, D] from af, af_p f32 [M] in ONE launch (snvrag_af_gate + snvrag_mlp_forward epi2 0).
+ * D = 384.  wstream: snvrag_mlp_pack of (a0, a3); vec (f32) = [b1 4D | b2 D | g2_b D | j_w[:, 0] D |
+ * j_w[:, 1] D | j_b D | ln_w D | ln_b D | g1_w 64 (row-major [32, 2]) | g1_b 32 | m0 m1 mb S00 S11 S01
+ * S0b S1b Sbb] with m the column means of (j_w[:, 0], j_w[:, 1], j_b) and S their centred second
+ * moments (1 / D); gate_frags: the gate GEMV's W2 [D, 32] as 12 tiles x 2 k16 steps x (bf16 hi,
+ * bf16 lo = bf16(W2 - hi)) 1 KiB MFMA fragments, lane l = (m = l % 32, h = l / 32) of fragment
+ * (T, s, part) holding W2[32 T + 16 ((m / 4) % 2) + 4 (m / 8) + m % 4][16 h + 8 s + 0 .. 7]
+ * (src/kernels.py mlp_afgate_pack). */
+int snvrag_mlp_afgate_forward(int64_t M, int D, const float* af, const float* af_p, const void* gate_frags,
+                              float res_scale, const void* wstream, const float* vec, void* out, void* stream);
 size_t snvrag_sgemm_pack_bytes(int D, int N);
 int snvrag_sgemm_pack(int D, int N, const void* w, void* out, void* stream);
 

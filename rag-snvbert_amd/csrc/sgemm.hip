@@ -392,7 +392,13 @@ void sg_kernel(SgArgs p) {
 // order baked into W2's columns at pack time), so phase 2 accumulates all D outputs (12 f32
 // tiles, 192 registers) pair by pair.  Per pair: 48 W1 fragments (the previous pair's epilogue
 // spread between them), then the previous pair's 48 W2 fragments.  4 waves x 32 rows.
-template <int D, bool RANK, int EPI2>
+// AFG: the input x = CrossAFInteraction(af, af_p) (fusion.py:82-86, the af_gate kernel's function)
+// computed in the prologue straight into the B fragments instead of read from memory — the gate
+// GEMV (32 hidden -> D) on MFMAs (split bf16: hi x hi + hi x lo + lo x hi, f32-level products),
+// the joint encoder's LayerNorm from closed-form moments of its 2-input affine map (see
+// af_gate_kernel), so the af_adapter chain is one launch (fusion.py:135-138).
+constexpr int AFG_TAB = 6 * 384 + 64 + 32 + 9;      // [g2_b | j0 | j1 | jb | ln_w | ln_b] D, g1_w, g1_b, moments
+template <int D, bool RANK, int EPI2, bool AFG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mlp_kernel(SgArgs p) {
   constexpr int KS = D / 16, NT = D / 32, F1 = 2 * KS, F2 = 4 * NT, FPP = F1 + F2;
   static_assert(F1 % 16 == 0 && F2 % 16 == 0, "parts are whole slabs");
@@ -409,11 +415,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const long rc = row < p.M ? row : (long)p.M - 1;
   // vector table [b1 H | RANK: c1 H, c2 H | b2 D | LN: g D, be D]
   constexpr int OB2 = H * (RANK ? 3 : 1);
-  const int nvec = OB2 + D * (EPI2 == 1 ? 3 : 1);
+  const int nvec = OB2 + D * (EPI2 == 1 ? 3 : 1) + (AFG ? AFG_TAB : 0);
   for (int i = tid; i < nvec; i += 256) sv[i] = p.vec[i];
   u32x4 xa[KS];
+  if constexpr (AFG) {
+    static_assert(D == 384 && !RANK, "AF-gate prologue: D = 384, no rank terms");
+    __syncthreads();                                 // the vector table (no LDS-DMA in flight yet)
+    const float* tg = sv + OB2 + D * (EPI2 == 1 ? 3 : 1);
+    const float* g1w = tg + 6 * D;
+    const float* g1b = g1w + 64;
+    const float* mo = g1b + 32;                      // m0 m1 mb S00 S11 S01 S0b S1b Sbb
+    const float a0 = p.r1[rc], a1 = p.r2[rc];
+    const float mean = mo[0] * a0 + mo[1] * a1 + mo[2];
+    const float var = a0 * a0 * mo[3] + a1 * a1 * mo[4] + 2.f * (a0 * a1 * mo[5] + a0 * mo[6] + a1 * mo[7]) + mo[8];
+    const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + 1e-5f);
+    // gate hidden units 16 hh + 8 s + j of this lane's row (the B fragments of the gate GEMV, k16
+    // step s), split into bf16 hi + lo
+    u32x4 hb[2], hl[2];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float h[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int u = 16 * hh + 8 * s + 2 * e + t;
+          h[t] = gelu_erf(g1w[u * 2] * a0 + g1w[u * 2 + 1] * a1 + g1b[u]);
+        }
+        const uint32_t w = sg_pack2(h[0], h[1]);
+        hb[s][e] = w;
+        hl[s][e] = sg_pack2(h[0] - __uint_as_float(w << 16), h[1] - __uint_as_float(w & 0xffff0000u));
+      }
+    // W2 fragments (tile T, step s, hi / lo) of the gate GEMV: afgate pack order, 1 KiB each
+    const u32x4* gw = reinterpret_cast<const u32x4*>(p.g2) + lane;
+    const float rs = p.slope;
+#pragma unroll
+    for (int T = 0; T < NT; ++T) {
+      u32x4 w[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) w[s][pt] = gw[((T * 2 + s) * 2 + pt) * 64];
+      f32x16 g = sg_mfma(w[0][0], hb[0], f32x16{});
+      g = sg_mfma(w[0][0], hl[0], g);
+      g = sg_mfma(w[0][1], hb[0], g);
+      g = sg_mfma(w[1][0], hb[1], g);
+      g = sg_mfma(w[1][0], hl[1], g);
+      g = sg_mfma(w[1][1], hb[1], g);
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {                 // feature 32 T + 16 hh + i
+        const int f = 32 * T + 16 * hh + i;
+        const float gt = 1.0f / (1.0f + __expf(-(g[i] + tg[f])));
+        const float enc = tg[D + f] * a0 + tg[2 * D + f] * a1 + tg[3 * D + f];
+        const float e = gelu_erf((enc - mean) * rstd * tg[4 * D + f] + tg[5 * D + f]);
+        v[i] = a0 + rs * (gt * e);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xa[2 * T][k] = sg_pack2(v[2 * k], v[2 * k + 1]);
+        xa[2 * T + 1][k] = sg_pack2(v[8 + 2 * k], v[9 + 2 * k]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) xa[s] = *reinterpret_cast<const u32x4*>(p.x + rc * D + sg_in_feat(s, hh, 0));
+  }
   float r1v = 0.f, r2v = 0.f;
   if constexpr (RANK) {
     const long ri = rc % p.period;
@@ -624,9 +691,9 @@ __global__ void mlp_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w
   }
 }
 
-template <int D, bool RANK, int EPI2>
+template <int D, bool RANK, int EPI2, bool AFG = false>
 static int mlp_launch(const SgArgs& a, hipStream_t s) {
-  auto kern = mlp_kernel<D, RANK, EPI2>;
+  auto kern = mlp_kernel<D, RANK, EPI2, AFG>;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 128)), dim3(256), lds, s, a);
@@ -870,6 +937,26 @@ extern "C" int snvrag_mlp_forward(int64_t M, int D, int epi2, const void* x, con
   evlog_begin(s);
   const int rc = epi2 == 0 ? (rank ? mlp_launch<384, true, 0>(a, s) : mlp_launch<384, false, 0>(a, s))
                            : (rank ? mlp_launch<384, true, 1>(a, s) : mlp_launch<384, false, 1>(a, s));
+  if (rc) return rc;
+  evlog_end(s, EV_GEMM, 2.0 * M * (double)D * 4 * D * 2);
+  return 0;
+}
+
+extern "C" int snvrag_mlp_afgate_forward(int64_t M, int D, const float* af, const float* af_p, const void* gate_frags,
+                                         float res_scale, const void* wstream, const float* vec, void* out,
+                                         void* stream) {
+  SNV_CHECK_ARG(D == 384, "MLP kernel needs D = 384");
+  SNV_CHECK_ARG(af && af_p && gate_frags && wstream && vec && out, "null pointer");
+  SNV_CHECK_ARG(M >= 0 && M < (1L << 31), "bad M");
+  SNV_CHECK_ARG(((uintptr_t)gate_frags % 16) == 0 && ((uintptr_t)wstream % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "pointers must be 16-byte aligned");
+  SNV_CHECK_ARG((4 * D + D + AFG_TAB) * 4 <= SG_VEC_BYTES, "vector table exceeds the LDS budget");
+  if (M == 0) return 0;
+  const SgArgs a{(int)M, D, nullptr, (bf16*)out, (const char*)wstream, vec, af, af_p, (int)M,
+                 nullptr, nullptr, res_scale, 0.f, nullptr, (const bf16*)gate_frags, 0};
+  hipStream_t s = as_stream(stream);
+  evlog_begin(s);
+  const int rc = mlp_launch<384, false, 0, true>(a, s);
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)D * 4 * D * 2);
   return 0;

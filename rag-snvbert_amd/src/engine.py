@@ -7,8 +7,10 @@ of libsnvrag kernels.  Kernel graph (one batch of B samples, 2B haplotypes):
   [rag means supplied by retrieval: rag_mean kernel]               K4 (neighbour histogram mean)
   posfeat ........................................................... conv chain, once per sample
   linear(D->D, rank-2 pos/af epilogue, lrelu, +resid) -> LN        emb_fusion x4 in ONE GEMM
-  af_gate -> linear(D->4D, gelu) -> linear(4D->D, sigmoid)          rag gate, once per sample
-  rag_concat -> linear(2D->4D, gelu) -> linear(4D->D) -> LN+maf tail  rag_fusion x2 in one GEMM
+  [af_gate ->] linear(D->4D, gelu) -> linear(4D->D, sigmoid)        rag gate, once per sample, ONE
+                                                                    launch (mlp_afgate) at bf16 D=384
+  rag_concat -> linear(2D->4D, gelu) -> linear(4D->D) -> LN+maf tail  rag_fusion x2 in one GEMM each
+                                                                    (cat in registers; gemm256_ln)
   encoder_forward (12 blocks, h1 and h2 batched)                    K7-K10
   hap head: linear(rank-2 af/af_p, gelu) -> linear -> LN -> linear(gelu) -> hap_head_out
   gt_head
@@ -64,6 +66,8 @@ class Engine:
     # bf16 at D = 384: the rag fusion's fusion[3] -> LN -> MAF tail on the wide-row GEMM (gemm256
     # EPI 1) instead of the row-panel GEMM's LN epilogue (class-level A/B switch; repack on change)
     rag_tail_wide = True
+    # ... and CrossAFInteraction inside the af_adapter MLP launch (mlp_afgate)
+    rag_afgate_fused = True
 
     def __init__(self, root: nn.Module):
         self.root = root
@@ -187,6 +191,9 @@ class Engine:
             # af_adapter: Linear -> GELU -> Linear -> Sigmoid in one launch, hidden on chip
             P.rf["a_mlp"] = K.mlp_pack(P.rf["a0"], P.rf["a3"])
             P.rf["a_mlp_v"] = K.sgemm_vec(torch.cat([P.rf["a0b"], P.rf["a3b"]]))
+            if self.rag_afgate_fused and P.ag_t[2].shape == (D, 32):
+                # CrossAFInteraction computed in the same launch (no [B, L, D] fused_af round trip)
+                P.rf["afg_frags"], P.rf["afg_v"] = K.mlp_afgate_pack(P.ag_t, P.rf["a_mlp_v"])
         elif sg_ok and P.rf["a0"].shape == (4 * D, D):
             P.rf["a0_sg"], P.rf["a0_v"] = K.sgemm_pack(P.rf["a0"]), K.sgemm_vec(P.rf["a0b"])
         # encoder
@@ -337,10 +344,13 @@ class Engine:
                              row_period=BL, act=N.ACT_LRELU, slope=0.1, resid=hm, ln=(ef["g"], ef["bb"]))
         if rag is not None:
             rf = P.rf
-            fa = K.af_gate(af, af_p, P.ag, D, T)                      # [B, L, D]
-            if "a_mlp" in rf:
+            if "afg_frags" in rf:
+                aw = K.mlp_afgate(af, af_p, rf["afg_frags"], P.ag.res_scale, rf["a_mlp"], rf["afg_v"], D)
+            elif "a_mlp" in rf:
+                fa = K.af_gate(af, af_p, P.ag, D, T)                  # [B, L, D]
                 aw = K.mlp(fa, rf["a_mlp"], rf["a_mlp_v"], epi2=0)
             else:
+                fa = K.af_gate(af, af_p, P.ag, D, T)
                 if "a0_sg" in rf:
                     t = K.sgemm(fa, rf["a0_sg"], rf["a0"].shape[0], rf["a0_v"], act=N.ACT_GELU)
                 else:

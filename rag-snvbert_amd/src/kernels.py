@@ -983,6 +983,50 @@ def mlp(x: torch.Tensor, wstream: torch.Tensor, vec: torch.Tensor, *, epi2: int,
     return out
 
 
+def mlp_afgate_pack(ag_t, mlp_vec: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(gate fragments bf16, vector table f32) of :func:`mlp_afgate` from CrossAFInteraction's
+    weights ``ag_t`` = [gate_net[0].weight [32, 2], .bias, gate_net[2].weight [D, 32], .bias,
+    joint_encoder[0].weight [D, 2], .bias, joint_encoder[1].weight, .bias] (f32) and the af_adapter
+    MLP's table ``mlp_vec`` = [b1 | b2] (include/snvrag.h snvrag_mlp_afgate_forward)."""
+    g1w, g1b, g2w, g2b, jw, jb, lnw, lnb = [t.detach().float() for t in ag_t]
+    D = g2w.shape[0]
+    assert D == 384 and g2w.shape[1] == 32 and g1w.shape == (32, 2) and jw.shape == (D, 2)
+    cols = [jw[:, 0].double(), jw[:, 1].double(), jb.double()]
+    mu = [c.mean() for c in cols]
+    cc = [c - m for c, m in zip(cols, mu)]
+    mom = torch.stack(mu + [(cc[0] * cc[0]).mean(), (cc[1] * cc[1]).mean(), (cc[0] * cc[1]).mean(),
+                            (cc[0] * cc[2]).mean(), (cc[1] * cc[2]).mean(), (cc[2] * cc[2]).mean()]).float()
+    vec = torch.cat([mlp_vec.float().reshape(-1), g2b, jw[:, 0], jw[:, 1], jb, lnw, lnb, g1w.reshape(-1), g1b,
+                     mom.to(g2b.device)]).contiguous()
+    dev = g2w.device
+    m = torch.arange(32, device=dev)
+    outf = 16 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3)
+    T = torch.arange(12, device=dev).view(12, 1, 1, 1)
+    s = torch.arange(2, device=dev).view(1, 2, 1, 1)
+    lane = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, 8)
+    rows = 32 * T + outf[lane % 32]
+    cols = 16 * (lane // 32) + 8 * s + j
+    w = g2w[rows.expand(12, 2, 64, 8), cols.expand(12, 2, 64, 8)]          # [T, s, lane, 8]
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    frags = torch.stack([hi, lo], 2).contiguous()                          # [T, s, part, lane, 8]
+    return frags, vec
+
+
+def mlp_afgate(af: torch.Tensor, af_p: torch.Tensor, frags: torch.Tensor, res_scale: float, wstream: torch.Tensor,
+               vec: torch.Tensor, D: int = 384) -> torch.Tensor:
+    """sigmoid(GELU(x W1^T + b1) W2^T + b2) with x = CrossAFInteraction(af, af_p) computed inside
+    the launch (fusion.py:135-138); [*af.shape, D] bf16."""
+    N.require_gpu(af, af_p)
+    af, af_p = _c(af.float()), _c(af_p.float())
+    assert af.numel() == af_p.numel()
+    out = torch.empty(*af.shape, D, device=af.device, dtype=torch.bfloat16)
+    check(N.lib().snvrag_mlp_afgate_forward(af.numel(), D, ptr(af), ptr(af_p), ptr(frags), res_scale, ptr(wstream),
+                                            ptr(vec), ptr(out), stream_ptr()), "mlp_afgate")
+    return out
+
+
 def sgemm_cat(q: torch.Tensor, x2: torch.Tensor, g2: torch.Tensor, period: int, wstream: torch.Tensor, n_out: int,
               vec: torch.Tensor) -> torch.Tensor:
     """GELU([q | bf16(x2 * g2[m % period])] W^T + b) [..., n_out] (bf16; the rag fusion's

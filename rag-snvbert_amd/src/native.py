@@ -150,6 +150,7 @@ _SIGS = {
     "snvrag_mlp_pack_bytes": ([C.c_int], sz),
     "snvrag_mlp_pack": ([C.c_int, vp, vp, vp, vp], C.c_int),
     "snvrag_mlp_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, i64, f32, vp, vp], C.c_int),
+    "snvrag_mlp_afgate_forward": ([i64, C.c_int, vp, vp, vp, f32, vp, vp, vp, vp], C.c_int),
     "snvrag_sgemm_cat_forward": ([i64, C.c_int, C.c_int, vp, vp, vp, i64, vp, vp, vp, vp], C.c_int),
     "snvrag_sgemm_pack_bytes": ([C.c_int, C.c_int], sz),
     "snvrag_sgemm_pack": ([C.c_int, C.c_int, vp, vp, vp], C.c_int),

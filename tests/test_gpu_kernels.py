@@ -523,6 +523,43 @@ def test_fused_mlp(M, mode):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M", [1030, 77, 1])
+def test_mlp_afgate_vs_fp32_and_two_launch_path(M):
+    """snvrag_mlp_afgate_forward (CrossAFInteraction computed in the af_adapter MLP's prologue:
+    fusion.py:82-86 then :135-138 in one launch) vs torch fp32 of the same chain (the gate input
+    rounded to bf16 where the two-launch path stores it) and vs snvrag_af_gate + snvrag_mlp_forward."""
+    g = torch.Generator(device="cpu").manual_seed(M)
+    D, H = 384, 1536
+    rn = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)
+    ag = [rn(32, 2, sc=0.8), rn(32, sc=0.1), rn(D, 32, sc=0.25), rn(D, sc=0.1), rn(D, 2, sc=0.7), rn(D, sc=0.1),
+          1 + rn(D, sc=0.1), rn(D, sc=0.1)]
+    rs = 0.37
+    af, afp = torch.rand(M, generator=g).to(DEV), torch.rand(M, generator=g).to(DEV)
+    af[:2], afp[:2] = torch.tensor([0.0, 1.0])[:M], torch.tensor([1e-4, 0.5])[:M]
+    w1 = (torch.randn(H, D, generator=g) / math.sqrt(D)).to(DEV, torch.bfloat16)
+    w2 = (torch.randn(D, H, generator=g) / math.sqrt(H)).to(DEV, torch.bfloat16)
+    b1, b2 = rn(H), rn(D, sc=0.1)
+    mv = torch.cat([b1, b2]).contiguous()
+    ws = K().mlp_pack(w1, w2)
+    # torch fp32 reference
+    c = torch.stack([af, afp], -1)
+    gate = torch.sigmoid(torch.nn.functional.gelu(c @ ag[0].t() + ag[1]) @ ag[2].t() + ag[3])
+    enc = torch.nn.functional.gelu(torch.nn.functional.layer_norm(c @ ag[4].t() + ag[5], (D,), ag[6], ag[7], 1e-5))
+    fa = (af[:, None] + rs * gate * enc).to(torch.bfloat16).float()
+    h = torch.nn.functional.gelu(fa @ w1.float().t() + b1).to(torch.bfloat16).float()
+    ref = torch.sigmoid(h @ w2.float().t() + b2)
+    frags, vec = K().mlp_afgate_pack(ag, mv)
+    out = K().mlp_afgate(af, afp, frags, rs, ws, vec)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
+    # the fused gate input against the af_gate kernel's (both bf16): a rare one-ulp rounding flip
+    from src import native as NN
+    w = NN.AfGateW(*[t.contiguous().data_ptr() for t in ag], rs)
+    fa2 = K().af_gate(af, afp, w, D, torch.bfloat16)
+    torch.testing.assert_close(fa2.float(), fa, rtol=1e-2, atol=1e-2)
+    two = K().mlp(fa2.view(M, D), ws, mv, epi2=0)
+    torch.testing.assert_close(out.float(), two.float(), rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("M,period", [(1000, 1000), (2060, 1030), (77, 33)])
 def test_stream_gemm_concatenated_input(M, period):
     """snvrag_sgemm_cat_forward (rag fusion: cat(h, aw * h_rag) -> Linear(2D, 4D) -> GELU, the cat built
