@@ -555,40 +555,40 @@ void g3_kernel(G2Args p) {
     const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.base ? p.base + row0 * p.ld_base : p.out), (short)0,
         (int)(b_bytes < 0x7fffffffL ? b_bytes : 0x7fffffffL), 0x00020000);
+    // (by halves of 8 features: the b / g / be of one half, 24 registers, beside the accumulators)
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      const int f0 = 96 * wave + 32 * t + 16 * hh;
-      u32x4 bv[4], gv[4], ev[4];
-      tile_vec(sb, t, bv);
-      tile_vec(sb + N, t, gv);
-      tile_vec(sb + 2 * N, t, ev);
+    for (int t = 0; t < TW; ++t)
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int rl = 32 * g + n;
-        float y[16];
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int f0 = 96 * wave + 32 * t + 16 * hh + 8 * h2;
+        u32x4 bv[2], gv[2], ev[2];
+        asm volatile(
+            "ds_read_b128 %0, %6 offset:0\n ds_read_b128 %1, %6 offset:16\n ds_read_b128 %2, %7 offset:0\n"
+            " ds_read_b128 %3, %7 offset:16\n ds_read_b128 %4, %8 offset:0\n ds_read_b128 %5, %8 offset:16\n"
+            " s_waitcnt lgkmcnt(0)"
+            : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(gv[0]), "=&v"(gv[1]), "=&v"(ev[0]), "=&v"(ev[1])
+            : "v"(lds_addr(sb) + 4 * f0), "v"(lds_addr(sb + N) + 4 * f0), "v"(lds_addr(sb + 2 * N) + 4 * f0));
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          y[i] = fmaf((acc[g][t][i] + __uint_as_float(bv[i >> 2][i & 3]) - mean[g]) * rstd[g],
-                      __uint_as_float(gv[i >> 2][i & 3]), __uint_as_float(ev[i >> 2][i & 3]));
-        if (p.base) {
+        for (int g = 0; g < G; ++g) {
+          const int rl = 32 * g + n;
+          float y[8];
 #pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(brs, (int)(rl * p.ld_base + f0 + 8 * h2) * 2, 0, 0);
+          for (int i = 0; i < 8; ++i)
+            y[i] = fmaf((acc[g][t][8 * h2 + i] + __uint_as_float(bv[i >> 2][i & 3]) - mean[g]) * rstd[g],
+                        __uint_as_float(gv[i >> 2][i & 3]), __uint_as_float(ev[i >> 2][i & 3]));
+          if (p.base) {
+            const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(brs, (int)(rl * p.ld_base + f0) * 2, 0, 0);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              y[8 * h2 + 2 * e] = __uint_as_float(r[e] << 16) + p.post_scale * (y[8 * h2 + 2 * e] * w[g]);
-              y[8 * h2 + 2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u) + p.post_scale * (y[8 * h2 + 2 * e + 1] * w[g]);
+              y[2 * e] = __uint_as_float(r[e] << 16) + p.post_scale * (y[2 * e] * w[g]);
+              y[2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u) + p.post_scale * (y[2 * e + 1] * w[g]);
             }
           }
-        }
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
           __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{g2_pack2(y[8 * h2], y[8 * h2 + 1]), g2_pack2(y[8 * h2 + 2], y[8 * h2 + 3]),
-                    g2_pack2(y[8 * h2 + 4], y[8 * h2 + 5]), g2_pack2(y[8 * h2 + 6], y[8 * h2 + 7])},
-              ors, (int)(rl * p.ldo + f0 + 8 * h2) * 2, 0, 0);
+              u32x4{g2_pack2(y[0], y[1]), g2_pack2(y[2], y[3]), g2_pack2(y[4], y[5]), g2_pack2(y[6], y[7])},
+              ors, (int)(rl * p.ldo + f0) * 2, 0, 0);
+        }
       }
-    }
     stamp(4, __builtin_amdgcn_s_memtime());
     stamp(5, __builtin_amdgcn_s_memrealtime());
     return;
@@ -797,7 +797,9 @@ extern "C" int snvrag_gemm256_ln_forward(int64_t M, int N, int K, const void* A,
   a.post_af_period = (long)post_af_period;
   hipStream_t s = as_stream(stream);
   evlog_begin(s);
-  const int rc = g3_dispatch<0, 1>(g3_groups(M), a, s);
+  // (at most 7 token groups unless option g2_groups asks for 8: the 8-group LN epilogue spills 36 B)
+  const int G = options().g2_groups == 8 ? 8 : std::min(7, g3_groups(M));
+  const int rc = g3_dispatch<0, 1>(G, a, s);
   if (rc) return rc;
   evlog_end(s, EV_GEMM, 2.0 * M * (double)N * K);
   return 0;

@@ -26,8 +26,14 @@ HOT = [
     ("snvrag::attn_bwd_dkv32", "training attention backward dK/dV"),
     ("snvrag::attn_bwd_dq32", "training attention backward dQ"),
     ("snvrag::sg_kernel<384, 0, 0, false, 8, false>", "QKV stream GEMM"),
-    ("snvrag::mlp_kernel<384, true, 1>", "hap-head fused MLP"),
-    ("snvrag::mlp_kernel<384, false, 0>", "af_adapter fused MLP"),
+    ("snvrag::mlp_kernel<384, true, 1, false>", "hap-head fused MLP"),
+    ("snvrag::mlp_kernel<384, false, 0, true>", "af_adapter fused MLP with the AF gate in its prologue"),
+    ("snvrag::sg_kernel<768, 0, 1, false, 4, true>", "rag fusion cat GEMM"),
+    ("snvrag::g3_kernel<4, 0, 0>", "training wide-row GEMM"),
+    ("snvrag::g3_kernel<7, 0, 0>", "training wide-row GEMM (M = 49 440)"),
+    ("snvrag::g3_kernel<6, 0, 1>", "rag fusion K = 4D projection + LN / MAF tail (bench M)"),
+    ("snvrag::g3_kernel<7, 0, 1>", "rag fusion K = 4D projection + LN / MAF tail"),
+    ("snvrag::tailw_kernel<0>", "wide-row block tail (bench roofline kernel)"),
     ("snvrag::dw_dma_kernel", "training dW"),
     ("snvrag::scan2_kernel<16, 2, 0>", "kNN panel scan"),
     # (bf16 template arguments: c++filt leaves these names mangled)
