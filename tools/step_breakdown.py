@@ -1,8 +1,8 @@
 """Per-kernel breakdown of bench.py's inference step from a rocprofv3 --kernel-trace CSV:
 python tools/step_breakdown.py TRACE.csv [N_STEPS]
 
-A step starts at the kNN's lut_kernel launch that precedes each bf16 af_gate launch (the rag
-gate, once per step); the breakdown covers the last N_STEPS complete steps (start to the next
+A step starts at the kNN's lut_kernel launch that precedes each rag-gate launch (the bf16 af_gate
+kernel, or since r6 the af_adapter MLP with the AF gate in its prologue; once per step); the breakdown covers the last N_STEPS complete steps (start to the next
 step's start), grouped by kernel name, in ms per step, with the span (wall clock between the
 step starts), the kernel-busy sum and the idle remainder."""
 import csv
@@ -12,7 +12,8 @@ from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 n_steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gate = [i for i, r in enumerate(rows) if "af_gate_kernelIDF16b" in r["Kernel_Name"]]
+gate = [i for i, r in enumerate(rows)
+        if "af_gate_kernelIDF16b" in r["Kernel_Name"] or "mlp_kernel<384, false, 0, true>" in r["Kernel_Name"]]
 starts = []
 for g in gate:
     s = max(i for i in range(g) if "lut_kernel" in rows[i]["Kernel_Name"])
