@@ -515,6 +515,9 @@ def train_bench(args, world, rank, dev):
     from src.main.pretrain_with_val_optimized import BERTTrainerWithValidationOptimized
     from src.model import build_model
     Bt, S, nref = 24, args.train_window, 5000
+    # the epoch-0 window masks come from numpy's global RNG (the reference's semantics; its CLI
+    # seeds it first): seeded here so every run and every rank retrieves from the same masks
+    np.random.seed(7)
     ds, vocab = make_rag_dataset(n_samples=Bt * world, n_sites=S, n_windows=1, n_ref_samples=nref, seed=7,
                                  name="train")
     shard = None

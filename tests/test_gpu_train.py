@@ -1367,3 +1367,114 @@ def test_token_table_gradient_vs_onehot_fp64(M, V, D, pad):
         W = torch.randn(V, D, device=DEV, requires_grad=True)
         A.tiny_embedding(tok.to(DEV), W, pad).backward(gy.to(DEV))
         torch.testing.assert_close(W.grad.cpu().double(), want, rtol=1e-5, atol=1e-4)
+
+
+def _configs1_case():
+    """configs[1] at its real shape (train_embedding_rag.py defaults; the bench's training leg):
+    B = 24 samples, a 512-site window (L = 1030 tokens), k = 8 neighbours from a 10 000-haplotype
+    panel, d384 / 12 layers / 12 heads, TRAIN mode with every dropout at p = 0.  Retrieval runs
+    once (the trainer's own process_batch_retrieval); its neighbour means are then held fixed, so
+    the loss is a smooth function of the weights for the finite differences below."""
+    from src.dataset.embedding_rag_dataset import embedding_rag_collate_fn
+    from src.dataset.synthetic import make_rag_dataset
+    from src.model import build_model
+    # (the epoch-0 window masks come from numpy's global RNG, as in the reference — the CLI seeds it
+    # first, train_embedding_rag.py main; unseeded, two processes retrieve different neighbours)
+    st = np.random.get_state()
+    np.random.seed(0)
+    ds, vocab = make_rag_dataset(n_samples=24, n_sites=512, n_windows=1, n_ref_samples=5000, seed=7, name="train")
+    np.random.set_state(st)
+    batch = embedding_rag_collate_fn([ds[i] for i in range(24)])
+    torch.manual_seed(0)
+    m = build_model(len(vocab), 384, 12, 12).to(DEV).train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    data = ds.process_batch_retrieval(dict(batch), m.bert.embedding, DEV, k_retrieve=8)
+    x = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in data.items()}
+    x["rag_emb_h1"], x["rag_emb_h2"] = x["rag_emb_h1"].detach(), x["rag_emb_h2"].detach()
+    return m, x
+
+
+def _configs1_loss(m, x):
+    from src.autograd_ops import focal_loss
+    out = m(x)
+    mk = x["mask"].bool()
+    return (3 * focal_loss(out[0], x["hap_1_label"], mk, 2.0, 1.0) + 3 * focal_loss(out[1], x["hap_2_label"], mk, 2.0, 1.0)
+            + 4 * focal_loss(out[2], x["gt_label"], mk, 2.0, 1.0))
+
+
+def test_train_configs1_shape_directional_derivatives_and_bf16_drift():
+    """configs[1] at full size (the shape the bench's training leg times), checked without a
+    reference run (the reference's autograd at B = 24, L = 1030 needs ~60 GB of host memory for
+    its attention matrices; the fixture-size tests pin it against the reference itself):
+      * exact-f32 mode: the gradient's directional derivative along its own direction, overall and
+        restricted to each layer class, equals the central finite difference of the loss
+        to 1.5e-3 (a wrong gradient — direction or scale — moves the difference quotient off |g|);
+      * the bf16 product path: loss within 1e-3 of f32, every layer class's gradient within a
+        relative error of 0.05 and cosine >= 0.999 of the f32 gradient (measured r6: 1e-4; rel
+        0.8e-3 - 1.3e-2, cos >= 0.99992)."""
+    from src import autograd_ops as AO
+    m, x = _configs1_case()
+    params = [(n, p) for n, p in m.named_parameters() if p.requires_grad]
+    AO.set_train_precision(torch.float32)
+    try:
+        m.zero_grad(set_to_none=True)
+        L0 = _configs1_loss(m, x)
+        L0.backward()
+        g32 = {n: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p)) for n, p in params}
+
+        def loss_at(step, d):
+            with torch.no_grad():
+                for n, p in params:
+                    if n in d:
+                        p.add_(d[n], alpha=step)
+            AO.weights_updated()
+            with torch.no_grad():
+                v = float(_configs1_loss(m, x))
+            with torch.no_grad():
+                for n, p in params:
+                    if n in d:
+                        p.add_(d[n], alpha=-step)
+            AO.weights_updated()
+            return v
+
+        groups = {"all": [n for n, _ in params]}
+        for n, _ in params:
+            groups.setdefault(_v18_layer_class(n), []).append(n)
+        L0v = float(L0.detach())
+        for gname, names in groups.items():
+            gn = math.sqrt(sum(float((g32[n].double() ** 2).sum()) for n in names))
+            if gn < 1e-6 * abs(L0v):
+                continue
+            d = {n: (g32[n] / gn) for n in names}
+            # step: a loss change of 2e-3 relative each way.  Measured (r6, profiles/r6_train_configs1_fd.txt):
+            # the difference quotient converges to |g| as the step shrinks (rel +1.5e-3 / +5e-4 / +2e-4
+            # at 8e-3 / 2e-3 / 5e-4: the curvature term), the loss repeats to 2e-7, so the noise floor
+            # of the quotient is ~4e-4 at 5e-4
+            eps = 2e-3 * abs(L0v) / gn
+            fd = (loss_at(eps, d) - loss_at(-eps, d)) / (2 * eps)
+            print(f"{gname:18s} |g| {gn:.6e}  finite difference {fd:.6e}  rel {(fd - gn) / gn:+.2e}")
+            assert abs(fd - gn) <= 1.5e-3 * gn, (gname, fd, gn)
+    finally:
+        AO.set_train_precision(torch.bfloat16)
+    m.zero_grad(set_to_none=True)
+    AO.weights_updated()
+    L16 = _configs1_loss(m, x)
+    L16.backward()
+    print(f"loss f32 {L0v:.4f} bf16 {float(L16.detach()):.4f}")
+    assert abs(float(L16.detach()) - L0v) <= 1e-3 * abs(L0v)
+    num, den, dot, n16 = {}, {}, {}, {}
+    for n, p in params:
+        c = _v18_layer_class(n)
+        a = g32[n].double()
+        b = p.grad.detach().double() if p.grad is not None else torch.zeros_like(a)
+        num[c] = num.get(c, 0.0) + float(((b - a) ** 2).sum())
+        den[c] = den.get(c, 0.0) + float((a ** 2).sum())
+        dot[c] = dot.get(c, 0.0) + float((a * b).sum())
+        n16[c] = n16.get(c, 0.0) + float((b ** 2).sum())
+    for c in sorted(num):
+        rel = math.sqrt(num[c] / max(den[c], 1e-30))
+        cos = dot[c] / math.sqrt(max(den[c] * n16[c], 1e-30))
+        print(f"bf16 vs f32 {c:18s} rel {rel:.3e} cos {cos:.6f}")
+        assert rel <= 0.05 and cos >= 0.999, (c, rel, cos)
