@@ -51,3 +51,35 @@ if os.environ.get("STACKS"):
     for e in rows[:40]:
         st = " <- ".join(s.split("/")[-1] for s in e.stack[:6]) or "(no Python stack: autograd engine)"
         print(f"{e.device_time_total / 1e3:7.3f} ms {e.count:4d}  {e.key:16s} {str(e.input_shapes)[:60]} {st[:260]}")
+
+if os.environ.get("PARENTS"):
+    # glue ops attributed to the autograd node (or forward op) that issued them: the nearest CPU
+    # ancestor that is an autograd evaluate_function / custom Function backward / top-level op
+    import collections
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof3:
+        tr.train_step(dict(batch))
+        torch.cuda.synchronize()
+    want = ("aten::cat", "aten::zeros", "aten::copy_", "aten::add_", "aten::add", "aten::_to_copy", "aten::clone",
+            "aten::fill_", "aten::zero_", "aten::mul", "aten::sum", "aten::slice_backward", "aten::gelu",
+            "aten::gelu_backward", "aten::index_put_", "aten::where", "aten::mean")
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for e in prof3.events():
+        if e.name not in want:
+            continue
+        # only top-level glue (not a copy_ inside _to_copy etc.)
+        if e.cpu_parent is not None and e.cpu_parent.name in want:
+            continue
+        p, anc = e.cpu_parent, "(top level)"
+        while p is not None:
+            if p.name.startswith("autograd::engine::evaluate_function") or "Backward" in p.name or \
+                    p.name.startswith("_Hip") or p.name.startswith("_Nbr"):
+                anc = p.name.replace("autograd::engine::evaluate_function: ", "")
+                break
+            p = p.cpu_parent
+        shp = str(e.input_shapes)[:70] if e.input_shapes else ""
+        key = (e.name, anc, shp)
+        agg[key][0] += getattr(e, "device_time_total", 0.0)
+        agg[key][1] += 1
+    print("\nGlue ops by issuing autograd node (one step: device ms, calls)")
+    for (n, a, s), (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
+        print(f"{t / 1e3:7.3f} ms {c:4d}  {n:22s} {a[:40]:40s} {s}")
