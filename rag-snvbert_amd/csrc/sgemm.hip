@@ -413,6 +413,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int ln = lane & 31, hh = lane >> 5;
   const long row = (long)blockIdx.x * 128 + wave * 32 + ln;
   const long rc = row < p.M ? row : (long)p.M - 1;
+  // first-round stagger (sg_kernel's): later rounds' activation loads and stores spread out
+  if (p.desync > 0 && blockIdx.x < 256) {
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
   // vector table [b1 H | RANK: c1 H, c2 H | b2 D | LN: g D, be D]
   constexpr int OB2 = H * (RANK ? 3 : 1);
   const int nvec = OB2 + D * (EPI2 == 1 ? 3 : 1) + (AFG ? AFG_TAB : 0);
@@ -692,8 +698,13 @@ __global__ void mlp_pack_kernel(int D, long n_pieces, const bf16* __restrict__ w
 }
 
 template <int D, bool RANK, int EPI2, bool AFG = false>
-static int mlp_launch(const SgArgs& a, hipStream_t s) {
+static int mlp_launch(SgArgs a, hipStream_t s) {
   auto kern = mlp_kernel<D, RANK, EPI2, AFG>;
+  // first-round stagger (r6, tools/sg4_desync_sweep.py OPT=mlp_desync at the bench shapes): the
+  // AF-gate form, whose prologue computes its input, 25 k cycles (0.83 vs 0.89 ms); the others 5 k
+  // (af_fusion: 1.465 vs 1.489 ms)
+  const int64_t dz = options().mlp_desync;
+  a.desync = cdiv(a.M, 128) >= 4 * 256 ? (dz >= 0 ? (int)dz : (AFG ? 25000 : 5000)) : 0;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.M, 128)), dim3(256), lds, s, a);
@@ -776,8 +787,12 @@ static int sg_launch(SgArgs a, hipStream_t s) {
   // first-round phase step (tail.hip's de-synchronised rounds): 10 k cycles for the 8-wave
   // projections (QKV at M = 527 360: 0.559 -> 0.540 ms; 20 k / 30 k: 0.557 / 0.584,
   // tools/proj_micro.py); SNVRAG_SG_DESYNC overrides
+  // 4-wave launches (r6, tools/sg4_desync_sweep.py): the LayerNorm form (emb_fusion: whole-tile
+  // prologue and epilogue bursts) 5.5 k — 0.675 vs 0.772 ms; the others 10 k (cat GEMM 1.626 vs
+  // 1.638, head 0.916 vs 0.920)
   const int64_t dz = options().sg_desync;
-  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256 ? (dz >= 0 ? (int)dz : (WAVES == 8 ? 10000 : 0)) : 0;
+  a.desync = cdiv(a.M, 32 * WAVES) >= 4 * 256
+                 ? (dz >= 0 ? (int)dz : (WAVES == 8 ? 10000 : EPI == SG_LN ? 5500 : 10000)) : 0;
   const size_t lds = (size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES;
   static_assert((size_t)SG_NSLOT * SG_SLAB + SG_VEC_BYTES <= 160 * 1024, "LDS budget");
   SNV_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

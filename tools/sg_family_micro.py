@@ -67,10 +67,11 @@ cases = [
     ("af_fusion MLP", lambda: K.mlp(x2, ml_s, ml_v, epi2=1, rank=(af, afp, BL)), 4.0 * M2 * D * H),
     ("AF-gate MLP", lambda: K.mlp_afgate(af, afp, afg_f, 0.1, ml_s, afg_v), 4.0 * BL * D * H),
 ]
-print(f"library {N.LIB_PATH}", flush=True)
-tot = 0.0
-for name, fn, fl in cases:
-    t = timeit(fn)
-    tot += t
-    print(f"{name:18s} {t:.4f} ms  {fl / t / 1e9 / 2500:.3f} of 2.5 PF", flush=True)
-print(f"sum (QKV x12 counted once) {tot:.4f} ms", flush=True)
+if __name__ == "__main__":
+    print(f"library {N.LIB_PATH}", flush=True)
+    tot = 0.0
+    for name, fn, fl in cases:
+        t = timeit(fn)
+        tot += t
+        print(f"{name:18s} {t:.4f} ms  {fl / t / 1e9 / 2500:.3f} of 2.5 PF", flush=True)
+    print(f"sum (QKV x12 counted once) {tot:.4f} ms", flush=True)
