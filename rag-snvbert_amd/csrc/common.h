@@ -67,6 +67,7 @@ struct Options {
   int64_t tail_desync;     // block-tail first-round stagger in cycles, -1 = auto
   int64_t sg_desync;       // stream-GEMM first-round stagger in cycles, -1 = auto
   int64_t mlp_desync;      // MLP kernel first-round stagger in cycles, -1 = auto
+  int64_t g2_desync;       // wide-row GEMM first-round stagger in cycles, -1 = auto
   int64_t sg_waves4;       // 1: 4-wave stream GEMM for the rank-free projections (A/B)
   int64_t ln_bwd_nopf;     // 1: LayerNorm backward without the next-row prefetch (A/B)
   int64_t attn_variant;    // inference attention (dh 32) A/B variant, 0 = default (attention.hip tile)

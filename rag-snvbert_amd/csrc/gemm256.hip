@@ -94,6 +94,7 @@ struct G2Args {
   float post_scale;
   const float* post_af;      // [period] or null: w = min(log1p(1 / (min(af, 1 - af) + 1e-6)), 3)
   long post_af_period;
+  int desync;                // g3: > 0, first-round stagger step in cycles (multi-round launches)
 };
 
 __device__ __forceinline__ float g2_maf_w(float af) {   // fusion.py:155-160
@@ -359,6 +360,11 @@ void g3_kernel(G2Args p) {
     if constexpr (VAR == 3)
       if ((threadIdx.x & 63) == 0) p.stamps[((long)blockIdx.x * 4 + wave) * 8 + i] = v;
   };
+  if (p.desync > 0 && blockIdx.x < 256) {             // first-round stagger (sg_kernel's)
+    const long wait = (long)p.desync * ((blockIdx.x >> 3) & 7);
+    const long t0 = (long)__builtin_amdgcn_s_memtime();
+    while ((long)__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(16);
+  }
   stamp(0, __builtin_amdgcn_s_memtime());
   stamp(1, __builtin_amdgcn_s_memrealtime());
   const long row0 = (long)blockIdx.x * (32 * G);
@@ -639,8 +645,12 @@ void g3_kernel(G2Args p) {
 }
 
 template <int G, int VAR, int EPI = 0>
-static int g3_launch(const G2Args& a, hipStream_t s) {
+static int g3_launch(G2Args a, hipStream_t s) {
   auto kern = g3_kernel<G, VAR, EPI>;
+  // first-round stagger for multi-round launches (r6, tools/g3_desync_sweep.py, the rag fusion's
+  // K = 4D projection at M = 527 360: 10 k cycles 0.929 vs 0.961 ms; training's one-round launches none)
+  const int64_t dz = options().g2_desync;
+  a.desync = cdiv(a.M, 32 * G) >= 4 * 256 ? (dz >= 0 ? (int)dz : 10000) : 0;
   // + bias table (+ EPI 1: LN g, be tables and the [4][G][32] row-sum exchange)
   constexpr size_t lds = (size_t)G3_NS * g3_img(G) + 384 * 4 + (EPI == 1 ? 2 * 384 * 4 + 4 * G * 32 * 4 : 0);
   static_assert(lds <= 160 * 1024, "LDS budget");

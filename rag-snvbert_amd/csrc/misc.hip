@@ -99,7 +99,7 @@ const OptDesc kOpts[] = {
     {"scan_nt", &Options::scan_nt, -1},            {"unfused_ln", &Options::unfused_ln, 0},
     {"encoder_chunk", &Options::encoder_chunk, 0}, {"gemm_tile128", &Options::gemm_tile128, 0},
     {"gemm_nw", &Options::gemm_nw, 0},             {"tail_variant", &Options::tail_variant, 0},
-    {"tail_desync", &Options::tail_desync, -1},    {"sg_desync", &Options::sg_desync, -1},      {"mlp_desync", &Options::mlp_desync, -1},
+    {"tail_desync", &Options::tail_desync, -1},    {"sg_desync", &Options::sg_desync, -1},      {"mlp_desync", &Options::mlp_desync, -1},      {"g2_desync", &Options::g2_desync, -1},
     {"sg_waves4", &Options::sg_waves4, 0},         {"ln_bwd_nopf", &Options::ln_bwd_nopf, 0},
     {"attn_variant", &Options::attn_variant, 0},   {"dw_xcd", &Options::dw_xcd, 1},
     {"ln_rows1", &Options::ln_rows1, 0},           {"tail_persist", &Options::tail_persist, 0},
