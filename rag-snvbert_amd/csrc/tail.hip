@@ -1194,9 +1194,10 @@ static int launch_tail(TailArgs a, hipStream_t s) {
       const long nwg = cdiv(a.M, TL_ROWS);
       const int64_t dz = options().tail_desync;
       // (first-round stagger 10 k cycles: tools/tailw_desync.py, two boxes: 1.409 / 1.403 ms vs
-      // 1.454 / 1.399 at tail_kernel's 25 k and 1.444 without; r6, the shorter prologue:
-      // 4 k — 1.315 vs 1.328 ms median at 10 k, tools/tailw_desync_sweep.py)
-      const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 4000) : 0;
+      // 1.454 / 1.399 at tail_kernel's 25 k and 1.444 without; r6: 4 k was 1 % faster alone
+      // (tools/tailw_desync_sweep.py) but 0.7 % slower inside the bench step, 1.363 vs 1.353 ms,
+      // profiles/r6_tail_desync_bench_ab.txt — 10 k kept)
+      const int desync = nwg >= 8 * 256 ? (dz >= 0 ? (int)dz : 10000) : 0;
       return tailw_launch(a.M, a.act, a.resid, a.out, a.ws, a.vec, a.b_o, a.g1, a.be1, a.eps, desync,
                           (int)options().tail_wide >= 2 ? (int)options().tail_wide - 1 : 0, s);
     }
